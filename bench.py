@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node CIFAR-10 CNN training throughput (images/sec) on MI355X.
+
+Metric/config from BASELINE.json: "images/sec (whole node) CIFAR-10 CNN training at 1/2/4/8
+MI355X"; model = the reference CNN (/root/reference/cifar10cnn.py:94-147, 24x24 center crop of
+32x32x3 inputs), bf16 compute with fp32 master weights, per-GPU batch 256 (global 256*N), synthetic
+uint8 images + random labels (no network), random-init weights.  Weak scaling: per-GPU work fixed.
+
+Every timed step is a complete training step: gather/crop, forward, loss, backward, gradient
+all-reduce (N>1, RCCL), SGD update with the on-device LR schedule.
+
+  python bench.py --gpus N --steps K --warmup W
+  torchrun --nproc-per-node N bench.py --gpus N ...     (the driver's launch for N > 1)
+  python bench.py --impl eager                          (framework-default PyTorch eager line)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+import dmlc  # noqa: E402,F401
+from dmlc.parallel import dist as D  # noqa: E402
+
+BASELINE_VALUE = None   # the reference publishes no number
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--impl", choices=["fused", "eager"], default="fused")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--dataset-size", type=int, default=50000)
+    return ap.parse_args()
+
+
+def make_data(n, device, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    data = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, generator=g)
+    return data.to(device), labels.to(device)
+
+
+def build_fused(args, info, data, labels):
+    from dmlc.engine.fused import FusedCifarEngine
+    eng = FusedCifarEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
+                           rank=info.rank, seed=0, comm_dtype=args.comm_dtype)
+    step = eng.step
+    return eng, step, (None if args.no_graph else eng.capture)
+
+
+def build_eager(args, info, data, labels):
+    from dmlc.engine.eager import EagerTrainer
+    tr = EagerTrainer("cifar_cnn", args.batch, data, labels, device=info.device, world_size=info.world_size,
+                      rank=info.rank, dtype="bf16")
+    return tr, tr.step, None
+
+
+def main():
+    args = parse()
+    info = D.init(D.env_info(), device="auto")
+    if info.world_size != args.gpus and info.rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
+    data, labels = make_data(args.dataset_size, info.device)
+    builder = build_fused if args.impl == "fused" else build_eager
+    eng, step, capture = builder(args, info, data, labels)
+
+    for _ in range(max(1, min(3, args.warmup))):     # eager warm-up before capture
+        step()
+    if capture is not None:
+        capture()
+    for _ in range(max(0, args.warmup - 3)):
+        step()
+    torch.cuda.synchronize()
+    D.barrier(info)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    D.barrier(info)
+    torch.cuda.synchronize()
+    elapsed = D.all_max(time.perf_counter() - t0, info)
+
+    n = info.world_size
+    ms = elapsed * 1000.0 / args.steps
+    gbatch = args.batch * n
+    value = gbatch * args.steps / elapsed
+    if info.rank == 0:
+        line = {
+            "metric": "images/sec (whole node) CIFAR-10 CNN training",
+            "value": round(value, 1),
+            "unit": "images/sec",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
+            "dtype": "bf16",
+            "data": "synthetic uint8 32x32x3 (50k images, device resident), random labels, random-init weights",
+            "config": {
+                "model": "cifar10_cnn (conv5x5-64, pool, conv5x5-64, pool, fc384, fc192, fc10; 24x24 center crop)",
+                "global_batch": gbatch,
+                "per_gpu_batch": args.batch,
+                "seq_len": None,
+                "parallelism": f"dp{n}",
+                "impl": args.impl + ("" if args.impl != "fused" or args.no_graph else "+hipgraph"),
+                "comm_dtype": args.comm_dtype,
+            },
+        }
+        print(json.dumps(line), flush=True)
+    D.shutdown(info)
+
+
+if __name__ == "__main__":
+    main()

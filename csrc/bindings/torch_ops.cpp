@@ -1,0 +1,320 @@
+// torch.ops.dmlc.* bindings of the HIP CNN kernels (csrc/kernels/*.hip).
+//
+// Every op validates device, dtype, contiguity and the exact shapes the kernel's indexing and grid
+// assume BEFORE launching (a mis-shaped launch on MI355X can fault the GPU), then launches on the
+// current HIP stream, so the ops compose with torch streams and are capturable into HIP graphs.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <vector>
+
+#include "../kernels/api.h"
+
+namespace {
+
+using at::Tensor;
+
+#define CHECK_HIP(expr)                                                                       \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    TORCH_CHECK(_e == hipSuccess, "dmlc HIP launch failed: ", hipGetErrorString(_e));         \
+  } while (0)
+
+void dev(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda(), n, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), n, " must be contiguous");
+}
+void check(const Tensor& t, const char* n, at::ScalarType st, std::vector<int64_t> shape) {
+  dev(t, n);
+  TORCH_CHECK(t.scalar_type() == st, n, " has dtype ", t.scalar_type(), ", expected ", st);
+  TORCH_CHECK(t.sizes().vec() == shape, n, " has shape ", t.sizes(), ", expected ", at::IntArrayRef(shape));
+}
+void check_numel(const Tensor& t, const char* n, at::ScalarType st, int64_t numel) {
+  dev(t, n);
+  TORCH_CHECK(t.scalar_type() == st, n, " has dtype ", t.scalar_type(), ", expected ", st);
+  TORCH_CHECK(t.numel() == numel, n, " has ", t.numel(), " elements, expected ", numel);
+}
+void check_min(const Tensor& t, const char* n, at::ScalarType st, int64_t numel) {
+  dev(t, n);
+  TORCH_CHECK(t.scalar_type() == st, n, " has dtype ", t.scalar_type(), ", expected ", st);
+  TORCH_CHECK(t.numel() >= numel, n, " has ", t.numel(), " elements, need at least ", numel);
+}
+
+DmlcIndexSrc index_src(const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t B) {
+  TORCH_CHECK(period >= 1, "period must be >= 1");
+  check_numel(idx, "idx", at::kInt, period * B);
+  DmlcIndexSrc s;
+  s.idx_base = idx.data_ptr<int>();
+  s.counter = nullptr;
+  if (counter.has_value()) {
+    check_numel(*counter, "counter", at::kLong, 1);
+    s.counter = counter->data_ptr<int64_t>();
+  }
+  s.period = (int)period;
+  return s;
+}
+
+hipStream_t stream_of(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_data(const Tensor& data) {
+  dev(data, "data");
+  TORCH_CHECK(data.scalar_type() == at::kByte && data.dim() == 4 && data.size(1) == 32 && data.size(2) == 32 &&
+                  data.size(3) == 3,
+              "data must be uint8 [N,32,32,3], got ", data.sizes());
+}
+
+void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
+               int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& out, const Tensor& am) {
+  const int64_t B = out.size(0);
+  check_data(data);
+  TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
+  check(w1f, "w1f", at::kBFloat16, {64, 160});
+  check_numel(b1, "b1", at::kFloat, 64);
+  check(out, "out", at::kBFloat16, {B, 12, 12, 64});
+  check(am, "am", at::kByte, {B, 12, 12, 64});
+  c10::hip::HIPGuard guard(out.device());
+  DmlcConv1FwdArgs a;
+  a.data = data.data_ptr<uint8_t>();
+  a.src = index_src(idx, counter, period, B);
+  a.B = (int)B; a.cy = (int)cy; a.cx = (int)cx;
+  a.w = w1f.data_ptr(); a.bias = b1.data_ptr<float>();
+  a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>();
+  CHECK_HIP(dmlc_conv1_fwd(&a, stream_of(out)));
+}
+
+void conv2_fwd(const Tensor& in, const Tensor& w2f, const Tensor& b2, const Tensor& out, const Tensor& am) {
+  const int64_t B = in.size(0);
+  check(in, "in", at::kBFloat16, {B, 12, 12, 64});
+  check(w2f, "w2f", at::kBFloat16, {64, 1600});
+  check_numel(b2, "b2", at::kFloat, 64);
+  check(out, "out", at::kBFloat16, {B, 6, 6, 64});
+  check(am, "am", at::kByte, {B, 6, 6, 64});
+  c10::hip::HIPGuard guard(in.device());
+  DmlcConv2FwdArgs a;
+  a.in = in.data_ptr(); a.w = w2f.data_ptr(); a.bias = b2.data_ptr<float>();
+  a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>(); a.B = (int)B;
+  CHECK_HIP(dmlc_conv2_fwd(&a, stream_of(in)));
+}
+
+void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const Tensor& dp1, const Tensor& dy2,
+                 const Tensor& dbias_part) {
+  const int64_t B = dp2.size(0);
+  check(dp2, "dp2", at::kBFloat16, {B, 6, 6, 64});
+  check(am2, "am2", at::kByte, {B, 6, 6, 64});
+  check(w2d, "w2d", at::kBFloat16, {64, 1600});
+  check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
+  check(dbias_part, "dbias_part", at::kFloat, {B, 64});
+  c10::hip::HIPGuard guard(dp2.device());
+  DmlcConv2DgradArgs a;
+  a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
+  a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.dbias_part = dbias_part.data_ptr<float>(); a.B = (int)B;
+  CHECK_HIP(dmlc_conv2_dgrad(&a, stream_of(dp2)));
+}
+
+void conv_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& data, const Tensor& idx,
+                const c10::optional<Tensor>& counter, int64_t period, int64_t cy, int64_t cx, const Tensor& dp1,
+                const Tensor& am1, const Tensor& part1, const Tensor& partb1) {
+  const int64_t B = p1.size(0);
+  check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
+  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
+  const int64_t g2 = part2.size(0), g1 = part1.size(0);
+  TORCH_CHECK(g2 >= 1 && g2 <= B && g1 >= 1 && g1 <= B, "split-K groups must be in [1,B]");
+  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+  check_data(data);
+  TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
+  check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+  check(am1, "am1", at::kByte, {B, 12, 12, 64});
+  check(part1, "part1", at::kFloat, {g1, 160, 64});
+  check(partb1, "partb1", at::kFloat, {g1, 64});
+  c10::hip::HIPGuard guard(p1.device());
+  DmlcConvWgradArgs a;
+  a.p1 = p1.data_ptr(); a.dy2 = dy2.data_ptr(); a.part2 = part2.data_ptr<float>(); a.g2 = (int)g2;
+  a.data = data.data_ptr<uint8_t>(); a.src = index_src(idx, counter, period, B);
+  a.cy = (int)cy; a.cx = (int)cx;
+  a.dp1 = dp1.data_ptr(); a.am1 = am1.data_ptr<uint8_t>();
+  a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1; a.B = (int)B;
+  CHECK_HIP(dmlc_conv_wgrad(&a, stream_of(p1)));
+}
+
+// params per problem (12 ints): M, N, K, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit, relu, nvalid
+void gemm_grouped(at::TensorList A, at::TensorList Bm, at::TensorList C, const c10::List<c10::optional<Tensor>>& bias,
+                  at::IntArrayRef params) {
+  const int n = (int)A.size();
+  TORCH_CHECK(n >= 1 && n <= DMLC_MAX_GEMM, "1..8 problems per group");
+  TORCH_CHECK((int)Bm.size() == n && (int)C.size() == n && (int)bias.size() == n, "list lengths differ");
+  TORCH_CHECK((int)params.size() == 12 * n, "params must hold 12 ints per problem");
+  DmlcGemmGroup G;
+  memset(&G, 0, sizeof(G));
+  G.nprob = n;
+  for (int i = 0; i < n; ++i) {
+    const int64_t* q = params.data() + 12 * i;
+    DmlcGemmProblem& P = G.p[i];
+    P.M = (int)q[0]; P.N = (int)q[1]; P.K = (int)q[2];
+    P.lda = (int)q[3]; P.a_kmajor = (int)q[4]; P.ldb = (int)q[5]; P.b_kmajor = (int)q[6];
+    P.ldc = (int)q[7]; P.c_mode = (int)q[8]; P.ksplit = (int)q[9]; P.relu = (int)q[10]; P.nvalid = (int)q[11];
+    TORCH_CHECK(P.M > 0 && P.K > 0 && P.M % 8 == 0 && P.K % 8 == 0, "gemm ", i, ": M,K must be positive multiples of 8");
+    TORCH_CHECK(P.lda % 8 == 0, "gemm ", i, ": lda must be a multiple of 8 (16-byte rows)");
+    check_min(A[i], "A", at::kBFloat16, P.a_kmajor ? (int64_t)(P.M - 1) * P.lda + P.K : (int64_t)(P.K - 1) * P.lda + P.M);
+    TORCH_CHECK(P.a_kmajor ? P.lda >= P.K : P.lda >= P.M, "gemm ", i, ": lda too small");
+    if (P.c_mode == 3) {
+      TORCH_CHECK(P.a_kmajor == 0, "gemm ", i, ": column sums need an m-major A");
+      check_min(C[i], "C", at::kFloat, std::min(P.M, P.nvalid));
+      P.ksplit = 1;
+      continue;
+    }
+    TORCH_CHECK(P.N > 0 && P.N % 8 == 0, "gemm ", i, ": N must be a positive multiple of 8");
+    TORCH_CHECK(P.ldb % 8 == 0, "gemm ", i, ": ldb must be a multiple of 8");
+    TORCH_CHECK(P.b_kmajor ? P.ldb >= P.K : P.ldb >= P.N, "gemm ", i, ": ldb too small");
+    check_min(Bm[i], "B", at::kBFloat16, P.b_kmajor ? (int64_t)(P.N - 1) * P.ldb + P.K : (int64_t)(P.K - 1) * P.ldb + P.N);
+    TORCH_CHECK(P.ksplit >= 1 && (P.ksplit == 1 || P.c_mode == 2), "gemm ", i, ": split-K needs c_mode 2");
+    TORCH_CHECK(P.nvalid >= 1 && P.nvalid <= P.N && P.ldc >= P.nvalid, "gemm ", i, ": bad nvalid/ldc");
+    const int64_t cneed = (int64_t)(P.c_mode == 2 ? P.ksplit : 1) * P.M * P.ldc;
+    check_min(C[i], "C", P.c_mode == 1 ? at::kBFloat16 : at::kFloat, cneed);
+    P.A = A[i].data_ptr(); P.B = Bm[i].data_ptr(); P.C = C[i].data_ptr();
+    P.bias = nullptr;
+    const c10::optional<Tensor> bo = bias.get(i);
+    if (bo.has_value()) {
+      check_min(*bo, "bias", at::kFloat, P.nvalid);
+      P.bias = bo->data_ptr<float>();
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    if (G.p[i].c_mode == 3) { G.p[i].A = A[i].data_ptr(); G.p[i].C = C[i].data_ptr(); G.p[i].bias = nullptr; }
+  }
+  c10::hip::HIPGuard guard(A[0].device());
+  CHECK_HIP(dmlc_gemm_grouped(&G, stream_of(A[0])));
+}
+
+void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tensor& b2, const Tensor& w3t,
+          const Tensor& b3, const Tensor& w3d, const Tensor& w2d, const Tensor& labels, const Tensor& idx,
+          const c10::optional<Tensor>& counter, int64_t period, double inv_batch, bool relu_logits, bool train,
+          const Tensor& h1, const Tensor& h2, const Tensor& dl, const Tensor& dh1, const Tensor& dh2,
+          const Tensor& loss_part, const Tensor& correct_part, const c10::optional<Tensor>& logits_out) {
+  TORCH_CHECK(h1part.dim() == 3 && h1part.size(2) == 384, "h1part must be [nsplit,B,384]");
+  const int64_t nsplit = h1part.size(0), B = h1part.size(1);
+  TORCH_CHECK(B % 16 == 0 && B > 0, "head: batch must be a positive multiple of 16");
+  check(h1part, "h1part", at::kFloat, {nsplit, B, 384});
+  check_numel(b1, "b1", at::kFloat, 384);
+  check(w2t, "w2t", at::kBFloat16, {192, 384});
+  check_numel(b2, "b2", at::kFloat, 192);
+  check(w3t, "w3t", at::kBFloat16, {16, 192});
+  check_numel(b3, "b3", at::kFloat, 10);
+  check(w3d, "w3d", at::kBFloat16, {192, 32});
+  check(w2d, "w2d", at::kBFloat16, {384, 192});
+  dev(labels, "labels");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.dim() == 1, "labels must be int32 [N]");
+  check(loss_part, "loss_part", at::kFloat, {B / 16});
+  check(correct_part, "correct_part", at::kInt, {B / 16});
+  if (train) {
+    check(h1, "h1", at::kBFloat16, {B, 384});
+    check(h2, "h2", at::kBFloat16, {B, 192});
+    check(dl, "dl", at::kBFloat16, {B, 16});
+    check(dh1, "dh1", at::kBFloat16, {B, 384});
+    check(dh2, "dh2", at::kBFloat16, {B, 192});
+  }
+  c10::hip::HIPGuard guard(h1part.device());
+  DmlcHeadArgs a;
+  a.h1part = h1part.data_ptr<float>(); a.nsplit = (int)nsplit;
+  a.b1 = b1.data_ptr<float>(); a.w2t = w2t.data_ptr(); a.b2 = b2.data_ptr<float>();
+  a.w3t = w3t.data_ptr(); a.b3 = b3.data_ptr<float>(); a.w3d = w3d.data_ptr(); a.w2d = w2d.data_ptr();
+  a.labels = labels.data_ptr<int>(); a.src = index_src(idx, counter, period, B);
+  a.B = (int)B; a.inv_batch = (float)inv_batch; a.relu_logits = relu_logits; a.train = train;
+  a.h1 = train ? h1.data_ptr() : nullptr; a.h2 = train ? h2.data_ptr() : nullptr; a.dl = train ? dl.data_ptr() : nullptr;
+  a.dh1 = train ? dh1.data_ptr() : nullptr; a.dh2 = train ? dh2.data_ptr() : nullptr;
+  a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
+  a.logits_out = nullptr;
+  if (logits_out.has_value()) {
+    check(*logits_out, "logits_out", at::kFloat, {B, 10});
+    a.logits_out = logits_out->data_ptr<float>();
+  }
+  CHECK_HIP(dmlc_head(&a, stream_of(h1part)));
+}
+
+void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_scale, at::IntArrayRef off,
+         const Tensor& part1, const Tensor& partb1, const Tensor& part2, const Tensor& partb2, const Tensor& w1f,
+         const Tensor& w2f, const Tensor& w2d, const Tensor& fc1n, const Tensor& fc2t, const Tensor& fc2n,
+         const Tensor& fc3t, const Tensor& fc3d, const Tensor& step, double lr0, double decay, double decay_steps,
+         bool staircase, const Tensor& ticket, const Tensor& loss_part, const Tensor& correct_part,
+         const Tensor& stats) {
+  TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
+  TORCH_CHECK(off.size() == 10, "off must have 10 entries");
+  static const int64_t numel[10] = {4800, 64, 102400, 64, 884736, 384, 73728, 192, 1920, 10};
+  for (int i = 0; i < 10; ++i) {
+    TORCH_CHECK(off[i] >= 0 && (i == 0 || off[i] >= off[i - 1] + numel[i - 1]), "bad param offsets");
+  }
+  const int64_t end = off[9] + 10;
+  check_min(master, "master", at::kFloat, end);
+  check_min(grad, "grad", at::kFloat, end);
+  const int64_t g1 = part1.size(0), g2 = part2.size(0), B = partb2.size(0);
+  check(part1, "part1", at::kFloat, {g1, 160, 64});
+  check(partb1, "partb1", at::kFloat, {g1, 64});
+  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+  check(partb2, "partb2", at::kFloat, {B, 64});
+  check(w1f, "w1f", at::kBFloat16, {64, 160});
+  check(w2f, "w2f", at::kBFloat16, {64, 1600});
+  check(w2d, "w2d", at::kBFloat16, {64, 1600});
+  check(fc1n, "fc1n", at::kBFloat16, {2304, 384});
+  check(fc2t, "fc2t", at::kBFloat16, {192, 384});
+  check(fc2n, "fc2n", at::kBFloat16, {384, 192});
+  check(fc3t, "fc3t", at::kBFloat16, {16, 192});
+  check(fc3d, "fc3d", at::kBFloat16, {192, 32});
+  check_numel(step, "step", at::kLong, 1);
+  check_numel(ticket, "ticket", at::kInt, 1);
+  dev(loss_part, "loss_part"); dev(correct_part, "correct_part");
+  TORCH_CHECK(loss_part.scalar_type() == at::kFloat && correct_part.scalar_type() == at::kInt &&
+                  loss_part.numel() == correct_part.numel(), "loss/correct partials mismatch");
+  dev(stats, "stats");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(1) == 4, "stats must be [R,4] fp32");
+  c10::hip::HIPGuard guard(master.device());
+  DmlcSgdArgs a;
+  a.master = master.data_ptr<float>(); a.grad = grad.data_ptr<float>();
+  a.mode = (int)mode; a.grad_scale = (float)grad_scale;
+  for (int i = 0; i < 10; ++i) a.off[i] = (int)off[i];
+  a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1;
+  a.part2 = part2.data_ptr<float>(); a.g2 = (int)g2;
+  a.partb2 = partb2.data_ptr<float>(); a.B = (int)B;
+  a.w1f = w1f.data_ptr(); a.w2f = w2f.data_ptr(); a.w2d = w2d.data_ptr(); a.fc1n = fc1n.data_ptr();
+  a.fc2t = fc2t.data_ptr(); a.fc2n = fc2n.data_ptr(); a.fc3t = fc3t.data_ptr(); a.fc3d = fc3d.data_ptr();
+  a.step = step.data_ptr<int64_t>(); a.lr0 = (float)lr0; a.decay = (float)decay;
+  a.decay_steps = (float)decay_steps; a.staircase = staircase;
+  a.ticket = reinterpret_cast<unsigned int*>(ticket.data_ptr<int>());
+  a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
+  a.nhead = (int)loss_part.numel();
+  a.stats = stats.data_ptr<float>(); a.stats_len = (int)stats.size(0);
+  CHECK_HIP(dmlc_sgd(&a, stream_of(master)));
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dmlc, m) {
+  m.def("conv1_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
+        "Tensor(a!) out, Tensor(b!) am) -> ()");
+  m.def("conv2_fwd(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
+  m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2, Tensor(c!) dbias_part) -> ()");
+  m.def("conv_wgrad(Tensor p1, Tensor dy2, Tensor(a!) part2, Tensor data, Tensor idx, Tensor? counter, int period, "
+        "int cy, int cx, Tensor dp1, Tensor am1, Tensor(b!) part1, Tensor(c!) partb1) -> ()");
+  m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params) -> ()");
+  m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
+        "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
+        "Tensor(a!) h1, Tensor(b!) h2, Tensor(c!) dl, Tensor(d!) dh1, Tensor(e!) dh2, Tensor(f!) loss_part, "
+        "Tensor(g!) correct_part, Tensor(h!)? logits_out) -> ()");
+  m.def("sgd(Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor part1, Tensor partb1, "
+        "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
+        "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
+        "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
+        "Tensor(m!) stats) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
+  m.impl("conv1_fwd", &conv1_fwd);
+  m.impl("conv2_fwd", &conv2_fwd);
+  m.impl("conv2_dgrad", &conv2_dgrad);
+  m.impl("conv_wgrad", &conv_wgrad);
+  m.impl("gemm_grouped", &gemm_grouped);
+  m.impl("head", &head);
+  m.impl("sgd", &sgd);
+}

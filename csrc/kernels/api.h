@@ -1,0 +1,143 @@
+// Host-side launch API of the HIP CNN kernels.
+//
+// Plain C structs + launch functions so that the torch binding TU (compiled by g++) never sees
+// device code, and the kernel TUs (compiled by hipcc) never include torch headers.
+// Every pointer is device memory; bf16 tensors are passed as `const void*` / `void*`.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+extern "C" {
+
+// Batch index source shared by the data-consuming kernels: sample index of row b is
+//   idx_base[(counter ? (*counter % period) : 0) * B + b]
+// so a captured graph walks an epoch permutation through the device step counter.
+struct DmlcIndexSrc {
+  const int* idx_base;
+  const int64_t* counter;   // nullable
+  int period;               // number of B-sized batches in idx_base
+};
+
+// conv1 5x5 (3->64) + bias + ReLU + maxpool 3x3/2 TF-SAME, fused with the uint8 gather + center
+// crop.  One workgroup per image.
+struct DmlcConv1FwdArgs {
+  const uint8_t* data;      // [N][32][32][3] uint8 (NHWC)
+  DmlcIndexSrc src;
+  int B, cy, cx;            // crop offsets (center crop = 4,4)
+  const void* w;            // bf16 [64][160]  (k = kh*32 + kw*4 + ci, zero padded)
+  const float* bias;        // [64]
+  void* out;                // bf16 [B][12][12][64]
+  uint8_t* am;              // [B][12][12][64] argmax (0..8) in the pool window, 255 = no gradient
+};
+
+// conv2 5x5 (64->64) + bias + ReLU + maxpool 3x3/2 TF-SAME.  One workgroup per image.
+struct DmlcConv2FwdArgs {
+  const void* in;           // bf16 [B][12][12][64]
+  const void* w;            // bf16 [64 co][1600]  (k = (kh*5+kw)*64 + ci)
+  const float* bias;        // [64]
+  void* out;                // bf16 [B][6][6][64]  (== [B][2304], NHWC flatten order)
+  uint8_t* am;              // [B][6][6][64]
+  int B;
+};
+
+// conv2 input-gradient with the pool2/ReLU backward fused into the operand staging.
+struct DmlcConv2DgradArgs {
+  const void* dp2;          // bf16 [B][6][6][64]  grad wrt pool2 output
+  const uint8_t* am2;       // [B][6][6][64]
+  const void* wd;           // bf16 [64 ci][1600]  (k' = (kh'*5+kw')*64 + co, W[4-kh'][4-kw'][ci][co])
+  void* dp1;                // bf16 [B][12][12][64] grad wrt pool1 output
+  void* dy2;                // bf16 [B][144][64]   grad wrt conv2 pre-activation (for wgrad)
+  float* dbias_part;        // [B][64] per-image conv2 bias-grad partials
+  int B;
+};
+
+// Weight gradients of both convolutions in ONE launch (split-K over image groups; fp32 partial
+// slabs reduced deterministically by the SGD kernel).
+struct DmlcConvWgradArgs {
+  // conv2: blocks [0, 10*g2)  -> (kh, ci-half, group)
+  const void* p1;           // bf16 [B][12][12][64]   (conv2 input)
+  const void* dy2;          // bf16 [B][144][64]
+  float* part2;             // [g2][1600][64]
+  int g2;
+  // conv1: blocks [10*g2, 10*g2 + g1) -> group
+  const uint8_t* data;      // [N][32][32][3]
+  DmlcIndexSrc src;
+  int cy, cx;
+  const void* dp1;          // bf16 [B][12][12][64]
+  const uint8_t* am1;       // [B][12][12][64]
+  float* part1;             // [g1][160][64]
+  float* partb1;            // [g1][64]
+  int g1;
+  int B;
+};
+
+// Grouped bf16 GEMM: up to 8 independent problems in one launch, 64x64 tiles, MFMA 16x16x32.
+//   a_kmajor=1: A(m,k) = A[m*lda + k]; 0: A(m,k) = A[k*lda + m]
+//   b_kmajor=1: B(k,n) = B[n*ldb + k]; 0: B(k,n) = B[k*ldb + n]
+//   c_mode 0: fp32 C[m*ldc+n] (+bias, relu)  1: bf16 C (+bias, relu)
+//          2: fp32 split-K partial slab C + split*M*ldc   3: column sums: C[m] = sum_k A(m,k)
+struct DmlcGemmProblem {
+  int M, N, K;
+  const void* A; int lda; int a_kmajor;
+  const void* B; int ldb; int b_kmajor;
+  void* C; int ldc; int c_mode;
+  int ksplit;
+  const float* bias; int relu;
+  int nvalid;               // store only columns n < nvalid
+  int tiles_m, tiles_n, block_start;   // filled by dmlc_gemm_grouped
+};
+#define DMLC_MAX_GEMM 8
+struct DmlcGemmGroup {
+  DmlcGemmProblem p[DMLC_MAX_GEMM];
+  int nprob;
+  int nblocks;
+};
+
+// MLP head, rows-parallel (16 rows per workgroup): fc1 split-K reduce + bias + ReLU, fc2, fc3,
+// (ReLU logits), softmax cross-entropy + accuracy, and (train) the backward through fc3/fc2.
+struct DmlcHeadArgs {
+  const float* h1part; int nsplit;   // [nsplit][B][384]
+  const float* b1;
+  const void* w2t; const float* b2;  // bf16 [192][384]
+  const void* w3t; const float* b3;  // bf16 [16][192] (rows >= 10 zero)
+  const void* w3d;                   // bf16 [192][32] (cols >= 10 zero)
+  const void* w2d;                   // bf16 [384][192]
+  const int* labels;                 // [N] dataset labels
+  DmlcIndexSrc src;
+  int B; float inv_batch; int relu_logits; int train;
+  void* h1; void* h2; void* dl; void* dh1; void* dh2;   // bf16 [B][384],[B][192],[B][16],[B][384],[B][192]
+  float* loss_part; int* correct_part;                  // [B/16]
+  float* logits_out;                                    // optional fp32 [B][10]
+};
+
+// Fused SGD over the flat fp32 parameter buffer (+ split-K partial reduction, LR schedule from the
+// device step counter, bf16 shadow-weight refresh, step++ by the last workgroup, stats ring).
+struct DmlcSgdArgs {
+  float* master;            // flat fp32 params (TF layouts)
+  float* grad;              // flat fp32 grads (fc part written by the GEMMs)
+  int mode;                 // 0 fused reduce+apply, 1 reduce only (conv grads -> grad), 2 apply from grad, 3 shadows only
+  float grad_scale;         // applied to the gradient in modes 0/2 (1/world for averaged DP)
+  // flat offsets of the 10 tensors, TF order
+  int off[10];
+  const float* part1; const float* partb1; int g1;   // conv1 partials
+  const float* part2; int g2;                        // conv2 partials
+  const float* partb2; int B;                        // conv2 bias partials [B][64]
+  // bf16 shadows
+  void* w1f; void* w2f; void* w2d; void* fc1n; void* fc2t; void* fc2n; void* fc3t; void* fc3d;
+  // schedule
+  int64_t* step; float lr0; float decay; float decay_steps; int staircase;
+  unsigned int* ticket;     // zero-initialised arrival counter
+  const float* loss_part; const int* correct_part; int nhead;
+  float* stats; int stats_len;   // ring [stats_len][4] = {step, loss, accuracy, lr}
+  int nblocks;
+};
+
+hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);
+hipError_t dmlc_conv2_fwd(const DmlcConv2FwdArgs* a, hipStream_t s);
+hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s);
+hipError_t dmlc_conv_wgrad(const DmlcConvWgradArgs* a, hipStream_t s);
+hipError_t dmlc_gemm_grouped(DmlcGemmGroup* g, hipStream_t s);
+hipError_t dmlc_head(const DmlcHeadArgs* a, hipStream_t s);
+hipError_t dmlc_sgd(DmlcSgdArgs* a, hipStream_t s);
+
+}  // extern "C"

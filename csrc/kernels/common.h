@@ -1,0 +1,65 @@
+// Shared device helpers for the CDNA4 (gfx950) CNN kernels.
+//
+// Conventions (see docs in cnn_conv.hip):
+//   * activations are NHWC bf16; accumulation is fp32 (MFMA 16x16x32 bf16);
+//   * MFMA lane maps (v_mfma_f32_16x16x32_bf16, wave64):
+//       A frag: lane l holds A[row = l&15][k = 8*(l>>4) + j], j = 0..7
+//       B frag: lane l holds B[k = 8*(l>>4) + j][col = l&15]
+//       C/D   : lane l holds C[row = 4*(l>>4) + i][col = l&15], i = 0..3
+//   * every kernel is launched with 256 threads = 4 waves.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmlc {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define DEV static __device__ __forceinline__
+#define LDS_AS __attribute__((address_space(3)))
+
+DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+DEV f32x4 zero4() { f32x4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of row q, columns 4p..4p+3
+// of a 4x16 block of 16-bit elements; lane i of the group receives column i (row q in element q).
+// Two reads (rows kb..kb+3 and kb+4..kb+7) give the 8-element MFMA fragment of one column.
+// EXEC must be all ones around these reads (no divergence).
+DEV bf16x8 tr_frag(const bf16* p0, const bf16* p1) {
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(p0));
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)(p1));
+  s16x8 r = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+DEV bf16x8 lds_b128(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+DEV bf16x8 glb_b128(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+DEV bf16x8 cat44(const bf16x4& a, const bf16x4& b) {
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+DEV bf16x4 pack4(float a, float b, float c, float d) {
+  bf16x4 r = {(bf16)a, (bf16)b, (bf16)c, (bf16)d};
+  return r;
+}
+
+DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// 16-byte chunk swizzle for [pixel][64 x bf16] LDS images (128-B rows): chunk c of pixel p is
+// stored at chunk slot c ^ (p & 7), spreading 16 consecutive pixels over all bank slots.
+DEV int swz128(int pix, int chunk) { return pix * 64 + ((chunk ^ (pix & 7)) << 3); }
+
+}  // namespace dmlc

@@ -1,0 +1,136 @@
+"""Eager (PyTorch-op) training engine.
+
+Used for (a) the CPU "plumbing" configuration (BASELINE config 1), (b) models without fused HIP
+kernels yet (ResNet-20), (c) the framework-default comparison line of the benchmark, and (d) as
+the numerics oracle for the fused engine.  Semantics follow the reference training step
+(/root/reference/cifar10cnn.py:159-164, :230): sparse softmax cross-entropy (mean), plain SGD,
+staircase LR decay, global_step++.  Data parallelism is synchronous: the flat gradient is
+all-reduced in two buckets (fc first, then conv — SURVEY.md §2.D) and averaged.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import config as C
+from ..models import build_model
+
+
+class EagerTrainer:
+    def __init__(self, model: str, batch_size: int, data: torch.Tensor, labels: torch.Tensor, *,
+                 device="cpu", world_size: int = 1, rank: int = 0, process_group=None, dtype: str = "fp32",
+                 lr: float = C.LEARNING_RATE, lr_decay: float = C.LR_DECAY,
+                 decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, relu_logits: bool = True,
+                 crop: int = C.CROP_HEIGHT, seed: int = 0, flat_params: Optional[torch.Tensor] = None,
+                 augment: bool = False):
+        self.device = torch.device(device)
+        self.model = build_model(model, seed=seed, relu_logits=relu_logits, flat=flat_params).to(self.device)
+        self.B = int(batch_size)
+        self.data = data.to(self.device)
+        self.labels = labels.to(self.device).long()
+        self.world_size, self.rank, self.pg = world_size, rank, process_group
+        self.dtype = dtype
+        self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
+        self.crop = crop
+        self.off = (32 - crop) // 2
+        self.seed = seed
+        self.augment = augment
+        self.n_data = self.data.shape[0]
+        self.shard = self.n_data // world_size
+        self.period = max(1, self.shard // self.B)
+        self.cur_epoch = -1
+        self.perm = None
+        self.global_step = 0
+        self.last_loss = float("nan")
+        self.last_acc = float("nan")
+        self.buckets = self.model.grad_buckets() if hasattr(self.model, "grad_buckets") else None
+
+    # ------------------------------------------------------------------------------------------
+    def lr(self, step: int) -> float:
+        if not self.staircase:
+            return self.lr0
+        return self.lr0 * self.decay ** math.floor(step / self.decay_steps)
+
+    def epoch_permutation(self, epoch: int) -> torch.Tensor:
+        g = torch.Generator().manual_seed(self.seed * 1000003 + epoch)
+        perm = torch.randperm(self.n_data, generator=g)
+        return perm[self.rank::self.world_size][: self.period * self.B]
+
+    def batch(self, step: int):
+        epoch = step // self.period
+        if epoch != self.cur_epoch:
+            self.perm = self.epoch_permutation(epoch).to(self.device)
+            self.cur_epoch = epoch
+        row = step % self.period
+        idx = self.perm[row * self.B:(row + 1) * self.B]
+        return self.images(idx), self.labels[idx]
+
+    def images(self, idx: torch.Tensor) -> torch.Tensor:
+        o, c = self.off, self.crop
+        x = self.data[idx]
+        if self.augment:
+            # random crop (±off) + horizontal flip, per batch (optional, D5)
+            dy, dx = (int(v) for v in torch.randint(0, 2 * o + 1, (2,)))
+            x = x[:, dy:dy + c, dx:dx + c, :]
+            if torch.rand(()) < 0.5:
+                x = x.flip(2)
+        else:
+            x = x[:, o:o + c, o:o + c, :]
+        return x.float()
+
+    def _allreduce_grads(self):
+        if self.world_size == 1:
+            return
+        for b in (self.buckets or [None]):
+            for p in self.model.parameters():
+                if p.grad is None:
+                    continue
+                g = p.grad if b is None else p.grad.view(-1)[b[0]:b[1]]
+                dist.all_reduce(g, group=self.pg)
+                g.div_(self.world_size)
+            if b is None:
+                break
+
+    def step(self):
+        x, y = self.batch(self.global_step)
+        self.model.train()
+        use_amp = self.dtype == "bf16" and self.device.type == "cuda"
+        with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=use_amp):
+            logits = self.model(x)
+        loss = torch.nn.functional.cross_entropy(logits.float(), y)
+        for p in self.model.parameters():
+            p.grad = None
+        loss.backward()
+        self._allreduce_grads()
+        lr = self.lr(self.global_step)
+        with torch.no_grad():
+            for p in self.model.parameters():
+                if p.grad is not None:
+                    p.add_(p.grad, alpha=-lr)
+        if hasattr(self.model, "after_step"):
+            self.model.after_step()
+        self.last_loss = loss.detach()
+        self.last_acc = (logits.detach().argmax(1) == y).float().mean()
+        self.global_step += 1
+
+    @torch.no_grad()
+    def evaluate(self, data: torch.Tensor, labels: torch.Tensor, max_batches: int = 0) -> float:
+        self.model.eval()
+        n = data.shape[0]
+        nb = math.ceil(n / self.B)
+        if max_batches:
+            nb = min(nb, max_batches)
+        correct = total = 0
+        o, c = self.off, self.crop
+        for i in range(nb):
+            x = data[i * self.B:(i + 1) * self.B].to(self.device)[:, o:o + c, o:o + c, :].float()
+            y = labels[i * self.B:(i + 1) * self.B].to(self.device).long()
+            with torch.autocast(self.device.type, dtype=torch.bfloat16,
+                                enabled=self.dtype == "bf16" and self.device.type == "cuda"):
+                logits = self.model(x)
+            correct += int((logits.argmax(1) == y).sum())
+            total += y.numel()
+        return correct / max(1, total)

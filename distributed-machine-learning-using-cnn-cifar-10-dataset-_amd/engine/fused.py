@@ -1,0 +1,353 @@
+"""Fused MI355X training engine for the reference CNN (hand-written HIP kernels + HIP graphs + RCCL).
+
+One training step (= one ``mon_sess.run([train_op, loss])`` of /root/reference/cifar10cnn.py:230,
+SURVEY.md §3.3) is eight kernel launches, all reading their inputs from device memory:
+
+  1 conv1_fwd    uint8 gather + center crop + conv1 + bias + ReLU + pool1 (+argmax)
+  2 conv2_fwd    conv2 + bias + ReLU + pool2 (+argmax)
+  3 gemm         fc1 forward, split-K fp32 partials
+  4 head         fc1 reduce/bias/ReLU, fc2, fc3, ReLU-logits, softmax-xent, accuracy, dlogits→dh2→dh1
+  5 gemm (x7)    fc1 dgrad + dW1 + dW2 + dW3 + db1 + db2 + db3 in ONE grouped launch
+  6 conv2_dgrad  pool2/ReLU backward gather + conv2 input-gradient (+ conv2 bias-grad partials)
+  7 conv_wgrad   conv2 and conv1 weight gradients (pool1/ReLU backward fused), split-K partials
+  8 sgd          partial reduction + SGD + LR schedule + bf16 shadow refresh + global_step++ + stats
+
+The batch index list is read through the device-resident global_step (``perm[step % period]``),
+so the whole step is a static HIP graph replayed once per step.  With data parallelism the fc
+gradients (90 % of the bytes, complete after launch 5) are all-reduced over RCCL on a side stream
+while launches 6-7 run, then the conv bucket, then the SGD applies.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import config as C
+from ..models import cifar_cnn as M
+from ..ops import _ext
+
+OPS = None
+
+
+def _ops():
+    global OPS
+    if OPS is None:
+        _ext.hip()
+        OPS = torch.ops.dmlc
+    return OPS
+
+
+SEG_OFF = [s.offset for s in M.PARAM_SPECS]
+SEG = {M.short(s.name): s for s in M.PARAM_SPECS}
+
+
+def _gemm_params(M_, N_, K_, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit=1, relu=0, nvalid=None):
+    return [M_, N_, K_, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit, relu, N_ if nvalid is None else nvalid]
+
+
+class FusedCifarEngine:
+    """Owns every device buffer of the fused step.  Not an nn.Module: parameters live in one flat
+    fp32 buffer (``self.master``) in the TF checkpoint layout; see models/cifar_cnn.py."""
+
+    def __init__(self, batch_size: int, data: torch.Tensor, labels: torch.Tensor, *, device=None,
+                 flat_params: Optional[torch.Tensor] = None, lr: float = C.LEARNING_RATE,
+                 lr_decay: float = C.LR_DECAY, decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True,
+                 relu_logits: bool = True, crop_offset=(4, 4), world_size: int = 1, rank: int = 0,
+                 process_group=None, seed: int = 0, fc1_split: Optional[int] = None, g1: Optional[int] = None,
+                 g2: Optional[int] = None, stats_len: int = 4096, comm_dtype: str = "fp32",
+                 capture_comm: bool = False):
+        ops = _ops()
+        self.ops = ops
+        self.device = torch.device(device or "cuda")
+        dev = self.device
+        B = int(batch_size)
+        if B % 16 != 0 or B < 16:
+            raise ValueError("fused engine needs a batch size that is a positive multiple of 16")
+        self.B = B
+        self.world_size, self.rank, self.pg = world_size, rank, process_group
+        self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
+        self.relu_logits = relu_logits
+        self.cy, self.cx = crop_offset
+        self.comm_dtype = comm_dtype
+        self.capture_comm = capture_comm
+        self.seed = seed
+
+        # --- data (device resident) ---------------------------------------------------------
+        assert data.dtype == torch.uint8 and tuple(data.shape[1:]) == (32, 32, 3)
+        self.data = data.to(dev).contiguous()
+        self.labels = labels.to(dev, torch.int32).contiguous()
+        self.n_data = self.data.shape[0]
+        self.shard = self.n_data // world_size
+        self.period = max(1, self.shard // B)
+        self.perm = torch.zeros(self.period * B, dtype=torch.int32, device=dev)
+        self.cur_epoch = -1
+
+        # --- parameters + shadows -------------------------------------------------------------
+        if flat_params is None:
+            flat_params = M.init_flat_params(torch.Generator().manual_seed(seed))
+        self.master = flat_params.to(dev, torch.float32).contiguous().clone()
+        self.grad = torch.zeros_like(self.master)
+        bf = torch.bfloat16
+        z = lambda *s, dt=bf: torch.zeros(*s, dtype=dt, device=dev)
+        self.w1f, self.w2f, self.w2d = z(64, 160), z(64, 1600), z(64, 1600)
+        self.fc1n, self.fc2t, self.fc2n = z(2304, 384), z(192, 384), z(384, 192)
+        self.fc3t, self.fc3d = z(16, 192), z(192, 32)
+
+        # --- activations / workspaces -------------------------------------------------------
+        self.fc1_split = fc1_split or self._pick_fc1_split(B)
+        self.g1 = g1 or max(1, min(B, B // 2))
+        self.g2 = g2 or max(1, min(B, 24 if B >= 24 else B))
+        self.p1, self.am1 = z(B, 12, 12, 64), z(B, 12, 12, 64, dt=torch.uint8)
+        self.p2, self.am2 = z(B, 6, 6, 64), z(B, 6, 6, 64, dt=torch.uint8)
+        self.h1part = z(self.fc1_split, B, 384, dt=torch.float32)
+        self.h1, self.h2, self.dl = z(B, 384), z(B, 192), z(B, 16)
+        self.dh1, self.dh2 = z(B, 384), z(B, 192)
+        self.dp2 = z(B, 6, 6, 64)
+        self.dp1, self.dy2 = z(B, 12, 12, 64), z(B, 144, 64)
+        self.dbias2 = z(B, 64, dt=torch.float32)
+        self.part2 = z(self.g2, 1600, 64, dt=torch.float32)
+        self.part1, self.partb1 = z(self.g1, 160, 64, dt=torch.float32), z(self.g1, 64, dt=torch.float32)
+        self.loss_part = z(B // 16, dt=torch.float32)
+        self.correct_part = z(B // 16, dt=torch.int32)
+        self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
+        self.logits_buf = z(B, 10, dt=torch.float32)
+
+        p = {k: self.master[s.offset:s.offset + s.numel] for k, s in SEG.items()}
+        self.pv = p
+        gv = {k: self.grad[s.offset:s.offset + s.numel] for k, s in SEG.items()}
+        self.gv = gv
+
+        # grouped GEMM problem lists
+        self._fc1_fwd = dict(A=[self.p2.view(B, 2304)], B=[self.fc1n], C=[self.h1part], bias=[None],
+                             params=_gemm_params(B, 384, 2304, 2304, 1, 384, 0, 384, 2, self.fc1_split))
+        self._fc_bwd = dict(
+            A=[self.dh1, self.p2.view(B, 2304), self.h1, self.h2, self.dh1, self.dh2, self.dl],
+            B=[self.fc1n, self.dh1, self.dh2, self.dl, self.dh1, self.dh2, self.dl],
+            C=[self.dp2.view(B, 2304), gv["full_weight_1"], gv["full_weight_2"], gv["full_weight_3"],
+               gv["full_bias_1"], gv["full_bias_2"], gv["full_bias_3"]],
+            bias=[None] * 7,
+            params=(_gemm_params(B, 2304, 384, 384, 1, 384, 1, 2304, 1)            # dp2 = dh1 W1^T
+                    + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 0)          # dW1 = p2^T dh1
+                    + _gemm_params(384, 192, B, 384, 0, 192, 0, 192, 0)            # dW2 = h1^T dh2
+                    + _gemm_params(192, 16, B, 192, 0, 16, 0, 10, 0, nvalid=10)    # dW3 = h2^T dl
+                    + _gemm_params(384, 8, B, 384, 0, 8, 0, 1, 3)                  # db1
+                    + _gemm_params(192, 8, B, 192, 0, 8, 0, 1, 3)                  # db2
+                    + _gemm_params(16, 8, B, 16, 0, 8, 0, 1, 3, nvalid=10)))       # db3
+
+        self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.comm_stream = torch.cuda.Stream(device=dev) if world_size > 1 else None
+        self.host_step = 0
+        self.refresh_shadows()
+
+    # ------------------------------------------------------------------------------------------
+    @staticmethod
+    def _pick_fc1_split(B: int) -> int:
+        # aim for ~192 workgroups: (B/64) * 6 tiles * split
+        tiles = max(1, math.ceil(B / 64)) * 6
+        return int(max(1, min(9, round(192 / tiles))))
+
+    def refresh_shadows(self):
+        self._sgd(mode=3)
+
+    def set_step(self, step: int):
+        self.step_t.fill_(int(step))
+        self.host_step = int(step)
+
+    # --- data order ---------------------------------------------------------------------------
+    def epoch_permutation(self, epoch: int) -> torch.Tensor:
+        """Rank-sharded permutation of the dataset for ``epoch`` (D6: every rank sees a disjoint
+        shard; the same global order on every rank because the seed is shared)."""
+        g = torch.Generator().manual_seed(self.seed * 1000003 + epoch)
+        perm = torch.randperm(self.n_data, generator=g)
+        shard = perm[self.rank::self.world_size][: self.period * self.B]
+        return shard.to(torch.int32)
+
+    def _maybe_new_epoch(self):
+        epoch = self.host_step // self.period
+        if epoch != self.cur_epoch:
+            self.perm.copy_(self.epoch_permutation(epoch), non_blocking=False)
+            self.cur_epoch = epoch
+
+    # --- kernels ------------------------------------------------------------------------------
+    def _forward(self, idx, counter, period, train=True, logits_out=None):
+        o, p, B = self.ops, self.pv, self.B
+        o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1, self.am1)
+        o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
+        f = self._fc1_fwd
+        o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
+        o.head(self.h1part, p["full_bias_1"], self.fc2t, p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d,
+               self.fc2n, self.labels, idx, counter, period, 1.0 / (B * self.world_size), self.relu_logits, train,
+               self.h1, self.h2, self.dl, self.dh1, self.dh2, self.loss_part, self.correct_part, logits_out)
+
+    def _fc_backward(self):
+        f = self._fc_bwd
+        self.ops.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
+
+    def _conv_backward(self):
+        o = self.ops
+        o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2, self.dbias2)
+        o.conv_wgrad(self.p1, self.dy2, self.part2, self.data, self.perm, self.step_t, self.period, self.cy,
+                     self.cx, self.dp1, self.am1, self.part1, self.partb1)
+
+    def _sgd(self, mode: int, scale: float = 1.0):
+        self.ops.sgd(self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.dbias2,
+                     self.w1f, self.w2f, self.w2d, self.fc1n, self.fc2t, self.fc2n, self.fc3t, self.fc3d,
+                     self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
+                     self.loss_part, self.correct_part, self.stats)
+
+    def _allreduce(self, t: torch.Tensor):
+        import torch.distributed as dist
+        if self.comm_dtype == "bf16":
+            tb = t.to(torch.bfloat16)
+            dist.all_reduce(tb, group=self.pg)
+            t.copy_(tb)
+        else:
+            dist.all_reduce(t, group=self.pg)
+
+    # segments of one step: each is a capturable list of launches on the current stream
+    def _seg_compute_a(self):
+        self._forward(self.perm, self.step_t, self.period, train=True)
+        self._fc_backward()
+
+    def _seg_compute_b(self):
+        self._conv_backward()
+        self._sgd(mode=0 if self.world_size == 1 else 1)
+
+    def _seg_apply(self):
+        self._sgd(mode=2, scale=1.0)
+
+    def compute_gradients(self):
+        """Forward + backward only (no update); the full gradient lands in ``self.grad``."""
+        self._maybe_new_epoch()
+        self._seg_compute_a()
+        self._conv_backward()
+        self._sgd(mode=1)
+        return self.grad
+
+    def _eager_step(self):
+        if self.world_size == 1:
+            self._seg_compute_a()
+            self._seg_compute_b()
+            return
+        main = torch.cuda.current_stream(self.device)
+        fc = self.grad[M.FC_BUCKET_OFFSET:]
+        conv = self.grad[:M.FC_BUCKET_OFFSET]
+        self._seg_compute_a()
+        ev = torch.cuda.Event()
+        ev.record(main)
+        self.comm_stream.wait_event(ev)
+        with torch.cuda.stream(self.comm_stream):
+            self._allreduce(fc)
+        self._seg_compute_b()
+        ev2 = torch.cuda.Event()
+        ev2.record(main)
+        self.comm_stream.wait_event(ev2)
+        with torch.cuda.stream(self.comm_stream):
+            self._allreduce(conv)
+        main.wait_stream(self.comm_stream)
+        self._seg_apply()
+
+    # --- graph capture --------------------------------------------------------------------------
+    def capture(self):
+        """Capture the step into HIP graph(s).  N=1: one graph.  N>1: compute graphs around eager
+        RCCL collectives (or one graph including the collectives when capture_comm=True)."""
+        torch.cuda.synchronize(self.device)
+        self.graphs = []
+        pool = torch.cuda.graph_pool_handle()
+        if self.world_size == 1:
+            segs = [self._eager_step]
+        elif self.capture_comm:
+            segs = [self._eager_step]
+        else:
+            segs = [self._seg_compute_a, self._seg_compute_b, self._seg_apply]
+        # state (step counter, master weights) must be identical before and after capture: a
+        # capture records launches without running them, so nothing changes here.
+        for fn in segs:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, pool=pool, stream=s):
+                    fn()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self.graphs.append(g)
+        torch.cuda.synchronize(self.device)
+
+    def step(self):
+        """One training step (asynchronous: returns once launched)."""
+        self._maybe_new_epoch()
+        if not self.graphs:
+            self._eager_step()
+        elif len(self.graphs) == 1:
+            self.graphs[0].replay()
+        else:
+            main = torch.cuda.current_stream(self.device)
+            self.graphs[0].replay()
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self.comm_stream.wait_event(ev)
+            with torch.cuda.stream(self.comm_stream):
+                self._allreduce(self.grad[M.FC_BUCKET_OFFSET:])
+            self.graphs[1].replay()
+            ev2 = torch.cuda.Event()
+            ev2.record(main)
+            self.comm_stream.wait_event(ev2)
+            with torch.cuda.stream(self.comm_stream):
+                self._allreduce(self.grad[:M.FC_BUCKET_OFFSET])
+            main.wait_stream(self.comm_stream)
+            self.graphs[2].replay()
+        self.host_step += 1
+
+    # --- evaluation -----------------------------------------------------------------------------
+    @torch.no_grad()
+    def evaluate(self, data: torch.Tensor, labels: torch.Tensor, max_batches: int = 0) -> float:
+        """Test accuracy over ``data`` (uint8 [N,32,32,3]) with the fused forward kernels."""
+        data = data.to(self.device).contiguous()
+        labels = labels.to(self.device, torch.int32).contiguous()
+        saved = (self.data, self.labels)
+        self.data, self.labels = data, labels
+        n = data.shape[0]
+        nb = math.ceil(n / self.B)
+        if max_batches:
+            nb = min(nb, max_batches)
+        correct, total = 0, 0
+        try:
+            for i in range(nb):
+                ids = torch.arange(i * self.B, (i + 1) * self.B, device=self.device, dtype=torch.int32)
+                valid = int(min(self.B, n - i * self.B))
+                ids = torch.clamp(ids, max=n - 1)
+                self._forward(ids, None, 1, train=False, logits_out=self.logits_buf)
+                pred = self.logits_buf[:valid].argmax(dim=1)
+                correct += int((pred == labels[i * self.B:i * self.B + valid].long()).sum())
+                total += valid
+        finally:
+            self.data, self.labels = saved
+        return correct / max(1, total)
+
+    @torch.no_grad()
+    def forward_logits(self, idx: torch.Tensor) -> torch.Tensor:
+        """Logits (fp32 [B,10]) of dataset rows ``idx`` (int32 [B]) — for tests."""
+        self._forward(idx.to(self.device, torch.int32).contiguous(), None, 1, train=False, logits_out=self.logits_buf)
+        return self.logits_buf.clone()
+
+    # --- state ----------------------------------------------------------------------------------
+    def read_stats(self, step: int) -> Dict[str, float]:
+        """Stats published by the SGD kernel for the step that produced global_step == ``step``."""
+        row = self.stats[(step - 1) % self.stats.shape[0]].tolist()
+        return {"global_step": int(row[0]), "loss": row[1], "accuracy": row[2], "lr": row[3]}
+
+    def global_step(self) -> int:
+        return int(self.step_t.item())
+
+    def flat_params(self) -> torch.Tensor:
+        return self.master.detach().cpu()
+
+    def load_flat_params(self, flat: torch.Tensor, step: Optional[int] = None):
+        self.master.copy_(flat.to(self.device, torch.float32))
+        if step is not None:
+            self.set_step(step)
+        self.refresh_shadows()

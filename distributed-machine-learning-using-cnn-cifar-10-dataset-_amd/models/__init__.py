@@ -1,0 +1,11 @@
+"""Model families: the reference CIFAR-10 CNN and ResNet-20 (BASELINE config 4)."""
+from .cifar_cnn import CifarCNN, PARAM_SPECS, FLAT_SIZE, NUM_PARAMS  # noqa: F401
+
+
+def build_model(name: str, seed: int = 0, relu_logits: bool = True, flat=None):
+    if name in ("cifar_cnn", "cnn", "cifar10_cnn"):
+        return CifarCNN(flat=flat, relu_logits=relu_logits, seed=seed)
+    if name in ("resnet20", "resnet-20"):
+        from .resnet import ResNet20
+        return ResNet20(seed=seed)
+    raise ValueError(f"unknown model {name!r}")

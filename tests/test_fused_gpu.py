@@ -1,0 +1,122 @@
+"""Numerics of the HIP kernels vs a plain PyTorch fp32 reference of the same ops (TF semantics).
+
+Every check goes through the fused engine, i.e. exactly the kernels the benchmark runs."""
+import pytest
+import torch
+
+from dmlc.engine.fused import FusedCifarEngine
+from dmlc.models import cifar_cnn as M
+
+pytestmark = pytest.mark.gpu
+
+
+def _synthetic(n, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    data = torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 10, (n,), dtype=torch.int32, generator=g)
+    return data, labels
+
+
+def _ref_grads(flat, data, labels, idx, relu_logits=True):
+    dev = "cuda"
+    flat = flat.to(dev).clone().requires_grad_(True)
+    x = data[idx.long()].to(dev)[:, 4:28, 4:28, :].float()
+    logits = M.cnn_forward(x, M.views(flat), relu_logits)
+    loss = M.cifar_loss(logits, labels[idx.long()].to(dev))
+    loss.backward()
+    return logits.detach(), loss.detach(), flat.grad.detach()
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+@pytest.mark.parametrize("B", [16, 64, 128])
+def test_forward_logits_match_reference(B):
+    data, labels = _synthetic(max(256, 2 * B))
+    eng = FusedCifarEngine(B, data, labels, seed=1)
+    idx = torch.randperm(data.shape[0])[:B].to(torch.int32)
+    got = eng.forward_logits(idx)
+    ref, _, _ = _ref_grads(eng.flat_params(), data, labels, idx)
+    assert _rel(got, ref) < 3e-2, _rel(got, ref)
+
+
+@pytest.mark.parametrize("B", [32, 128])
+def test_gradients_match_reference(B):
+    data, labels = _synthetic(4 * B, seed=3)
+    eng = FusedCifarEngine(B, data, labels, seed=2)
+    eng._maybe_new_epoch()
+    idx = eng.perm[:B].cpu()
+    grad = eng.compute_gradients().cpu()
+    _, _, gref = _ref_grads(eng.flat_params(), data, labels, idx)
+    gref = gref.cpu()
+    for s in M.PARAM_SPECS:
+        a = grad[s.offset:s.offset + s.numel]
+        b = gref[s.offset:s.offset + s.numel]
+        if b.norm() < 1e-8:
+            assert a.norm() < 1e-4, s.name
+            continue
+        cos = float(torch.nn.functional.cosine_similarity(a, b, dim=0))
+        assert cos > 0.99 and _rel(a, b) < 0.1, (s.name, cos, _rel(a, b))
+
+
+def test_sgd_step_matches_reference_update():
+    B = 64
+    data, labels = _synthetic(4 * B, seed=5)
+    eng = FusedCifarEngine(B, data, labels, seed=4, lr=0.01)
+    before = eng.flat_params().clone()
+    eng._maybe_new_epoch()
+    idx = eng.perm[:B].cpu()
+    eng.step()
+    torch.cuda.synchronize()
+    after = eng.flat_params()
+    _, loss, gref = _ref_grads(before, data, labels, idx)
+    expect = before - 0.01 * gref.cpu()
+    assert eng.global_step() == 1
+    st = eng.read_stats(1)
+    assert abs(st["loss"] - float(loss)) / max(1.0, abs(float(loss))) < 2e-2
+    assert abs(st["lr"] - 0.01) < 1e-7
+    delta, dref = after - before, expect - before
+    assert float(torch.nn.functional.cosine_similarity(delta, dref, dim=0)) > 0.99
+
+
+def test_graph_replay_equals_eager_and_is_deterministic():
+    B = 64
+    data, labels = _synthetic(8 * B, seed=7)
+    a = FusedCifarEngine(B, data, labels, seed=8)
+    b = FusedCifarEngine(B, data, labels, seed=8)
+    for _ in range(3):
+        a.step()
+    b.capture()
+    for _ in range(3):
+        b.step()
+    torch.cuda.synchronize()
+    assert a.global_step() == b.global_step() == 3
+    assert torch.equal(a.flat_params(), b.flat_params())
+
+
+def test_training_reduces_loss():
+    B = 128
+    data, labels = _synthetic(2048, seed=9)
+    # learnable synthetic task: the label is a function of the mean intensity of a channel
+    labels = (data[:, :, :, 0].float().mean(dim=(1, 2)) / 25.6).clamp(max=9).to(torch.int32)
+    eng = FusedCifarEngine(B, data, labels, seed=10, lr=0.002)
+    eng.capture()
+    losses = []
+    for i in range(60):
+        eng.step()
+        if (i + 1) % 10 == 0:
+            torch.cuda.synchronize()
+            losses.append(eng.read_stats(eng.host_step)["loss"])
+    assert losses[-1] < losses[0], losses
+
+
+def test_lr_staircase_schedule_on_device():
+    B = 16
+    data, labels = _synthetic(64, seed=11)
+    eng = FusedCifarEngine(B, data, labels, seed=12, lr=0.1, lr_decay=0.5, decay_steps=2)
+    for _ in range(5):
+        eng.step()
+    torch.cuda.synchronize()
+    lrs = [eng.read_stats(s)["lr"] for s in range(1, 6)]
+    assert lrs == pytest.approx([0.1, 0.1, 0.05, 0.05, 0.025])
