@@ -75,7 +75,7 @@ void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   check_numel(b1, "b1", at::kFloat, 64);
   check(out, "out", at::kBFloat16, {B, 12, 12, 64});
   check(am, "am", at::kByte, {B, 12, 12, 64});
-  c10::hip::HIPGuard guard(out.device());
+  c10::DeviceGuard guard(out.device());
   DmlcConv1FwdArgs a;
   a.data = data.data_ptr<uint8_t>();
   a.src = index_src(idx, counter, period, B);
@@ -92,7 +92,7 @@ void conv2_fwd(const Tensor& in, const Tensor& w2f, const Tensor& b2, const Tens
   check_numel(b2, "b2", at::kFloat, 64);
   check(out, "out", at::kBFloat16, {B, 6, 6, 64});
   check(am, "am", at::kByte, {B, 6, 6, 64});
-  c10::hip::HIPGuard guard(in.device());
+  c10::DeviceGuard guard(in.device());
   DmlcConv2FwdArgs a;
   a.in = in.data_ptr(); a.w = w2f.data_ptr(); a.bias = b2.data_ptr<float>();
   a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>(); a.B = (int)B;
@@ -108,7 +108,7 @@ void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const 
   check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
   check(dbias_part, "dbias_part", at::kFloat, {B, 64});
-  c10::hip::HIPGuard guard(dp2.device());
+  c10::DeviceGuard guard(dp2.device());
   DmlcConv2DgradArgs a;
   a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
   a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.dbias_part = dbias_part.data_ptr<float>(); a.B = (int)B;
@@ -130,7 +130,7 @@ void conv_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const 
   check(am1, "am1", at::kByte, {B, 12, 12, 64});
   check(part1, "part1", at::kFloat, {g1, 160, 64});
   check(partb1, "partb1", at::kFloat, {g1, 64});
-  c10::hip::HIPGuard guard(p1.device());
+  c10::DeviceGuard guard(p1.device());
   DmlcConvWgradArgs a;
   a.p1 = p1.data_ptr(); a.dy2 = dy2.data_ptr(); a.part2 = part2.data_ptr<float>(); a.g2 = (int)g2;
   a.data = data.data_ptr<uint8_t>(); a.src = index_src(idx, counter, period, B);
@@ -185,7 +185,7 @@ void gemm_grouped(at::TensorList A, at::TensorList Bm, at::TensorList C, const c
   for (int i = 0; i < n; ++i) {
     if (G.p[i].c_mode == 3) { G.p[i].A = A[i].data_ptr(); G.p[i].C = C[i].data_ptr(); G.p[i].bias = nullptr; }
   }
-  c10::hip::HIPGuard guard(A[0].device());
+  c10::DeviceGuard guard(A[0].device());
   CHECK_HIP(dmlc_gemm_grouped(&G, stream_of(A[0])));
 }
 
@@ -216,7 +216,7 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
     check(dh1, "dh1", at::kBFloat16, {B, 384});
     check(dh2, "dh2", at::kBFloat16, {B, 192});
   }
-  c10::hip::HIPGuard guard(h1part.device());
+  c10::DeviceGuard guard(h1part.device());
   DmlcHeadArgs a;
   a.h1part = h1part.data_ptr<float>(); a.nsplit = (int)nsplit;
   a.b1 = b1.data_ptr<float>(); a.w2t = w2t.data_ptr(); a.b2 = b2.data_ptr<float>();
@@ -269,7 +269,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
                   loss_part.numel() == correct_part.numel(), "loss/correct partials mismatch");
   dev(stats, "stats");
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(1) == 4, "stats must be [R,4] fp32");
-  c10::hip::HIPGuard guard(master.device());
+  c10::DeviceGuard guard(master.device());
   DmlcSgdArgs a;
   a.master = master.data_ptr<float>(); a.grad = grad.data_ptr<float>();
   a.mode = (int)mode; a.grad_scale = (float)grad_scale;

@@ -75,7 +75,7 @@ struct DmlcConvWgradArgs {
 //   a_kmajor=1: A(m,k) = A[m*lda + k]; 0: A(m,k) = A[k*lda + m]
 //   b_kmajor=1: B(k,n) = B[n*ldb + k]; 0: B(k,n) = B[k*ldb + n]
 //   c_mode 0: fp32 C[m*ldc+n] (+bias, relu)  1: bf16 C (+bias, relu)
-//          2: fp32 split-K partial slab C + split*M*ldc   3: column sums: C[m] = sum_k A(m,k)
+//          2: fp32 split-K partial slab C + split*M*ldc   3: column sums: C[m] = sum_k A(m,k), m < nvalid
 struct DmlcGemmProblem {
   int M, N, K;
   const void* A; int lda; int a_kmajor;

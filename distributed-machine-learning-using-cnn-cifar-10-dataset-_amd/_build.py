@@ -2,8 +2,8 @@
 
 * ``_lib/libdmlc_hip.so`` — CDNA4 HIP kernels (``csrc/kernels/*.hip``, hipcc --offload-arch=gfx950)
   + their torch.ops bindings (``csrc/bindings/torch_ops.cpp``).
-* ``_lib/libdmlc_rt.so``  — CPU runtime (``csrc/runtime/*.cpp``): CIFAR-10 binary reader, TF
-  TensorBundle-V2 checkpoint writer/reader, crc32c, TFRecord/event writer.
+* ``_lib/_dmlc_rt*.so``   — CPU runtime, a pybind11 module (``csrc/runtime/*.cpp``): CIFAR-10
+  binary reader, TF TensorBundle-V2 checkpoint writer/reader, crc32c, TFRecord/event writer.
 
 Objects are rebuilt only when a content hash of their sources + flags changes, so importing the
 package (or running the tests) after a build costs nothing.  ``python -m dmlc._build`` forces a
@@ -29,7 +29,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 HIP_LIB = os.path.join(LIB_DIR, "libdmlc_hip.so")
-RT_LIB = os.path.join(LIB_DIR, "libdmlc_rt.so")
+RT_LIB = os.path.join(LIB_DIR, "_dmlc_rt" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 
 
 def _torch_paths():
@@ -112,10 +112,13 @@ def build(hip: bool = True, rt: bool = True, jobs: int | None = None) -> dict:
         jobs_list.append((bsrc, headers, o, ["g++"], torch_flags))
     if rt:
         rt_headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+        import pybind11
+        rt_flags = ["-std=c++17", "-O3", "-fPIC", "-fvisibility=hidden", f"-I{py_inc}",
+                    f"-I{pybind11.get_include()}"]
         for src in sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))):
             o = os.path.join(OBJ_DIR, "rt_" + os.path.basename(src) + ".o")
             rt_objs.append(o)
-            jobs_list.append((src, rt_headers, o, ["g++"], torch_flags + ["-O3"]))
+            jobs_list.append((src, rt_headers, o, ["g++"], rt_flags))
     with cf.ThreadPoolExecutor(jobs) as ex:
         futs = [ex.submit(_compile, *j) for j in jobs_list]
         for f in futs:
@@ -126,7 +129,7 @@ def build(hip: bool = True, rt: bool = True, jobs: int | None = None) -> dict:
               + [f"-L{torch_lib}", "-lc10_hip", "-ltorch_hip"])
         out["hip"] = HIP_LIB
     if rt and rt_objs:
-        _link(rt_objs, RT_LIB, ["g++", "-shared", "-fPIC"] + torch_link)
+        _link(rt_objs, RT_LIB, ["g++", "-shared", "-fPIC", "-pthread"])
         out["rt"] = RT_LIB
     return out
 

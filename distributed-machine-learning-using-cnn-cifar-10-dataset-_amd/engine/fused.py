@@ -134,8 +134,8 @@ class FusedCifarEngine:
                     + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 0)          # dW1 = p2^T dh1
                     + _gemm_params(384, 192, B, 384, 0, 192, 0, 192, 0)            # dW2 = h1^T dh2
                     + _gemm_params(192, 16, B, 192, 0, 16, 0, 10, 0, nvalid=10)    # dW3 = h2^T dl
-                    + _gemm_params(384, 8, B, 384, 0, 8, 0, 1, 3)                  # db1
-                    + _gemm_params(192, 8, B, 192, 0, 8, 0, 1, 3)                  # db2
+                    + _gemm_params(384, 8, B, 384, 0, 8, 0, 1, 3, nvalid=384)      # db1
+                    + _gemm_params(192, 8, B, 192, 0, 8, 0, 1, 3, nvalid=192)      # db2
                     + _gemm_params(16, 8, B, 16, 0, 8, 0, 1, 3, nvalid=10)))       # db3
 
         self.graphs: List[torch.cuda.CUDAGraph] = []

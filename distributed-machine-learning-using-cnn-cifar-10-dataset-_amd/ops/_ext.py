@@ -2,7 +2,7 @@
 
 ``hip()`` makes ``torch.ops.dmlc.*`` (the CDNA4 kernels) available and FAILS LOUDLY when it cannot:
 on a GPU box a silent fallback to PyTorch ops would hide that the native path is not running.
-``rt()`` loads the CPU runtime (``torch.ops.dmlc_rt.*``).  Both build in-tree on first use if the
+``rt()`` returns the native CPU runtime module (``_dmlc_rt``, pybind11).  Both build in-tree on first use if the
 shared object is missing (``_build.py``; a prebuilt ``.so`` in the tree is used as is).
 """
 from __future__ import annotations
@@ -34,13 +34,18 @@ def hip() -> None:
         _loaded["hip"] = True
 
 
-def rt() -> None:
+def rt():
+    """The native CPU runtime module (pybind11, ``csrc/runtime``)."""
     with _lock:
         if _loaded["rt"]:
-            return
+            return _loaded["rt"]
         path = _ensure("rt")
-        torch.ops.load_library(path)
-        _loaded["rt"] = True
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("_dmlc_rt", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _loaded["rt"] = mod
+        return mod
 
 
 def hip_available() -> bool:

@@ -96,11 +96,12 @@ def test_graph_replay_equals_eager_and_is_deterministic():
 
 
 def test_training_reduces_loss():
+    # The reference model (raw 0..255 pixels, ReLU on the logits) dies at most learning rates; the
+    # convergence check runs the same kernels with linear logits (the --relu_logits=false variant).
+    from dmlc.data import synthetic
     B = 128
-    data, labels = _synthetic(2048, seed=9)
-    # learnable synthetic task: the label is a function of the mean intensity of a channel
-    labels = (data[:, :, :, 0].float().mean(dim=(1, 2)) / 25.6).clamp(max=9).to(torch.int32)
-    eng = FusedCifarEngine(B, data, labels, seed=10, lr=0.002)
+    data, labels = synthetic(2048, seed=9, learnable=True)
+    eng = FusedCifarEngine(B, data, labels, seed=10, lr=0.0005, relu_logits=False)
     eng.capture()
     losses = []
     for i in range(60):
@@ -108,7 +109,7 @@ def test_training_reduces_loss():
         if (i + 1) % 10 == 0:
             torch.cuda.synchronize()
             losses.append(eng.read_stats(eng.host_step)["loss"])
-    assert losses[-1] < losses[0], losses
+    assert losses[-1] < 0.9 * losses[0], losses
 
 
 def test_lr_staircase_schedule_on_device():
