@@ -63,6 +63,7 @@ class TrainConfig:
     augment: bool = False                 # D5: reference uses a deterministic center crop
     synthetic: bool = False
     synthetic_size: int = 50000
+    download: bool = False                # fetch the CIFAR-10 archive if absent (offline by default)
     model: str = "cifar_cnn"              # cifar_cnn | resnet20
     dtype: str = "bf16"                   # fp32 | bf16 | fp8
     impl: str = "auto"                    # auto | fused (HIP kernels + hipGraph) | eager (torch ops)

@@ -116,6 +116,17 @@ class EagerTrainer:
         self.last_acc = (logits.detach().argmax(1) == y).float().mean()
         self.global_step += 1
 
+    def flat_params(self) -> torch.Tensor:
+        return self.model.flat.detach().cpu().clone()
+
+    @torch.no_grad()
+    def load_flat_params(self, flat: torch.Tensor, step: Optional[int] = None):
+        self.model.flat.copy_(flat.to(self.model.flat.device, self.model.flat.dtype))
+        if hasattr(self.model, "after_load"):
+            self.model.after_load()
+        if step is not None:
+            self.global_step = int(step)
+
     @torch.no_grad()
     def evaluate(self, data: torch.Tensor, labels: torch.Tensor, max_batches: int = 0) -> float:
         self.model.eval()

@@ -1,0 +1,262 @@
+"""Training session: the reference's ``main()`` (/root/reference/cifar10cnn.py:179-242) rebuilt around
+synchronous data parallelism, the fused MI355X engine and explicit hooks.
+
+Hook semantics follow what TF1's MonitoredTrainingSession gave the reference (SURVEY.md §3.2, §3.5,
+§5.1-§5.5):
+  * StopAtStepHook(last_step=generations): stop once global_step >= last_step (absolute, so a
+    resumed run finishes at the same step; :219);
+  * chief-only checkpoint saver: at session start, every ``checkpoint_secs`` and at the end,
+    ``max_to_keep`` newest kept; restore of the latest checkpoint at start-up (:222);
+  * chief step counter: ``global_step/sec`` into the events file every 100 steps;
+  * console lines kept verbatim: ``Starting Training``, ``global_step %s, task:%d_step %d, training
+    accuracy %g`` every ``output_every`` local iterations (:232-235) and `` --- Test Accuracy =
+    {:.2f}%.`` every ``eval_every`` (:237-241).
+Reference defects fixed: D1 the eval actually evaluates the test set; D2 one
+authoritative global_step shared by all ranks; D3 the staircase LR decays with global_step
+(``--lr_schedule=constant`` reproduces the reference as run); D6 every rank trains on a disjoint
+shard of each epoch's permutation; D11 the printed training accuracy is that of the batch just
+trained on (fused into the loss kernel) instead of an extra forward pass on a fresh batch.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import time
+from typing import Dict, Optional
+
+import torch
+
+from .. import checkpoint as CK
+from .. import config as C
+from ..parallel import dist as D
+from ..utils.events import EventsWriter, MetricsLog
+
+
+# --- engine adapters: one interface over the fused HIP engine and the eager torch engine ------------
+class _FusedAdapter:
+    kind = "fused"
+
+    def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, data, labels):
+        from .fused import FusedCifarEngine
+        self.eng = FusedCifarEngine(cfg.batch_size, data, labels, device=info.device, world_size=info.world_size,
+                                    rank=max(0, info.rank), seed=cfg.seed, lr=cfg.learning_rate,
+                                    lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
+                                    staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
+                                    crop_offset=((32 - cfg.crop) // 2,) * 2, comm_dtype=cfg.comm_dtype)
+        self.graph = cfg.graph
+        from ..models import cifar_cnn as M
+        self.specs = M.PARAM_SPECS
+
+    def start(self):
+        pass
+
+    def step(self):
+        self.eng.step()
+        if self.graph and not self.eng.graphs:
+            # the first step runs eagerly (lazy code-object load, LDS attributes); then the whole
+            # step is captured once and replayed as a HIP graph
+            self.eng.capture()
+
+    @property
+    def global_step(self) -> int:
+        return self.eng.host_step
+
+    def stats(self) -> Dict[str, float]:
+        return self.eng.read_stats(self.eng.host_step)
+
+    def flat(self) -> torch.Tensor:
+        return self.eng.flat_params()
+
+    def load(self, flat: torch.Tensor, step: int):
+        self.eng.load_flat_params(flat, step)
+
+    def evaluate(self, x, y, max_batches=0) -> float:
+        return self.eng.evaluate(x, y, max_batches)
+
+    def sync(self):
+        torch.cuda.synchronize(self.eng.device)
+
+
+class _EagerAdapter:
+    kind = "eager"
+
+    def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, data, labels):
+        from .eager import EagerTrainer
+        self.tr = EagerTrainer(cfg.model, cfg.batch_size, data, labels, device=info.device,
+                               world_size=info.world_size, rank=max(0, info.rank), dtype=cfg.dtype,
+                               lr=cfg.learning_rate, lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
+                               staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
+                               crop=cfg.crop, seed=cfg.seed, augment=cfg.augment)
+        self.specs = self.tr.model.specs
+
+    def start(self):
+        pass
+
+    def step(self):
+        self.tr.step()
+
+    @property
+    def global_step(self) -> int:
+        return self.tr.global_step
+
+    def stats(self) -> Dict[str, float]:
+        return {"global_step": self.tr.global_step, "loss": float(self.tr.last_loss),
+                "accuracy": float(self.tr.last_acc), "lr": self.tr.lr(self.tr.global_step - 1)}
+
+    def flat(self) -> torch.Tensor:
+        return self.tr.flat_params()
+
+    def load(self, flat: torch.Tensor, step: int):
+        self.tr.load_flat_params(flat, step)
+
+    def evaluate(self, x, y, max_batches=0) -> float:
+        return self.tr.evaluate(x, y, max_batches)
+
+    def sync(self):
+        if self.tr.device.type == "cuda":
+            torch.cuda.synchronize(self.tr.device)
+
+
+def pick_impl(cfg: C.TrainConfig, device: torch.device) -> str:
+    if cfg.impl != "auto":
+        return cfg.impl
+    if (device.type == "cuda" and cfg.model == "cifar_cnn" and cfg.dtype == "bf16" and cfg.crop == 24
+            and cfg.batch_size % 16 == 0 and not cfg.augment):
+        return "fused"
+    return "eager"
+
+
+def _fault_injection(step: int, rank: int):
+    """Test hook: DMLC_FAULT_STEP / DMLC_FAULT_RANK kill this rank hard at a step,
+    on the first attempt only (DMLC_RESTART_COUNT is set by the launcher)."""
+    fs = os.environ.get("DMLC_FAULT_STEP")
+    if fs is None or int(os.environ.get("DMLC_RESTART_COUNT", "0")) > 0:
+        return
+    if step == int(fs) and rank == int(os.environ.get("DMLC_FAULT_RANK", "0")):
+        print(f"[fault-injection] rank {rank} exiting at global_step {step}", flush=True)
+        os._exit(17)
+
+
+class Session:
+    """One worker's training session."""
+
+    def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, log=print):
+        self.cfg, self.info, self.log = cfg, info, log
+        self.chief = info.rank == 0
+        tr_x, tr_y, te_x, te_y = _load_data(cfg, info)
+        self.test = (te_x, te_y)
+        impl = pick_impl(cfg, info.device)
+        self.engine = (_FusedAdapter if impl == "fused" else _EagerAdapter)(cfg, info, tr_x, tr_y)
+        self.impl = impl
+        self.ckpt = None
+        self.events = None
+        self.metrics = MetricsLog(None)
+        if self.chief and cfg.log_dir:
+            if cfg.save_checkpoints:
+                self.ckpt = CK.CheckpointManager(cfg.log_dir, cfg.max_to_keep, cfg.checkpoint_secs)
+            self.events = EventsWriter(cfg.log_dir)
+            self.metrics = MetricsLog(cfg.metrics_file or os.path.join(cfg.log_dir, "metrics.jsonl"))
+
+    # --- checkpoint --------------------------------------------------------------------------------
+    def restore(self) -> int:
+        """Chief loads the latest checkpoint in log_dir (if any) and broadcasts it to every rank."""
+        step = torch.zeros(1, dtype=torch.int64)
+        flat = self.engine.flat().clone()
+        have = torch.zeros(1, dtype=torch.int64)
+        if self.chief and self.cfg.log_dir:
+            path = CK.latest_checkpoint(self.cfg.log_dir)
+            if path:
+                tensors = CK.read_bundle(path)
+                flat, s, _ = CK.load_model_tensors(tensors, flat_size=flat.numel(), specs=self.engine.specs)
+                step[0] = s
+                have[0] = 1
+                self.log(f"Restored {path} (global_step {s})")
+        if self.info.world_size > 1:
+            dev = self.info.device if self.info.backend == "nccl" else torch.device("cpu")
+            bufs = [t.to(dev) for t in (have, step, flat)]
+            for b in bufs:
+                D.broadcast_(b, self.info)
+            have, step, flat = (b.cpu() for b in bufs)
+        if int(have[0]):
+            self.engine.load(flat, int(step[0]))
+        return int(step[0])
+
+    def save(self, force=False):
+        if self.ckpt is not None and (force or self.ckpt.due()):
+            gs = self.engine.global_step
+            self.ckpt.save(gs, CK.model_tensors(self.engine.flat(), gs, 0, specs=self.engine.specs))
+
+    # --- main loop -----------------------------------------------------------------------------------
+    def run(self) -> Dict[str, float]:
+        cfg, eng = self.cfg, self.engine
+        self.restore()
+        self.save(force=True)            # CheckpointSaverHook.after_create_session
+        eng.start()
+        self.log("Starting Training")
+        i = 0
+        last_t, last_step = time.time(), eng.global_step
+        result = {}
+        while eng.global_step < cfg.generations:        # StopAtStepHook(last_step=GENERATIONS)
+            _fault_injection(eng.global_step, self.info.rank)
+            eng.step()
+            if (i + 1) % cfg.output_every == 0:
+                st = eng.stats()
+                now = time.time()
+                steps = eng.global_step - last_step
+                ips = steps * cfg.batch_size * self.info.world_size / max(1e-9, now - last_t)
+                self.log("global_step %s, task:%d_step %d, training accuracy %g"
+                         % (eng.global_step, cfg.task_index, i, st["accuracy"]))
+                self.metrics.write(step=eng.global_step, loss=st["loss"], accuracy=st["accuracy"], lr=st["lr"],
+                                   images_per_sec=ips, step_ms=1000.0 * (now - last_t) / max(1, steps))
+                if self.events is not None:
+                    self.events.scalars(eng.global_step, {"global_step/sec": steps / max(1e-9, now - last_t),
+                                                          "loss": st["loss"], "accuracy": st["accuracy"],
+                                                          "learning_rate": st["lr"]})
+                last_t, last_step = now, eng.global_step
+                result = dict(st, images_per_sec=ips)
+            if (i + 1) % cfg.eval_every == 0:
+                acc = eng.evaluate(*self.test, max_batches=cfg.eval_batches)
+                self.log(" --- Test Accuracy = {:.2f}%.".format(100.0 * acc))
+                self.metrics.write(step=eng.global_step, test_accuracy=acc)
+                result["test_accuracy"] = acc
+            if self.ckpt is not None and self.ckpt.due():
+                self.save()
+            i += 1
+        eng.sync()
+        self.save(force=True)            # CheckpointSaverHook.end
+        result["global_step"] = eng.global_step
+        if self.events is not None:
+            self.events.close()
+        self.metrics.close()
+        return result
+
+
+def _load_data(cfg: C.TrainConfig, info: D.DistInfo):
+    from ..data import dataset
+    return dataset(cfg, is_chief=info.rank == 0, barrier=lambda: D.barrier(info))
+
+
+def main(argv=None) -> int:
+    """CLI entry (``python cifar10cnn.py ...`` / ``python -m dmlc.train ...``)."""
+    from .. import cli
+    cfg, _unparsed = cli.parse(argv)
+    role = cli.resolve_role(cfg)
+    if role.kind == "none":
+        return 0                          # unknown --job_name: the reference silently did nothing
+    if role.kind == "ps":
+        return D.serve_ps(role, log=lambda m: print(m, flush=True))
+    info = D.init(D.role_info(role), device=cfg.device, timeout_s=cfg.pg_timeout_s)
+    try:
+        sess = Session(cfg, info, log=lambda m: print(m, flush=True))
+        res = sess.run()
+        if info.rank == 0:
+            print(f"done: {res}", flush=True)
+        D.report_done(info)
+    finally:
+        D.shutdown(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -5,17 +5,25 @@ Replaces the reference's tf.train.ClusterSpec / tf.train.Server gRPC runtime
 synchronous collectives.  Two entry styles are supported:
   * torchrun-style env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT);
   * the reference's CLI roles (``--ps_hosts/--worker_hosts/--job_name/--task_index``), mapped by
-    :mod:`dmlc.cli` onto the same fields.
+    :func:`dmlc.cli.resolve_role` onto the same fields.  With a ``ps`` task the TCPStore is served by
+    the ps process (:func:`serve_ps`), which exits once every worker has reported completion.
+
+Failure detection: every collective runs under the process-group timeout
+(``pg_timeout_s``), so a dead rank makes the survivors fail fast instead of hanging; the local
+launcher (:mod:`dmlc.launch`) then restarts the world from the latest checkpoint.
 """
 from __future__ import annotations
 
 import dataclasses
 import datetime
 import os
+import time
 from typing import Optional
 
 import torch
 import torch.distributed as dist
+
+DONE_KEY = "dmlc/workers_done"
 
 
 @dataclasses.dataclass
@@ -28,6 +36,9 @@ class DistInfo:
     backend: str = "gloo"
     device: torch.device = torch.device("cpu")
     initialized: bool = False
+    store: Optional[object] = None
+    store_is_ps: bool = False
+    from_env: bool = False        # torchrun-style env: rendezvous via env:// (the agent's store)
 
     @property
     def is_chief(self) -> bool:
@@ -39,7 +50,13 @@ def env_info() -> DistInfo:
     return DistInfo(rank=int(os.environ.get("RANK", "0")), world_size=ws,
                     local_rank=int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0"))),
                     master_addr=os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                    master_port=int(os.environ.get("MASTER_PORT", "29500")))
+                    master_port=int(os.environ.get("MASTER_PORT", "29500")), from_env="RANK" in os.environ)
+
+
+def role_info(role) -> DistInfo:
+    return DistInfo(rank=role.rank, world_size=role.world_size, local_rank=role.local_rank,
+                    master_addr=role.master_addr, master_port=role.master_port, store_is_ps=role.store_is_ps,
+                    from_env=role.from_env)
 
 
 def pick_device(local_rank: int, want: str = "auto") -> torch.device:
@@ -60,16 +77,46 @@ def init(info: Optional[DistInfo] = None, device: str = "auto", timeout_s: float
     info.device = pick_device(info.local_rank, device)
     info.backend = backend or ("nccl" if info.device.type == "cuda" else "gloo")
     if info.world_size > 1 and not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", info.master_addr)
-        os.environ.setdefault("MASTER_PORT", str(info.master_port))
+        timeout = datetime.timedelta(seconds=timeout_s)
         kw = {}
         if info.backend == "nccl":
             kw["device_id"] = info.device
-        dist.init_process_group(info.backend, init_method=f"tcp://{info.master_addr}:{info.master_port}",
-                                rank=info.rank, world_size=info.world_size,
-                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        if info.from_env:
+            os.environ.setdefault("MASTER_ADDR", info.master_addr)
+            os.environ.setdefault("MASTER_PORT", str(info.master_port))
+            dist.init_process_group(info.backend, init_method="env://", rank=info.rank,
+                                    world_size=info.world_size, timeout=timeout, **kw)
+        else:
+            # rank 0 hosts the store unless a ps task serves it (reference CLI with --ps_hosts)
+            info.store = dist.TCPStore(info.master_addr, info.master_port, None,
+                                       is_master=(info.rank == 0 and not info.store_is_ps), timeout=timeout,
+                                       wait_for_workers=False)
+            dist.init_process_group(info.backend, store=info.store, rank=info.rank, world_size=info.world_size,
+                                    timeout=timeout, **kw)
         info.initialized = True
     return info
+
+
+def serve_ps(role, timeout_s: float = 86400.0, poll_s: float = 0.2, log=print) -> int:
+    """The ``--job_name=ps`` process: host the rendezvous store, wait until all workers are done."""
+    store = dist.TCPStore(role.master_addr, role.master_port, None, is_master=True,
+                          timeout=datetime.timedelta(seconds=timeout_s), wait_for_workers=False)
+    log(f"ps: rendezvous store serving {role.master_addr}:{role.master_port} for {role.world_size} worker(s)")
+    t0 = time.time()
+    while True:
+        done = store.add(DONE_KEY, 0)
+        if done >= role.world_size:
+            log(f"ps: all {role.world_size} worker(s) finished")
+            return 0
+        if time.time() - t0 > timeout_s:
+            log("ps: timed out waiting for workers")
+            return 1
+        time.sleep(poll_s)
+
+
+def report_done(info: DistInfo):
+    if info.store is not None and info.store_is_ps:
+        info.store.add(DONE_KEY, 1)
 
 
 def barrier(info: DistInfo):
@@ -88,6 +135,14 @@ def all_max(value: float, info: DistInfo) -> float:
     return float(t.item())
 
 
+def broadcast_(t: torch.Tensor, info: DistInfo, src: int = 0) -> torch.Tensor:
+    """In-place broadcast from ``src`` (chief restores a checkpoint, every rank starts identical)."""
+    if info.world_size > 1 and dist.is_initialized():
+        dist.broadcast(t, src)
+    return t
+
+
 def shutdown(info: DistInfo):
     if info.initialized and dist.is_initialized():
         dist.destroy_process_group()
+        info.initialized = False

@@ -8,6 +8,7 @@ registered ``torch.ops.dmlc`` operators) exists exactly once.
 """
 import importlib
 import importlib.abc
+import importlib.machinery
 import importlib.util
 import os
 import sys
@@ -30,11 +31,29 @@ class _AliasLoader(importlib.abc.Loader):
     def exec_module(self, module):
         pass
 
+    # runpy (``python -m dmlc.<module>``) runs the real module's code object as __main__
+    def _real_spec(self):
+        return importlib.util.find_spec(self.real)
+
+    def get_code(self, fullname):
+        spec = self._real_spec()
+        return spec.loader.get_code(self.real)
+
+    def is_package(self, fullname):
+        return self._real_spec().submodule_search_locations is not None
+
 
 class _AliasFinder(importlib.abc.MetaPathFinder):
     def find_spec(self, fullname, path, target=None):
         if fullname.startswith(ALIAS + "."):
-            return importlib.util.spec_from_loader(fullname, _AliasLoader(REAL + fullname[len(ALIAS):]))
+            real = REAL + fullname[len(ALIAS):]
+            real_spec = importlib.util.find_spec(real)
+            if real_spec is None:
+                return None
+            spec = importlib.machinery.ModuleSpec(fullname, _AliasLoader(real), origin=real_spec.origin,
+                                                  is_package=real_spec.submodule_search_locations is not None)
+            spec.has_location = real_spec.has_location
+            return spec
         return None
 
 

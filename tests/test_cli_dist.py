@@ -1,0 +1,166 @@
+"""CLI compatibility, role mapping, gloo data-parallel equivalence, the reference's ps/worker recipe,
+and launcher fault injection + resume ('Distributed (fake cluster)', §5.3, §5.6)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from dmlc import checkpoint as CK
+from dmlc import cli
+from dmlc.config import TrainConfig
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENTRY = os.path.join(REPO, "cifar10cnn.py")
+
+
+# ---- flags ----------------------------------------------------------------------------------------
+def test_reference_flags_and_defaults():
+    cfg, rest = cli.parse([])
+    # cifar10cnn.py:249-272 defaults
+    assert (cfg.ps_hosts, cfg.worker_hosts, cfg.job_name, cfg.task_index) == ("", "", "", 0)
+    assert cfg.data_dir == "/tmp/mnist_data" and cfg.log_dir == "/tmp/train_logs"
+    # cifar10cnn.py:9-27 constants
+    assert (cfg.batch_size, cfg.generations, cfg.learning_rate, cfg.lr_decay, cfg.num_gens_to_wait) == \
+        (128, 20000, 0.1, 0.9, 250.0)
+    assert (cfg.output_every, cfg.eval_every, cfg.crop) == (200, 500, 24)
+    cfg, rest = cli.parse(["--ps_hosts=localhost:2222", "--worker_hosts=localhost:2223,localhost:2224",
+                           "--job_name=worker", "--task_index=1", "--some_tf_flag=3", "--log_dir", "/x"])
+    assert cfg.task_index == 1 and cfg.log_dir == "/x" and rest == ["--some_tf_flag=3"]
+
+
+def test_bool_flags():
+    cfg, _ = cli.parse(["--relu_logits=false", "--synthetic"])
+    assert cfg.relu_logits is False and cfg.synthetic is True
+    with pytest.raises(SystemExit):
+        cli.parse(["--relu_logits=maybe"])
+
+
+def test_role_mapping():
+    base = dict(ps_hosts="localhost:2222", worker_hosts="localhost:2223,localhost:2224,otherhost:2225")
+    r = cli.resolve_role(TrainConfig(job_name="worker", task_index=1, **base), env={})
+    assert (r.kind, r.rank, r.world_size, r.local_rank) == ("worker", 1, 3, 1)
+    assert (r.master_addr, r.master_port, r.store_is_ps) == ("127.0.0.1", 2222, True)
+    r = cli.resolve_role(TrainConfig(job_name="worker", task_index=2, **base), env={})
+    assert r.local_rank == 0                      # first worker on otherhost
+    r = cli.resolve_role(TrainConfig(job_name="ps", task_index=0, **base), env={})
+    assert r.kind == "ps" and r.world_size == 3
+    r = cli.resolve_role(TrainConfig(job_name="worker", task_index=0, worker_hosts="localhost:5000,localhost:5001"),
+                         env={})
+    assert r.master_port == 5000 and not r.store_is_ps
+    assert cli.resolve_role(TrainConfig(job_name="chief"), env={}).kind == "none"
+    r = cli.resolve_role(TrainConfig(), env={"RANK": "3", "WORLD_SIZE": "8", "LOCAL_RANK": "3",
+                                             "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "1234"})
+    assert (r.rank, r.world_size, r.master_port, r.from_env) == (3, 8, 1234, True)
+    with pytest.raises(ValueError):
+        cli.resolve_role(TrainConfig(job_name="worker", task_index=5, **base), env={})
+
+
+# ---- gloo DP equivalence ----------------------------------------------------------------------------
+def _dp_worker(rank, world, port, out, steps, B):
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    import dmlc  # noqa: F401
+    from dmlc.data import synthetic
+    from dmlc.engine.eager import EagerTrainer
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    x, y = synthetic(256, seed=1)
+    tr = EagerTrainer("cifar_cnn", B, x, y, world_size=world, rank=rank, lr=1e-4, relu_logits=False, seed=3)
+    for _ in range(steps):
+        tr.step()
+    torch.save(tr.flat_params(), os.path.join(out, f"rank{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_gloo_dp_equals_single_process_large_batch(tmp_path):
+    import torch.multiprocessing as mp
+    from dmlc.data import synthetic
+    from dmlc.engine.eager import EagerTrainer
+    from dmlc.models import cifar_cnn as M
+    world, B, steps = 2, 16, 3
+    mp.spawn(_dp_worker, args=(world, cli.free_port(), str(tmp_path), steps, B), nprocs=world, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    assert torch.equal(r0, r1)                   # replicas stay identical
+    # single process, global batch = union of the ranks' shards, mean loss over 2B
+    x, y = synthetic(256, seed=1)
+    ranks = [EagerTrainer("cifar_cnn", B, x, y, world_size=world, rank=r, seed=3) for r in range(world)]
+    flat = M.init_flat_params(torch.Generator().manual_seed(3)).requires_grad_(True)
+    for s in range(steps):
+        idx = torch.cat([t.epoch_permutation(s // t.period)[(s % t.period) * B:(s % t.period + 1) * B]
+                         for t in ranks])
+        xb = x[idx][:, 4:28, 4:28, :].float()
+        loss = M.cifar_loss(M.cnn_forward(xb, M.views(flat), relu_logits=False), y[idx])
+        g, = torch.autograd.grad(loss, flat)
+        lr = 1e-4 * 0.9 ** (s // 250)
+        flat = (flat - lr * g).detach().requires_grad_(True)
+    init = M.init_flat_params(torch.Generator().manual_seed(3))
+    d_dp, d_ref = r0 - init, flat.detach() - init
+    # fp32 summation-order noise only (a missing 1/world average would give ~1.0)
+    assert float((d_dp - d_ref).norm() / d_ref.norm()) < 1e-3
+
+
+def test_rank_shards_are_disjoint():
+    from dmlc.data import synthetic
+    from dmlc.engine.eager import EagerTrainer
+    x, y = synthetic(100, seed=0)
+    shards = [set(EagerTrainer("cifar_cnn", 10, x, y, world_size=4, rank=r).epoch_permutation(0).tolist())
+              for r in range(4)]
+    assert all(len(s) == 20 for s in shards)
+    assert len(set.union(*shards)) == 80
+
+
+# ---- the reference's 3-terminal recipe (1 ps + 2 workers), CPU / gloo ---------------------------------
+COMMON = ["--synthetic", "--synthetic_size=512", "--batch_size=16", "--device=cpu", "--learning_rate=0.0001",
+          "--relu_logits=false", "--output_every=5", "--eval_every=10", "--eval_batches=1"]
+
+
+def _env():
+    e = dict(os.environ)
+    e["OMP_NUM_THREADS"] = "2"
+    e.pop("RANK", None)
+    e.pop("WORLD_SIZE", None)
+    return e
+
+
+@pytest.mark.timeout(300)
+def test_ps_worker_recipe(tmp_path):
+    p0, p1, p2 = cli.free_port(), cli.free_port(), cli.free_port()
+    hosts = [f"--ps_hosts=localhost:{p0}", f"--worker_hosts=localhost:{p1},localhost:{p2}"]
+    flags = hosts + COMMON + [f"--log_dir={tmp_path}", "--generations=12"]
+    ps = subprocess.Popen([sys.executable, ENTRY, "--job_name=ps", "--task_index=0"] + flags, env=_env(),
+                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    ws = [subprocess.Popen([sys.executable, ENTRY, "--job_name=worker", f"--task_index={k}"] + flags, env=_env(),
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for k in range(2)]
+    outs = [w.communicate(timeout=240)[0] for w in ws]
+    ps_out = ps.communicate(timeout=60)[0]
+    assert [w.returncode for w in ws] == [0, 0], outs
+    assert ps.returncode == 0, ps_out
+    assert "all 2 worker(s) finished" in ps_out
+    assert "Starting Training" in outs[0] and "global_step 10, task:0_step 9, training accuracy" in outs[0]
+    assert "global_step 10, task:1_step 9, training accuracy" in outs[1]
+    assert " --- Test Accuracy = " in outs[0]
+    assert CK.latest_checkpoint(str(tmp_path)).endswith("model.ckpt-12")
+    # only the chief writes checkpoints / events / metrics
+    recs = [json.loads(l) for l in open(tmp_path / "metrics.jsonl")]
+    assert recs[-1]["step"] == 10 or recs[-1].get("test_accuracy") is not None
+
+
+@pytest.mark.timeout(300)
+def test_launcher_fault_injection_resumes_from_checkpoint(tmp_path):
+    env = _env()
+    env.update(DMLC_FAULT_STEP="7", DMLC_FAULT_RANK="1")
+    cmd = [sys.executable, "-m", "dmlc.launch", "--nproc", "2", "--max_restarts", "2", "--"] + COMMON + \
+          [f"--log_dir={tmp_path}", "--generations=15", "--checkpoint_secs=0"]
+    r = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=280)
+    assert r.returncode == 0, r.stdout
+    assert "[fault-injection] rank 1 exiting at global_step 7" in r.stdout
+    assert "restart 1/2" in r.stdout
+    assert "Restored" in r.stdout                 # the relaunched chief resumed from a checkpoint
+    path = CK.latest_checkpoint(str(tmp_path))
+    assert path.endswith("model.ckpt-15")
+    assert int(CK.read_bundle(path)["global_step"]) == 15
