@@ -99,45 +99,52 @@ void conv2_fwd(const Tensor& in, const Tensor& w2f, const Tensor& b2, const Tens
   CHECK_HIP(dmlc_conv2_fwd(&a, stream_of(in)));
 }
 
-void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const Tensor& dp1, const Tensor& dy2,
-                 const Tensor& dbias_part) {
+void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const Tensor& dp1, const Tensor& dy2) {
   const int64_t B = dp2.size(0);
   check(dp2, "dp2", at::kBFloat16, {B, 6, 6, 64});
   check(am2, "am2", at::kByte, {B, 6, 6, 64});
   check(w2d, "w2d", at::kBFloat16, {64, 1600});
   check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  check(dbias_part, "dbias_part", at::kFloat, {B, 64});
   c10::DeviceGuard guard(dp2.device());
   DmlcConv2DgradArgs a;
   a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
-  a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.dbias_part = dbias_part.data_ptr<float>(); a.B = (int)B;
+  a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B;
   CHECK_HIP(dmlc_conv2_dgrad(&a, stream_of(dp2)));
 }
 
-void conv_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& data, const Tensor& idx,
-                const c10::optional<Tensor>& counter, int64_t period, int64_t cy, int64_t cx, const Tensor& dp1,
-                const Tensor& am1, const Tensor& part1, const Tensor& partb1) {
-  const int64_t B = p1.size(0);
-  check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
-  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  const int64_t g2 = part2.size(0), g1 = part1.size(0);
-  TORCH_CHECK(g2 >= 1 && g2 <= B && g1 >= 1 && g1 <= B, "split-K groups must be in [1,B]");
-  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+void conv1_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
+                 int64_t cy, int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1,
+                 const Tensor& partb1) {
+  const int64_t B = dp1.size(0), g1 = part1.size(0);
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
+  TORCH_CHECK(g1 >= 1 && g1 <= B, "split-K groups must be in [1,B]");
   check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
   check(am1, "am1", at::kByte, {B, 12, 12, 64});
-  check(part1, "part1", at::kFloat, {g1, 160, 64});
+  check(part1, "part1", at::kFloat, {g1, 80, 64});
   check(partb1, "partb1", at::kFloat, {g1, 64});
-  c10::DeviceGuard guard(p1.device());
-  DmlcConvWgradArgs a;
-  a.p1 = p1.data_ptr(); a.dy2 = dy2.data_ptr(); a.part2 = part2.data_ptr<float>(); a.g2 = (int)g2;
+  c10::DeviceGuard guard(dp1.device());
+  DmlcConv1WgradArgs a;
   a.data = data.data_ptr<uint8_t>(); a.src = index_src(idx, counter, period, B);
   a.cy = (int)cy; a.cx = (int)cx;
   a.dp1 = dp1.data_ptr(); a.am1 = am1.data_ptr<uint8_t>();
   a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1; a.B = (int)B;
-  CHECK_HIP(dmlc_conv_wgrad(&a, stream_of(p1)));
+  CHECK_HIP(dmlc_conv1_wgrad(&a, stream_of(dp1)));
+}
+
+void conv2_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2) {
+  const int64_t B = p1.size(0), g2 = part2.size(0);
+  TORCH_CHECK(g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
+  check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
+  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
+  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+  check(partb2, "partb2", at::kFloat, {g2, 64});
+  c10::DeviceGuard guard(p1.device());
+  DmlcConv2WgradArgs a;
+  a.p1 = p1.data_ptr(); a.dy2 = dy2.data_ptr(); a.part2 = part2.data_ptr<float>();
+  a.partb2 = partb2.data_ptr<float>(); a.g2 = (int)g2; a.B = (int)B;
+  CHECK_HIP(dmlc_conv2_wgrad(&a, stream_of(p1)));
 }
 
 // params per problem (12 ints): M, N, K, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit, relu, nvalid
@@ -249,11 +256,13 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   const int64_t end = off[9] + 10;
   check_min(master, "master", at::kFloat, end);
   check_min(grad, "grad", at::kFloat, end);
-  const int64_t g1 = part1.size(0), g2 = part2.size(0), B = partb2.size(0);
-  check(part1, "part1", at::kFloat, {g1, 160, 64});
+  const int64_t g1 = part1.size(0), g2 = part2.size(0);
+  check(part1, "part1", at::kFloat, {g1, 80, 64});
   check(partb1, "partb1", at::kFloat, {g1, 64});
   check(part2, "part2", at::kFloat, {g2, 1600, 64});
-  check(partb2, "partb2", at::kFloat, {B, 64});
+  check(partb2, "partb2", at::kFloat, {g2, 64});
+  TORCH_CHECK(loss_part.numel() >= 1, "loss partials missing");
+  const int64_t B = loss_part.numel() * 16;
   check(w1f, "w1f", at::kBFloat16, {64, 160});
   check(w2f, "w2f", at::kBFloat16, {64, 1600});
   check(w2d, "w2d", at::kBFloat16, {64, 1600});
@@ -294,9 +303,10 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("conv1_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
         "Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("conv2_fwd(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
-  m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2, Tensor(c!) dbias_part) -> ()");
-  m.def("conv_wgrad(Tensor p1, Tensor dy2, Tensor(a!) part2, Tensor data, Tensor idx, Tensor? counter, int period, "
-        "int cy, int cx, Tensor dp1, Tensor am1, Tensor(b!) part1, Tensor(c!) partb1) -> ()");
+  m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
+  m.def("conv1_wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
+        "Tensor(a!) part1, Tensor(b!) partb1) -> ()");
+  m.def("conv2_wgrad(Tensor p1, Tensor dy2, Tensor(a!) part2, Tensor(b!) partb2) -> ()");
   m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params) -> ()");
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
@@ -313,7 +323,8 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("conv1_fwd", &conv1_fwd);
   m.impl("conv2_fwd", &conv2_fwd);
   m.impl("conv2_dgrad", &conv2_dgrad);
-  m.impl("conv_wgrad", &conv_wgrad);
+  m.impl("conv1_wgrad", &conv1_wgrad);
+  m.impl("conv2_wgrad", &conv2_wgrad);
   m.impl("gemm_grouped", &gemm_grouped);
   m.impl("head", &head);
   m.impl("sgd", &sgd);

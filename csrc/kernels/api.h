@@ -47,27 +47,29 @@ struct DmlcConv2DgradArgs {
   const void* wd;           // bf16 [64 ci][1600]  (k' = (kh'*5+kw')*64 + co, W[4-kh'][4-kw'][ci][co])
   void* dp1;                // bf16 [B][12][12][64] grad wrt pool1 output
   void* dy2;                // bf16 [B][144][64]   grad wrt conv2 pre-activation (for wgrad)
-  float* dbias_part;        // [B][64] per-image conv2 bias-grad partials
   int B;
 };
 
-// Weight gradients of both convolutions in ONE launch (split-K over image groups; fp32 partial
-// slabs reduced deterministically by the SGD kernel).
-struct DmlcConvWgradArgs {
-  // conv2: blocks [0, 10*g2)  -> (kh, ci-half, group)
-  const void* p1;           // bf16 [B][12][12][64]   (conv2 input)
-  const void* dy2;          // bf16 [B][144][64]
-  float* part2;             // [g2][1600][64]
-  int g2;
-  // conv1: blocks [10*g2, 10*g2 + g1) -> group
+// conv1 weight gradient (pool1/ReLU backward fused; split-K over image groups).
+struct DmlcConv1WgradArgs {
   const uint8_t* data;      // [N][32][32][3]
   DmlcIndexSrc src;
   int cy, cx;
-  const void* dp1;          // bf16 [B][12][12][64]
+  const void* dp1;          // bf16 [B][12][12][64]  grad wrt pool1 output
   const uint8_t* am1;       // [B][12][12][64]
-  float* part1;             // [g1][160][64]
+  float* part1;             // [g1][80][64]  k'' = kh*16 + kw*3 + ci (k'' % 16 == 15 unused)
   float* partb1;            // [g1][64]
   int g1;
+  int B;
+};
+
+// conv2 weight gradient: blocks (kh, image group); fp32 partial slab per group.
+struct DmlcConv2WgradArgs {
+  const void* p1;           // bf16 [B][12][12][64]   (conv2 input)
+  const void* dy2;          // bf16 [B][144][64]      (conv2 pre-activation gradient)
+  float* part2;             // [g2][1600][64]
+  float* partb2;            // [g2][64] conv2 bias-grad partials (written by the kh == 0 blocks)
+  int g2;
   int B;
 };
 
@@ -119,9 +121,9 @@ struct DmlcSgdArgs {
   float grad_scale;         // applied to the gradient in modes 0/2 (1/world for averaged DP)
   // flat offsets of the 10 tensors, TF order
   int off[10];
-  const float* part1; const float* partb1; int g1;   // conv1 partials
-  const float* part2; int g2;                        // conv2 partials
-  const float* partb2; int B;                        // conv2 bias partials [B][64]
+  const float* part1; const float* partb1; int g1;   // conv1 partials [g1][80][64], [g1][64]
+  const float* part2; int g2;                        // conv2 partials [g2][1600][64]
+  const float* partb2; int B;                        // conv2 bias partials [g2][64]
   // bf16 shadows
   void* w1f; void* w2f; void* w2d; void* fc1n; void* fc2t; void* fc2n; void* fc3t; void* fc3d;
   // schedule
@@ -135,7 +137,8 @@ struct DmlcSgdArgs {
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_fwd(const DmlcConv2FwdArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s);
-hipError_t dmlc_conv_wgrad(const DmlcConvWgradArgs* a, hipStream_t s);
+hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s);
+hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s);
 hipError_t dmlc_gemm_grouped(DmlcGemmGroup* g, hipStream_t s);
 hipError_t dmlc_head(const DmlcHeadArgs* a, hipStream_t s);
 hipError_t dmlc_sgd(DmlcSgdArgs* a, hipStream_t s);

@@ -1,4 +1,4 @@
-// Convolution kernels of the CIFAR-10 CNN for gfx950 (MI355X), one image per 256-thread workgroup.
+// Convolution kernels of the CIFAR-10 CNN for gfx950 (MI355X), one image per 512-thread workgroup.
 //
 // Replaces TF's Conv2D / BiasAdd / Relu / MaxPool (+ their gradients) used by
 // /root/reference/cifar10cnn.py:106-123.
@@ -20,16 +20,11 @@
 //     weight gradients read both operands from NHWC LDS images with ds_read_b64_tr_b16 (hardware
 //     transpose) so no transposed copies are materialised; they are split-K over image groups with
 //     fp32 partial slabs reduced deterministically by the SGD kernel.
-#include "common.h"
-#include "api.h"
+#include "conv_common.h"
 
 namespace dmlc {
 
-DEV int batch_index(const DmlcIndexSrc& s, int B, int b) {
-  int row = 0;
-  if (s.counter) row = (int)(*s.counter % (int64_t)s.period);
-  return s.idx_base[row * B + b];
-}
+constexpr int NT = 512;   // 8 waves per image: 2 waves per SIMD hide each other's LDS / memory latency
 
 // ---------------------------------------------------------------------------------------------
 // conv1 input image: 24x24 crop of the uint8 NHWC image at (cy,cx), zero halo of 2, stored as
@@ -38,15 +33,13 @@ constexpr int C1_XIN = 28 * 32 * 4;        // 3584 bf16
 constexpr int C1_OUT = 576 * 64;           // 36864 bf16
 
 DEV void stage_conv1_input(bf16* xin, const uint8_t* src, int cy, int cx, int tid) {
-  for (int p = tid; p < 28 * 32; p += 256) {
+  for (int p = tid; p < 28 * 32; p += NT) {
     const int r = p >> 5, c = p & 31;
     const int iy = r - 2, ix = c - 2;
-    bf16x4 v = pack4(0.f, 0.f, 0.f, 0.f);
-    if (iy >= 0 && iy < 24 && ix >= 0 && ix < 24) {
-      const uint8_t* s = src + ((cy + iy) * 32 + (cx + ix)) * 3;
-      v = pack4((float)s[0], (float)s[1], (float)s[2], 0.f);
-    }
-    *reinterpret_cast<bf16x4*>(xin + p * 4) = v;
+    const bool ok = iy >= 0 && iy < 24 && ix >= 0 && ix < 24;
+    const uint8_t* s = src + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);     // branch-free loads
+    const float c0 = s[0], c1 = s[1], c2 = s[2];
+    *reinterpret_cast<bf16x4*>(xin + p * 4) = ok ? pack4(c0, c1, c2, 0.f) : pack4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -60,83 +53,100 @@ DEV void store_relu_tile(bf16* cout, int px, int co_base, const f32x4& acc, cons
 
 // TF-SAME 3x3/2 max-pool over an LDS image [H*W][64] (swizzled) -> global out [HO*WO][64] bf16 +
 // argmax bytes.  Padding is bottom/right only (in = 2*out), padded cells never win.
+// The inputs are post-ReLU (>= 0), so bf16 bit patterns order like their values: each candidate is a
+// 32-bit key (bits << 16 | 15 - d) and one integer max per element keeps value AND first argmax
+// (ties -> smallest d, like a strict '>' scan).  Sign bits are masked so a -0.0 ranks as 0.
 template <int H>
 DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid) {
   constexpr int HO = H / 2;
-  for (int task = tid; task < HO * HO * 8; task += 256) {
+  for (int task = tid; task < HO * HO * 8; task += NT) {
     const int q = task >> 3, c = task & 7;
     const int py = q / HO, px = q - py * HO;
-    float best[8];
-    int arg[8];
+    uint32_t key[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { best[j] = -1.f; arg[j] = 0; }
+    for (int j = 0; j < 8; ++j) key[j] = 0;
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
       const int y = 2 * py + d / 3, x = 2 * px + d % 3;
-      if (y < H && x < H) {
-        const bf16x8 v = lds_b128(cout + swz128(y * H + x, c));
+      if ((d / 3 < 2 || y < H) && (d % 3 < 2 || x < H)) {
+        const uint4 v = *reinterpret_cast<const uint4*>(cout + swz128(y * H + x, c));
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, tag = 15 - d;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = (float)v[j];
-          if (f > best[j]) { best[j] = f; arg[j] = d; }
+        for (int i = 0; i < 4; ++i) {
+          key[2 * i] = max(key[2 * i], ((wv[i] << 16) & 0x7fff0000u) | tag);
+          key[2 * i + 1] = max(key[2 * i + 1], (wv[i] & 0x7fff0000u) | tag);
         }
       }
     }
-    bf16x8 o;
-    uint64_t a = 0;
+    uint4 o;
+    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+    uint32_t alo = 0, ahi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ow[i] = (key[2 * i] >> 16) | (key[2 * i + 1] & 0xffff0000u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      o[j] = (bf16)best[j];
-      a |= (uint64_t)(best[j] > 0.f ? arg[j] : 255) << (8 * j);
+      const uint32_t arg = (key[j] >> 16) ? 15 - (key[j] & 15) : 255;
+      if (j < 4) alo |= arg << (8 * j);
+      else ahi |= arg << (8 * (j - 4));
     }
-    *reinterpret_cast<bf16x8*>(out + q * 64 + c * 8) = o;
-    *reinterpret_cast<uint64_t*>(am + q * 64 + c * 8) = a;
+    *reinterpret_cast<uint4*>(out + q * 64 + c * 8) = o;
+    *reinterpret_cast<uint2*>(am + q * 64 + c * 8) = make_uint2(alo, ahi);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void k_conv1_fwd(DmlcConv1FwdArgs a) {
+__global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* xin = reinterpret_cast<bf16*>(smem);
   bf16* cout = xin + C1_XIN;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
+  const int g = lane >> 4, li = lane & 15, cp = w & 1, pq = w >> 1;
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 
   const int img = batch_index(a.src, a.B, b);
   stage_conv1_input(xin, a.data + (size_t)img * 3072, a.cy, a.cx, tid);
 
-  // A operand: weights [64 co][160 k]; this wave owns co = 16w .. 16w+15.
-  const bf16* W = reinterpret_cast<const bf16*>(a.w) + (16 * w + li) * 160 + 8 * g;
-  bf16x8 wa[5];
+  // A operand: weights [64 co][160 k]; this wave owns co tiles 2cp, 2cp+1 (32 channels) and the
+  // pixel tiles 9pq .. 9pq+8 (of 36): every B fragment read from LDS feeds two MFMAs.
+  const bf16* W = reinterpret_cast<const bf16*>(a.w) + (32 * cp + li) * 160 + 8 * g;
+  bf16x8 wa[2][5];
 #pragma unroll
-  for (int kh = 0; kh < 5; ++kh) wa[kh] = glb_b128(W + 32 * kh);
-  float b4[4];
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) b4[i] = a.bias[16 * w + 4 * g + i];
+    for (int kh = 0; kh < 5; ++kh) wa[h][kh] = glb_b128(W + h * 16 * 160 + 32 * kh);
+  float b4[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b4[h][i] = a.bias[32 * cp + 16 * h + 4 * g + i];
   __syncthreads();
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 1);
 
-#pragma unroll 1
-  for (int ch = 0; ch < 3; ++ch) {        // 3 chunks x 12 pixel tiles of 16 = 576 pixels
-    f32x4 acc[12];
+  f32x4 acc[2][9];
 #pragma unroll
-    for (int t = 0; t < 12; ++t) acc[t] = zero4();
+  for (int t = 0; t < 9; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
 #pragma unroll
-    for (int t = 0; t < 12; ++t) {
-      const int px = (ch * 12 + t) * 16 + li;
-      const int y = px / 24, x = px - (px / 24) * 24;
-      const bf16* base = xin + (y * 32 + x + 2 * g) * 4;   // k = 8g..8g+7 -> kw = 2g,2g+1 ; ci 0..3
+  for (int t = 0; t < 9; ++t) {
+    const int px = (pq * 9 + t) * 16 + li;
+    const int y = px / 24, x = px - (px / 24) * 24;
+    const bf16* base = xin + (y * 32 + x + 2 * g) * 4;   // k = 8g..8g+7 -> kw = 2g,2g+1 ; ci 0..3
 #pragma unroll
-      for (int kh = 0; kh < 5; ++kh) {
-        const bf16* p = base + kh * 128;
-        const bf16x8 bx = cat44(*reinterpret_cast<const bf16x4*>(p), *reinterpret_cast<const bf16x4*>(p + 4));
-        acc[t] = mfma16(wa[kh], bx, acc[t]);
-      }
+    for (int kh = 0; kh < 5; ++kh) {
+      const bf16* p = base + kh * 128;
+      const bf16x8 bx = cat44(*reinterpret_cast<const bf16x4*>(p), *reinterpret_cast<const bf16x4*>(p + 4));
+      acc[0][t] = mfma16(wa[0][kh], bx, acc[0][t]);
+      acc[1][t] = mfma16(wa[1][kh], bx, acc[1][t]);
     }
-#pragma unroll
-    for (int t = 0; t < 12; ++t) store_relu_tile(cout, (ch * 12 + t) * 16 + li, 16 * w + 4 * g, acc[t], b4);
   }
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      store_relu_tile(cout, (pq * 9 + t) * 16 + li, 32 * cp + 16 * h + 4 * g, acc[h][t], b4[h]);
   __syncthreads();
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 2);
   pool_emit<24>(cout, reinterpret_cast<bf16*>(a.out) + (size_t)b * 9216, a.am + (size_t)b * 9216, tid);
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 3);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -146,17 +156,24 @@ __global__ __launch_bounds__(256, 2) void k_conv1_fwd(DmlcConv1FwdArgs a) {
 constexpr int C2_XIN = 256 * 64;
 constexpr int C2_OUT = 144 * 64;
 
-DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, f32x4 (&acc)[9], int w, int g, int li) {
-  const bf16* W = Wg + (16 * w + li) * 1600 + 8 * g;
-  int pb[9];
+// Wave w owns c_out tile (w & 3) and the pixel tiles 0..4 (w < 4) or 5..8 (w >= 4).  The weight
+// fragments of the tile live in registers, streamed from L2 one kh ahead; every B fragment is one
+// ds_read_b128 of the swizzled LDS image.  (Blocking two c_out tiles per wave halves the LDS reads
+// but doubles the per-block weight stream from L2, which measured 1.6x slower: L2->CU bandwidth,
+// not LDS, is the tighter limit for a 204 KB weight matrix re-read by every image's block.)
+template <int NTILE>
+DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, f32x4 (&acc)[NTILE], int t0, int ct, int g,
+                    int li) {
+  const bf16* W = Wg + (16 * ct + li) * 1600 + 8 * g;
+  int pb[NTILE];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int px = 16 * t + li;
+  for (int t = 0; t < NTILE; ++t) {
+    const int px = 16 * (t0 + t) + li;
     const int y = px / 12;
     pb[t] = y * 16 + (px - y * 12);
   }
 #pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t] = zero4();
+  for (int t = 0; t < NTILE; ++t) acc[t] = zero4();
   bf16x8 wc[10], wn[10];
 #pragma unroll
   for (int j = 0; j < 10; ++j) wc[j] = glb_b128(W + j * 32);
@@ -171,7 +188,7 @@ DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, f32x4 (&acc)[9
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
+        for (int t = 0; t < NTILE; ++t) {
           const bf16x8 bx = lds_b128(xin + swz128(pb[t] + kh * 16 + kw, 4 * s + g));
           acc[t] = mfma16(wc[kw * 2 + s], bx, acc[t]);
         }
@@ -184,249 +201,110 @@ DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, f32x4 (&acc)[9
   }
 }
 
-__global__ __launch_bounds__(256, 2) void k_conv2_fwd(DmlcConv2FwdArgs a) {
+// fn(co_tile, px_tile, acc) for every finished 16x16 output tile of this wave.
+template <class F>
+DEV void conv2_tiles(const bf16* Wg, const bf16* xin, int w, int g, int li, F&& fn) {
+  if (w < 4) {
+    f32x4 acc[5];
+    conv2_core<5>(Wg, xin, acc, 0, w & 3, g, li);
+#pragma unroll
+    for (int t = 0; t < 5; ++t) fn(w & 3, t, acc[t]);
+  } else {
+    f32x4 acc[4];
+    conv2_core<4>(Wg, xin, acc, 5, w & 3, g, li);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) fn(w & 3, 5 + t, acc[t]);
+  }
+}
+
+__global__ __launch_bounds__(NT, 1) void k_conv2_fwd(DmlcConv2FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* xin = reinterpret_cast<bf16*>(smem);
   bf16* cout = xin + C2_XIN;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const bf16* in = reinterpret_cast<const bf16*>(a.in) + (size_t)b * 9216;
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 0);
 
-  for (int s = tid; s < 2048; s += 256) {
-    const int pix = s >> 3, c = s & 7;
+  uint4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int s = tid + i * NT, pix = s >> 3, c = s & 7;
     const int iy = (pix >> 4) - 2, ix = (pix & 15) - 2;
-    bf16x8 v = {};
-    if (iy >= 0 && iy < 12 && ix >= 0 && ix < 12) v = glb_b128(in + (iy * 12 + ix) * 64 + c * 8);
-    *reinterpret_cast<bf16x8*>(xin + swz128(pix, c)) = v;
+    v[i] = load_sel(reinterpret_cast<const uint4*>(in + (iy * 12 + ix) * 64 + c * 8), reinterpret_cast<const uint4*>(in),
+                    iy >= 0 && iy < 12 && ix >= 0 && ix < 12);
   }
-  float b4[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) b4[i] = a.bias[16 * w + 4 * g + i];
+  for (int i = 0; i < 4; ++i) {
+    const int s = tid + i * NT;
+    *reinterpret_cast<uint4*>(xin + swz128(s >> 3, s & 7)) = v[i];
+  }
+  float b4[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b4[h][i] = a.bias[16 * (w & 3) + 4 * g + i];
   __syncthreads();
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 1);
 
-  f32x4 acc[9];
-  conv2_core(reinterpret_cast<const bf16*>(a.w), xin, acc, w, g, li);
-#pragma unroll
-  for (int t = 0; t < 9; ++t) store_relu_tile(cout, 16 * t + li, 16 * w + 4 * g, acc[t], b4);
+  conv2_tiles(reinterpret_cast<const bf16*>(a.w), xin, w, g, li, [&](int ct, int t, const f32x4& acc) {
+    store_relu_tile(cout, 16 * t + li, 16 * ct + 4 * g, acc, b4[0]);
+  });
   __syncthreads();
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 2);
   pool_emit<12>(cout, reinterpret_cast<bf16*>(a.out) + (size_t)b * 2304, a.am + (size_t)b * 2304, tid);
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 3);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Pool/ReLU backward as a gather: grad at conv pixel (y,x) = sum over the pool windows (py,px) that
-// contain it and whose argmax is (y-2py, x-2px) of dpool[py][px].  HO = pooled size.
-template <int HO>
-DEV void pool_bwd_gather(const bf16* __restrict__ dp, const uint8_t* __restrict__ am, int y, int x, int c,
-                         float (&accv)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) accv[j] = 0.f;
-  const int py0 = max(0, (y - 1) >> 1), py1 = min(HO - 1, y >> 1);
-  const int px0 = max(0, (x - 1) >> 1), px1 = min(HO - 1, x >> 1);
-  for (int py = py0; py <= py1; ++py) {
-    for (int px = px0; px <= px1; ++px) {
-      const int d = (y - 2 * py) * 3 + (x - 2 * px);
-      const int o = (py * HO + px) * 64 + c * 8;
-      const uint64_t av = *reinterpret_cast<const uint64_t*>(am + o);
-      const bf16x8 dv = glb_b128(dp + o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if ((int)((av >> (8 * j)) & 0xff) == d) accv[j] += (float)dv[j];
-    }
-  }
-}
-
-// Reduce per-thread channel sums (thread's chunk = tid & 7) over the workgroup: red[64] result.
-DEV void block_chunk_sum(float (&v)[8], float* red /*[4][64]*/, int tid) {
-  const int lane = tid & 63, w = tid >> 6;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float s = v[j];
-    s += __shfl_xor(s, 8);
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
-    v[j] = s;
-  }
-  if (lane < 8) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[w * 64 + lane * 8 + j] = v[j];
-  }
-}
-
-__global__ __launch_bounds__(256, 2) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
+__global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* dyp = reinterpret_cast<bf16*>(smem);
   bf16* outs = dyp + C2_XIN;
-  float* red = reinterpret_cast<float*>(outs + C2_OUT);
+  bf16* dp2 = outs + C2_OUT;                                    // [36][64] staged pool2 grad
+  uint8_t* am2 = reinterpret_cast<uint8_t*>(dp2 + 2304);        // [36][64] staged argmax
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const bf16* dp2 = reinterpret_cast<const bf16*>(a.dp2) + (size_t)b * 2304;
-  const uint8_t* am2 = a.am2 + (size_t)b * 2304;
+  DMLC_STAMP(DMLC_TK_DGRAD, 0);
+  stage16<288>(dp2, reinterpret_cast<const bf16*>(a.dp2) + (size_t)b * 2304, tid);
+  stage16<144>(am2, a.am2 + (size_t)b * 2304, tid);
   bf16* dy2 = reinterpret_cast<bf16*>(a.dy2) + (size_t)b * 9216;
 
   // halo of the padded 16x16 grad image
-  for (int s = tid; s < 2048; s += 256) {
+  for (int s = tid; s < 2048; s += NT) {
     const int pix = s >> 3, c = s & 7;
     const int r = pix >> 4, col = pix & 15;
     if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(dyp + swz128(pix, c)) = bf16x8{};
   }
-  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int task = tid; task < 1152; task += 256) {
-    const int p = task >> 3, c = task & 7;
-    const int y = p / 12, x = p - (p / 12) * 12;
-    float accv[8];
-    pool_bwd_gather<6>(dp2, am2, y, x, c, accv);
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { o[j] = (bf16)accv[j]; bsum[j] += (float)o[j]; }
-    *reinterpret_cast<bf16x8*>(dyp + swz128((y + 2) * 16 + x + 2, c)) = o;
-    *reinterpret_cast<bf16x8*>(dy2 + p * 64 + c * 8) = o;
-  }
-  block_chunk_sum(bsum, red, tid);
   __syncthreads();
-  if (tid < 64) a.dbias_part[b * 64 + tid] = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+  DMLC_STAMP(DMLC_TK_DGRAD, 1);
+  for (int task = tid; task < 36 * 8; task += NT) {
+    const int win = task >> 3, c = task & 7, py = win / 6, px = win - py * 6;
+    float o[4][8];
+    pool_bwd_2x2<6>(dp2, am2, py, px, c, o);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
+      const bf16x8 v = to_bf16x8(o[k]);
+      *reinterpret_cast<bf16x8*>(dyp + swz128((y + 2) * 16 + x + 2, c)) = v;
+      *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8) = v;
+    }
+  }
+  __syncthreads();
+  DMLC_STAMP(DMLC_TK_DGRAD, 2);
 
-  f32x4 acc[9];
-  conv2_core(reinterpret_cast<const bf16*>(a.wd), dyp, acc, w, g, li);
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int px = 16 * t + li, cb = 16 * w + 4 * g;
-    const bf16x4 v = pack4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+  conv2_tiles(reinterpret_cast<const bf16*>(a.wd), dyp, w, g, li, [&](int ct, int t, const f32x4& acc) {
+    const int px = 16 * t + li, cb = 16 * ct + 4 * g;
+    const bf16x4 v = pack4(acc[0], acc[1], acc[2], acc[3]);
     *reinterpret_cast<bf16x4*>(outs + swz128(px, cb >> 3) + ((cb >> 2) & 1) * 4) = v;
-  }
+  });
   __syncthreads();
+  DMLC_STAMP(DMLC_TK_DGRAD, 3);
   bf16* dp1 = reinterpret_cast<bf16*>(a.dp1) + (size_t)b * 9216;
-  for (int s = tid; s < 1152; s += 256) {
+  for (int s = tid; s < 1152; s += NT) {
     const int p = s >> 3, c = s & 7;
     *reinterpret_cast<bf16x8*>(dp1 + p * 64 + c * 8) = lds_b128(outs + swz128(p, c));
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Weight gradients.  Reduction index r = output pixel; both operands are NHWC LDS images read
-// with the hardware transpose (lane 4q+p of a 16-lane group addresses row r = rb+q, cols 4p..4p+3).
-constexpr int W2_XT = 12 * 16 * 32;     // conv2 x rows kh..kh+11, 16 cols, 32 ci (one half)
-constexpr int W2_DY = 160 * 64;         // conv2 dy, 144 pixels + 16 zero rows
-constexpr int WG_LDS_BYTES = (C1_XIN + C1_OUT) * 2 + 4 * 64 * 4;
-
-DEV void conv2_wgrad_block(const DmlcConvWgradArgs& a, int blk, char* smem) {
-  bf16* xt = reinterpret_cast<bf16*>(smem);
-  bf16* dyt = xt + W2_XT;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int kh = blk % 5, hh = (blk / 5) & 1, grp = blk / 10;
-  const int b0 = grp * a.B / a.g2, b1 = (grp + 1) * a.B / a.g2;
-
-  f32x4 acc[5][2];
-#pragma unroll
-  for (int kw = 0; kw < 5; ++kw) { acc[kw][0] = zero4(); acc[kw][1] = zero4(); }
-
-  for (int b = b0; b < b1; ++b) {
-    const bf16* x = reinterpret_cast<const bf16*>(a.p1) + (size_t)b * 9216;
-    const bf16* dy = reinterpret_cast<const bf16*>(a.dy2) + (size_t)b * 9216;
-    for (int s = tid; s < 12 * 16 * 4; s += 256) {
-      const int pix = s >> 2, c = s & 3;
-      const int iy = kh + (pix >> 4) - 2, ix = (pix & 15) - 2;
-      bf16x8 v = {};
-      if (iy >= 0 && iy < 12 && ix >= 0 && ix < 12) v = glb_b128(x + (iy * 12 + ix) * 64 + hh * 32 + c * 8);
-      *reinterpret_cast<bf16x8*>(xt + pix * 32 + c * 8) = v;
-    }
-    for (int s = tid; s < 160 * 8; s += 256) {
-      const int pix = s >> 3, c = s & 7;
-      bf16x8 v = {};
-      if (pix < 144) v = glb_b128(dy + pix * 64 + c * 8);
-      *reinterpret_cast<bf16x8*>(dyt + pix * 64 + c * 8) = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-      const int rA = 32 * s + 8 * g + q, rB = rA + 4;
-      const bf16x8 bf = tr_frag(dyt + rA * 64 + 16 * w + 4 * p, dyt + rB * 64 + 16 * w + 4 * p);
-      const int cA = min(rA, 143), cB = min(rB, 143);
-      const int yA = cA / 12, yB = cB / 12;
-      const int pA = yA * 16 + cA - yA * 12, pB = yB * 16 + cB - yB * 12;
-#pragma unroll
-      for (int kw = 0; kw < 5; ++kw) {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-          const bf16x8 af = tr_frag(xt + (pA + kw) * 32 + 16 * mt + 4 * p, xt + (pB + kw) * 32 + 16 * mt + 4 * p);
-          acc[kw][mt] = mfma16(af, bf, acc[kw][mt]);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  float* out = a.part2 + (size_t)grp * 1600 * 64;
-#pragma unroll
-  for (int kw = 0; kw < 5; ++kw)
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int krow = (kh * 5 + kw) * 64 + hh * 32 + 16 * mt + 4 * g + i;
-        out[krow * 64 + 16 * w + li] = acc[kw][mt][i];
-      }
-}
-
-DEV void conv1_wgrad_block(const DmlcConvWgradArgs& a, int grp, char* smem) {
-  bf16* xin = reinterpret_cast<bf16*>(smem);
-  bf16* dyt = xin + C1_XIN;
-  float* red = reinterpret_cast<float*>(dyt + C1_OUT);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int b0 = grp * a.B / a.g1, b1 = (grp + 1) * a.B / a.g1;
-
-  f32x4 acc[10];
-#pragma unroll
-  for (int mt = 0; mt < 10; ++mt) acc[mt] = zero4();
-  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-
-  for (int b = b0; b < b1; ++b) {
-    const int img = batch_index(a.src, a.B, b);
-    stage_conv1_input(xin, a.data + (size_t)img * 3072, a.cy, a.cx, tid);
-    const bf16* dp1 = reinterpret_cast<const bf16*>(a.dp1) + (size_t)b * 9216;
-    const uint8_t* am1 = a.am1 + (size_t)b * 9216;
-    for (int task = tid; task < 576 * 8; task += 256) {
-      const int pp = task >> 3, c = task & 7;
-      const int y = pp / 24, x = pp - (pp / 24) * 24;
-      float accv[8];
-      pool_bwd_gather<12>(dp1, am1, y, x, c, accv);
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { o[j] = (bf16)accv[j]; bsum[j] += (float)o[j]; }
-      *reinterpret_cast<bf16x8*>(dyt + pp * 64 + c * 8) = o;
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int s = 0; s < 18; ++s) {
-      const int rA = 32 * s + 8 * g + q, rB = rA + 4;
-      const bf16x8 bf = tr_frag(dyt + rA * 64 + 16 * w + 4 * p, dyt + rB * 64 + 16 * w + 4 * p);
-      const int yA = rA / 24, yB = rB / 24;
-      const int xA = rA - yA * 24, xB = rB - yB * 24;
-#pragma unroll
-      for (int mt = 0; mt < 10; ++mt) {
-        const int kh = mt >> 1, kw0 = 4 * (mt & 1);
-        const bf16x8 af = tr_frag(xin + ((yA + kh) * 32 + xA + kw0 + p) * 4,
-                                  xin + ((yB + kh) * 32 + xB + kw0 + p) * 4);
-        acc[mt] = mfma16(af, bf, acc[mt]);
-      }
-    }
-    __syncthreads();
-  }
-  float* out = a.part1 + (size_t)grp * 160 * 64;
-#pragma unroll
-  for (int mt = 0; mt < 10; ++mt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) out[(16 * mt + 4 * g + i) * 64 + 16 * w + li] = acc[mt][i];
-  block_chunk_sum(bsum, red, tid);
-  __syncthreads();
-  if (tid < 64) a.partb1[grp * 64 + tid] = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
-}
-
-__global__ __launch_bounds__(256, 2) void k_conv_wgrad(DmlcConvWgradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int blk = blockIdx.x;
-  if (blk < 10 * a.g2) conv2_wgrad_block(a, blk, smem);
-  else conv1_wgrad_block(a, blk - 10 * a.g2, smem);
+  DMLC_STAMP(DMLC_TK_DGRAD, 4);
 }
 
 }  // namespace dmlc
@@ -441,7 +319,7 @@ void allow_lds(const void* f, size_t bytes, bool& done) {
     done = true;
   }
 }
-bool g_c1 = false, g_wg = false;
+bool g_c1 = false;
 }  // namespace
 
 extern "C" {
@@ -449,26 +327,19 @@ extern "C" {
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s) {
   const size_t lds = (C1_XIN + C1_OUT) * 2;
   allow_lds(reinterpret_cast<const void*>(&k_conv1_fwd), lds, g_c1);
-  hipLaunchKernelGGL(k_conv1_fwd, dim3(a->B), dim3(256), lds, s, *a);
+  hipLaunchKernelGGL(k_conv1_fwd, dim3(a->B), dim3(NT), lds, s, *a);
   return hipGetLastError();
 }
 
 hipError_t dmlc_conv2_fwd(const DmlcConv2FwdArgs* a, hipStream_t s) {
   const size_t lds = (C2_XIN + C2_OUT) * 2;
-  hipLaunchKernelGGL(k_conv2_fwd, dim3(a->B), dim3(256), lds, s, *a);
+  hipLaunchKernelGGL(k_conv2_fwd, dim3(a->B), dim3(NT), lds, s, *a);
   return hipGetLastError();
 }
 
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s) {
-  const size_t lds = (C2_XIN + C2_OUT) * 2 + 4 * 64 * 4;
-  hipLaunchKernelGGL(k_conv2_dgrad, dim3(a->B), dim3(256), lds, s, *a);
-  return hipGetLastError();
-}
-
-hipError_t dmlc_conv_wgrad(const DmlcConvWgradArgs* a, hipStream_t s) {
-  static_assert((W2_XT + W2_DY) * 2 <= WG_LDS_BYTES, "conv2 wgrad staging must fit");
-  allow_lds(reinterpret_cast<const void*>(&k_conv_wgrad), WG_LDS_BYTES, g_wg);
-  hipLaunchKernelGGL(k_conv_wgrad, dim3(10 * a->g2 + a->g1), dim3(256), WG_LDS_BYTES, s, *a);
+  const size_t lds = (C2_XIN + C2_OUT) * 2 + 2304 * 3;
+  hipLaunchKernelGGL(k_conv2_dgrad, dim3(a->B), dim3(NT), lds, s, *a);
   return hipGetLastError();
 }
 

@@ -8,43 +8,51 @@
 //   * m/n-major operands (the weight-gradient case, where the reduction runs over the batch) are
 //     staged untransposed as [32 k][rows] and read with the gfx950 hardware transpose
 //     ds_read_b64_tr_b16 — no transposed copy of any activation is ever written.
-// 64x64 tiles, 4 waves in 2x2, each wave 2x2 MFMA 16x16x32 tiles, register-staged double buffer,
-// optional split-K into fp32 partial slabs (reduced by the consumer kernel's prologue).
+// 64x64 tiles, 4 waves in 2x2, each wave 2x2 MFMA 16x16x32 tiles; K is staged in 128-deep chunks
+// (4 k-steps, 8 x 16-B loads per thread in flight) with the next chunk's loads issued before the
+// current chunk's MFMAs (register-staged double buffer); optional split-K into fp32 partial slabs
+// (reduced by the consumer kernel's prologue).
 #include "common.h"
 #include "api.h"
 
 namespace dmlc {
 
-constexpr int KC_LD = 40;   // k-major tile row stride (bf16): 80 B rows, 16-B aligned
-constexpr int MC_LD = 72;   // m-major tile row stride (bf16): 144 B rows, 16-B aligned
-constexpr int TILE_ELEMS = 64 * KC_LD > 32 * MC_LD ? 64 * KC_LD : 32 * MC_LD;
+constexpr int KC = 128;                     // K chunk staged per phase (4 MFMA k-steps)
+constexpr int KC_LD = KC + 8;               // k-major tile row stride (bf16): 272-B rows, b128 reads conflict-free
+constexpr int MC_LD = 72;                   // m-major tile row stride (bf16): 144-B rows, tr reads conflict-free
+constexpr int TILE_ELEMS = 64 * KC_LD > KC * MC_LD ? 64 * KC_LD : KC * MC_LD;
+constexpr int PIECES = 64 * KC / 8 / 256;   // 16-byte pieces per thread per operand per chunk (4)
+constexpr size_t GEMM_LDS = (size_t)2 * 2 * TILE_ELEMS * 2;
 
-struct Stage {
-  bf16x8 v;
-  int dst;
+// One operand's share of a 64-row x KC-deep chunk, held in registers between the global load and the
+// LDS store (so the next chunk's loads are in flight while the current chunk is multiplied).
+struct Chunk {
+  uint4 v[PIECES];
+  MDEV void load(const bf16* __restrict__ X, int ld, int kmajor, int R, int K, int r0, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const int c = tid + i * 256;
+      int gr, gk;
+      if (kmajor) { gr = r0 + (c >> 4); gk = k0 + 8 * (c & 15); }
+      else { gk = k0 + (c >> 3); gr = r0 + 8 * (c & 7); }
+      v[i] = load_sel(reinterpret_cast<const uint4*>(kmajor ? X + (size_t)gr * ld + gk : X + (size_t)gk * ld + gr),
+                      reinterpret_cast<const uint4*>(X), gr < R && gk < K);
+    }
+  }
+  MDEV void store(bf16* sm, int kmajor, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const int c = tid + i * 256;
+      const int off = kmajor ? (c >> 4) * KC_LD + 8 * (c & 15) : (c >> 3) * MC_LD + 8 * (c & 7);
+      *reinterpret_cast<uint4*>(sm + off) = v[i];
+    }
+  }
 };
 
-// Load one 16-byte piece of a 64-row x 32-k operand tile into registers.
-DEV Stage load_piece(const bf16* __restrict__ X, int ld, int kmajor, int R, int K, int r0, int k0, int tid) {
-  Stage st;
-  if (kmajor) {
-    const int row = tid >> 2, kc = tid & 3;
-    const int gr = r0 + row, gk = k0 + 8 * kc;
-    st.v = (gr < R && gk < K) ? glb_b128(X + (size_t)gr * ld + gk) : bf16x8{};
-    st.dst = row * KC_LD + 8 * kc;
-  } else {
-    const int kk = tid >> 3, rc = tid & 7;
-    const int gk = k0 + kk, gr = r0 + 8 * rc;
-    st.v = (gk < K && gr < R) ? glb_b128(X + (size_t)gk * ld + gr) : bf16x8{};
-    st.dst = kk * MC_LD + 8 * rc;
-  }
-  return st;
-}
-
-DEV bf16x8 frag(const bf16* sm, int kmajor, int rr0, int g, int li) {
-  if (kmajor) return lds_b128(sm + (rr0 + li) * KC_LD + 8 * g);
+DEV bf16x8 frag(const bf16* sm, int kmajor, int rr0, int kk, int g, int li) {
+  if (kmajor) return lds_b128(sm + (rr0 + li) * KC_LD + kk * 32 + 8 * g);
   const int q = li >> 2, p = li & 3;
-  return tr_frag(sm + (8 * g + q) * MC_LD + rr0 + 4 * p, sm + (8 * g + 4 + q) * MC_LD + rr0 + 4 * p);
+  return tr_frag(sm + (kk * 32 + 8 * g + q) * MC_LD + rr0 + 4 * p, sm + (kk * 32 + 8 * g + 4 + q) * MC_LD + rr0 + 4 * p);
 }
 
 DEV void colsum_block(const DmlcGemmProblem& P, int local, float* red) {
@@ -53,8 +61,10 @@ DEV void colsum_block(const DmlcGemmProblem& P, int local, float* red) {
   const int col = local * 64 + (tid & 63);
   const bf16* A = reinterpret_cast<const bf16*>(P.A);
   float s = 0.f;
-  if (col < P.M)
+  if (col < P.M) {
+#pragma unroll 8
     for (int k = tid >> 6; k < P.K; k += 4) s += (float)A[(size_t)k * P.lda + col];
+  }
   red[tid] = s;
   __syncthreads();
   if (tid < 64 && col < P.M && col < P.nvalid)
@@ -62,14 +72,16 @@ DEV void colsum_block(const DmlcGemmProblem& P, int local, float* red) {
 }
 
 __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
-  __shared__ __attribute__((aligned(16))) bf16 sA[2][TILE_ELEMS];
-  __shared__ __attribute__((aligned(16))) bf16 sB[2][TILE_ELEMS];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* sA = reinterpret_cast<bf16*>(smem);             // [2][TILE_ELEMS]
+  bf16* sB = sA + 2 * TILE_ELEMS;                        // [2][TILE_ELEMS]
   const int blk = blockIdx.x;
   int pi = 0;
   while (pi + 1 < G.nprob && blk >= G.p[pi + 1].block_start) ++pi;
   const DmlcGemmProblem P = G.p[pi];
   const int local = blk - P.block_start;
-  if (P.c_mode == 3) { colsum_block(P, local, reinterpret_cast<float*>(&sA[0][0])); return; }
+  DMLC_STAMP(DMLC_TK_GEMM, 0);
+  if (P.c_mode == 3) { colsum_block(P, local, reinterpret_cast<float*>(smem)); return; }
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -78,7 +90,7 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
   const int m0 = (t / P.tiles_n) * 64, n0 = (t % P.tiles_n) * 64;
   const int ksteps = (P.K + 31) >> 5;
   const int per = (ksteps + P.ksplit - 1) / P.ksplit;
-  const int ks0 = split * per, ks1 = min(ksteps, ks0 + per);
+  const int kbeg = split * per * 32, kend = min(P.K, (split * per + per) * 32);
   const bf16* A = reinterpret_cast<const bf16*>(P.A);
   const bf16* B = reinterpret_cast<const bf16*>(P.B);
   const int wm = w >> 1, wn = w & 1;
@@ -87,35 +99,36 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) { acc[i][0] = zero4(); acc[i][1] = zero4(); }
 
-  if (ks0 < ks1) {
-    Stage pa = load_piece(A, P.lda, P.a_kmajor, P.M, P.K, m0, ks0 * 32, tid);
-    Stage pb = load_piece(B, P.ldb, P.b_kmajor, P.N, P.K, n0, ks0 * 32, tid);
-    *reinterpret_cast<bf16x8*>(&sA[0][pa.dst]) = pa.v;
-    *reinterpret_cast<bf16x8*>(&sB[0][pb.dst]) = pb.v;
-    __syncthreads();
+  if (kbeg < kend) {
+    Chunk ca, cb;
+    ca.load(A, P.lda, P.a_kmajor, P.M, kend, m0, kbeg, tid);
+    cb.load(B, P.ldb, P.b_kmajor, P.N, kend, n0, kbeg, tid);
     int buf = 0;
-    for (int ks = ks0; ks < ks1; ++ks) {
-      const bool more = ks + 1 < ks1;
-      if (more) {
-        pa = load_piece(A, P.lda, P.a_kmajor, P.M, P.K, m0, (ks + 1) * 32, tid);
-        pb = load_piece(B, P.ldb, P.b_kmajor, P.N, P.K, n0, (ks + 1) * 32, tid);
-      }
-      const bf16x8 a0 = frag(sA[buf], P.a_kmajor, 32 * wm, g, li);
-      const bf16x8 a1 = frag(sA[buf], P.a_kmajor, 32 * wm + 16, g, li);
-      const bf16x8 b0 = frag(sB[buf], P.b_kmajor, 32 * wn, g, li);
-      const bf16x8 b1 = frag(sB[buf], P.b_kmajor, 32 * wn + 16, g, li);
-      acc[0][0] = mfma16(a0, b0, acc[0][0]);
-      acc[0][1] = mfma16(a0, b1, acc[0][1]);
-      acc[1][0] = mfma16(a1, b0, acc[1][0]);
-      acc[1][1] = mfma16(a1, b1, acc[1][1]);
-      if (more) {
-        *reinterpret_cast<bf16x8*>(&sA[buf ^ 1][pa.dst]) = pa.v;
-        *reinterpret_cast<bf16x8*>(&sB[buf ^ 1][pb.dst]) = pb.v;
+    for (int k0 = kbeg; k0 < kend; k0 += KC) {
+      bf16* a_s = sA + buf * TILE_ELEMS;
+      bf16* b_s = sB + buf * TILE_ELEMS;
+      ca.store(a_s, P.a_kmajor, tid);
+      cb.store(b_s, P.b_kmajor, tid);
+      if (k0 + KC < kend) {                    // next chunk in flight during this chunk's MFMAs
+        ca.load(A, P.lda, P.a_kmajor, P.M, kend, m0, k0 + KC, tid);
+        cb.load(B, P.ldb, P.b_kmajor, P.N, kend, n0, k0 + KC, tid);
       }
       __syncthreads();
-      buf ^= 1;
-    }
+      const int nk = min(KC, kend - k0 + 31) >> 5;
+      for (int kk = 0; kk < nk; ++kk) {
+        const bf16x8 a0 = frag(a_s, P.a_kmajor, 32 * wm, kk, g, li);
+        const bf16x8 a1 = frag(a_s, P.a_kmajor, 32 * wm + 16, kk, g, li);
+        const bf16x8 b0 = frag(b_s, P.b_kmajor, 32 * wn, kk, g, li);
+        const bf16x8 b1 = frag(b_s, P.b_kmajor, 32 * wn + 16, kk, g, li);
+        acc[0][0] = mfma16(a0, b0, acc[0][0]);
+        acc[0][1] = mfma16(a0, b1, acc[0][1]);
+        acc[1][0] = mfma16(a1, b0, acc[1][0]);
+        acc[1][1] = mfma16(a1, b1, acc[1][1]);
+      }
+      buf ^= 1;                                 // the other buffer was last read two chunks ago,
+    }                                           // behind this chunk's barrier
   }
+  DMLC_STAMP(DMLC_TK_GEMM, 1);
 
   // epilogue: acc[i][j] holds C[m0+32wm+16i+4g+r][n0+32wn+16j+li]
 #pragma unroll
@@ -140,6 +153,7 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
         else reinterpret_cast<bf16*>(P.C)[(size_t)m * P.ldc + n] = (bf16)v;
       }
     }
+  DMLC_STAMP(DMLC_TK_GEMM, 2);
 }
 
 }  // namespace dmlc
@@ -159,6 +173,12 @@ extern "C" hipError_t dmlc_gemm_grouped(DmlcGemmGroup* G, hipStream_t s) {
   }
   G->nblocks = blocks;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_gemm_grouped, dim3(blocks), dim3(256), 0, s, *G);
+  static bool lds_set = false;
+  if (!lds_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_grouped),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GEMM_LDS);
+    lds_set = true;
+  }
+  hipLaunchKernelGGL(k_gemm_grouped, dim3(blocks), dim3(256), GEMM_LDS, s, *G);
   return hipGetLastError();
 }

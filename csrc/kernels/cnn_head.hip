@@ -4,15 +4,18 @@
 // Replaces /root/reference/cifar10cnn.py:130-176 (full1..full3, cifar_loss, batch_accuracy) and the
 // corresponding autodiff ops (SURVEY.md §2.B N7/N8/N10-N12, §2.C xent10_fwd_bwd + linear_bwd_dx).
 //
-// Rows-parallel: 16 batch rows per 256-thread workgroup; everything per row stays in LDS.  Every
+// Rows-parallel: 16 batch rows per workgroup of 16 waves; everything per row stays in LDS.  Every
 // product is computed TRANSPOSED (C[feature][row]) so the weight fragment streams from L2 and each
-// lane ends up with 4 consecutive features of one row.  Weight *gradients* of fc1/fc2/fc3 are NOT
-// computed here (they need a reduction over the whole batch): the grouped GEMM kernel does them.
+// lane ends up with 4 consecutive features of one row.  The weight fragments of a wave's output
+// tiles are loaded up front (fc2 at entry, behind the fc1 reduction; fc2^T right after the fc2
+// MFMAs, behind the loss phase), so each phase pays at most one exposed L2 latency.  Weight
+// *gradients* of fc1/fc2/fc3 need a reduction over the whole batch: the grouped GEMM kernel does them.
 #include "common.h"
 #include "api.h"
 
 namespace dmlc {
 
+constexpr int HT = 1024;     // 16 waves
 constexpr int H1_LD = 392;   // 784-B rows: 16-B aligned, rows land on distinct bank slots
 constexpr int H2_LD = 200;   // 400-B rows
 constexpr int DL_LD = 40;    // 80-B rows (k padded to 32 with zeros)
@@ -23,7 +26,12 @@ DEV int head_index(const DmlcIndexSrc& s, int B, int b) {
   return s.idx_base[row * B + b];
 }
 
-__global__ __launch_bounds__(256) void k_head(DmlcHeadArgs a) {
+DEV bf16x4 relu_mask4(const f32x4& acc, const bf16x4& h) {
+  return pack4((float)h[0] > 0.f ? acc[0] : 0.f, (float)h[1] > 0.f ? acc[1] : 0.f,
+               (float)h[2] > 0.f ? acc[2] : 0.f, (float)h[3] > 0.f ? acc[3] : 0.f);
+}
+
+__global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 h1s[16 * H1_LD];
   __shared__ __attribute__((aligned(16))) bf16 h2s[16 * H2_LD];
   __shared__ __attribute__((aligned(16))) bf16 dh2s[16 * H2_LD];
@@ -32,47 +40,84 @@ __global__ __launch_bounds__(256) void k_head(DmlcHeadArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int r0 = blockIdx.x * 16;
+  DMLC_STAMP(DMLC_TK_HEAD, 0);
 
-  // (a) h1 = relu(sum_s part[s] + b1)
-  for (int e = tid; e < 16 * 96; e += 256) {
-    const int r = e / 96, n = (e - r * 96) * 4;
-    float4 s = *reinterpret_cast<const float4*>(a.b1 + n);
-    for (int sp = 0; sp < a.nsplit; ++sp) {
-      const float4 v = *reinterpret_cast<const float4*>(a.h1part + ((size_t)sp * a.B + r0 + r) * 384 + n);
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-    }
-    const bf16x4 o = pack4(fmaxf(s.x, 0.f), fmaxf(s.y, 0.f), fmaxf(s.z, 0.f), fmaxf(s.w, 0.f));
-    *reinterpret_cast<bf16x4*>(h1s + r * H1_LD + n) = o;
-    if (a.train) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.h1) + (size_t)(r0 + r) * 384 + n) = o;
+  // fc2 weight fragments of this wave's output tile (waves 0..11: features 16w..16w+15), in flight
+  // while the fc1 partial sums are reduced
+  bf16x8 w2f[12];
+  if (w < 12) {
+    const bf16* W = reinterpret_cast<const bf16*>(a.w2t) + (16 * w + li) * 384 + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < 12; ++ks) w2f[ks] = glb_b128(W + ks * 32);
   }
-  __syncthreads();
 
-  // (b) h2 = relu(h1 W2 + b2): C[n][r] = sum_k W2t[n][k] h1[r][k]; wave w: n-tiles w, w+4, w+8
+  // (a) h1 = relu(sum_s part[s] + b1): 16 x 96 float4, at most 2 per thread, all loads in flight
   {
-    const bf16* W = reinterpret_cast<const bf16*>(a.w2t);
-    f32x4 acc[3] = {zero4(), zero4(), zero4()};
+    float4 acc[2];
+    int e[2];
 #pragma unroll
-    for (int ks = 0; ks < 12; ++ks) {
-      const bf16x8 bx = lds_b128(h1s + li * H1_LD + ks * 32 + 8 * g);
+    for (int u = 0; u < 2; ++u) {
+      e[u] = tid + u * HT;
+      const int ec = e[u] < 16 * 96 ? e[u] : 0;               // branch-free: clamp, discard later
+      const int r = ec / 96, n = (ec - r * 96) * 4;
+      acc[u] = *reinterpret_cast<const float4*>(a.b1 + n);
+      const float* hp = a.h1part + (size_t)(r0 + r) * 384 + n;
+      const size_t sstride = (size_t)a.B * 384;
+      int sp = 0;
+      for (; sp + 4 <= a.nsplit; sp += 4) {
+        float4 v[4];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int nt = w + 4 * j;
-        acc[j] = mfma16(glb_b128(W + (16 * nt + li) * 384 + ks * 32 + 8 * g), bx, acc[j]);
+        for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(hp + (sp + k) * sstride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { acc[u].x += v[k].x; acc[u].y += v[k].y; acc[u].z += v[k].z; acc[u].w += v[k].w; }
+      }
+      for (; sp < a.nsplit; ++sp) {
+        const float4 v = *reinterpret_cast<const float4*>(hp + sp * sstride);
+        acc[u].x += v.x; acc[u].y += v.y; acc[u].z += v.z; acc[u].w += v.w;
       }
     }
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int n = 16 * (w + 4 * j) + 4 * g;
-      const bf16x4 o = pack4(fmaxf(acc[j][0] + a.b2[n], 0.f), fmaxf(acc[j][1] + a.b2[n + 1], 0.f),
-                             fmaxf(acc[j][2] + a.b2[n + 2], 0.f), fmaxf(acc[j][3] + a.b2[n + 3], 0.f));
-      *reinterpret_cast<bf16x4*>(h2s + li * H2_LD + n) = o;
-      if (a.train) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.h2) + (size_t)(r0 + li) * 192 + n) = o;
+    for (int u = 0; u < 2; ++u) {
+      if (e[u] < 16 * 96) {
+        const int r = e[u] / 96, n = (e[u] - r * 96) * 4;
+        const bf16x4 o = pack4(fmaxf(acc[u].x, 0.f), fmaxf(acc[u].y, 0.f), fmaxf(acc[u].z, 0.f), fmaxf(acc[u].w, 0.f));
+        *reinterpret_cast<bf16x4*>(h1s + r * H1_LD + n) = o;
+        if (a.train) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.h1) + (size_t)(r0 + r) * 384 + n) = o;
+      }
     }
   }
   __syncthreads();
+  DMLC_STAMP(DMLC_TK_HEAD, 1);
 
-  // (c) logits = [relu](h2 W3 + b3): wave 0, one 16x16 tile, K = 192
-  if (w == 0) {
+  // (b) h2 = relu(h1 W2 + b2): C[n][r] = sum_k W2t[n][k] h1[r][k]
+  if (w < 12) {
+    f32x4 acc = zero4();
+#pragma unroll
+    for (int ks = 0; ks < 12; ++ks) acc = mfma16(w2f[ks], lds_b128(h1s + li * H1_LD + ks * 32 + 8 * g), acc);
+    const int n = 16 * w + 4 * g;
+    const bf16x4 o = pack4(fmaxf(acc[0] + a.b2[n], 0.f), fmaxf(acc[1] + a.b2[n + 1], 0.f),
+                           fmaxf(acc[2] + a.b2[n + 2], 0.f), fmaxf(acc[3] + a.b2[n + 3], 0.f));
+    *reinterpret_cast<bf16x4*>(h2s + li * H2_LD + n) = o;
+    if (a.train) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.h2) + (size_t)(r0 + li) * 192 + n) = o;
+  }
+  // fc2^T fragments for (f): tiles w and w+16 (w < 8) of the 24 dh1 feature tiles, K = 192
+  bf16x8 w2d[2][6];
+  if (a.train) {
+    const bf16* W = reinterpret_cast<const bf16*>(a.w2d);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j == 0 || w < 8) {
+        const bf16* Wr = W + (16 * (w + 16 * j) + li) * 192 + 8 * g;
+#pragma unroll
+        for (int ks = 0; ks < 6; ++ks) w2d[j][ks] = glb_b128(Wr + ks * 32);
+      }
+    }
+  }
+  __syncthreads();
+  DMLC_STAMP(DMLC_TK_HEAD, 2);
+
+  // (c) logits = [relu](h2 W3 + b3): wave 12, one 16x16 tile, K = 192
+  if (w == 12) {
     const bf16* W = reinterpret_cast<const bf16*>(a.w3t);
     f32x4 acc = zero4();
 #pragma unroll
@@ -90,8 +135,8 @@ __global__ __launch_bounds__(256) void k_head(DmlcHeadArgs a) {
   }
   __syncthreads();
 
-  // (d) softmax cross-entropy, accuracy, dlogits (wave 0, lanes 0..15 = rows)
-  if (w == 0) {
+  // (d) softmax cross-entropy, accuracy, dlogits (wave 12, lanes 0..15 = rows)
+  if (w == 12) {
     float loss = 0.f, corr = 0.f;
     if (lane < 16) {
       const int b = r0 + lane;
@@ -133,47 +178,32 @@ __global__ __launch_bounds__(256) void k_head(DmlcHeadArgs a) {
   }
   if (!a.train) return;
   __syncthreads();
+  DMLC_STAMP(DMLC_TK_HEAD, 3);
 
-  // (e) dh2 = (dl W3^T) * (h2 > 0): C[n][r] = sum_k W3d[n][k] dl[r][k], K = 32 (one step)
-  {
+  // (e) dh2 = (dl W3^T) * (h2 > 0): C[n][r] = sum_k W3d[n][k] dl[r][k], K = 32 (one step), waves 0..11
+  if (w < 12) {
     const bf16* W = reinterpret_cast<const bf16*>(a.w3d);
-    const bf16x8 bx = lds_b128(dls + li * DL_LD + 8 * g);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int nt = w + 4 * j;
-      const f32x4 acc = mfma16(glb_b128(W + (16 * nt + li) * 32 + 8 * g), bx, zero4());
-      const int n = 16 * nt + 4 * g;
-      const bf16x4 hv = *reinterpret_cast<const bf16x4*>(h2s + li * H2_LD + n);
-      const bf16x4 o = pack4((float)hv[0] > 0.f ? acc[0] : 0.f, (float)hv[1] > 0.f ? acc[1] : 0.f,
-                             (float)hv[2] > 0.f ? acc[2] : 0.f, (float)hv[3] > 0.f ? acc[3] : 0.f);
-      *reinterpret_cast<bf16x4*>(dh2s + li * H2_LD + n) = o;
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh2) + (size_t)(r0 + li) * 192 + n) = o;
-    }
+    const f32x4 acc = mfma16(glb_b128(W + (16 * w + li) * 32 + 8 * g), lds_b128(dls + li * DL_LD + 8 * g), zero4());
+    const int n = 16 * w + 4 * g;
+    const bf16x4 o = relu_mask4(acc, *reinterpret_cast<const bf16x4*>(h2s + li * H2_LD + n));
+    *reinterpret_cast<bf16x4*>(dh2s + li * H2_LD + n) = o;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh2) + (size_t)(r0 + li) * 192 + n) = o;
   }
   __syncthreads();
+  DMLC_STAMP(DMLC_TK_HEAD, 4);
 
-  // (f) dh1 = (dh2 W2^T) * (h1 > 0): C[n][r] = sum_k W2n[n][k] dh2[r][k], n < 384, K = 192
-  {
-    const bf16* W = reinterpret_cast<const bf16*>(a.w2d);
-    f32x4 acc[6] = {zero4(), zero4(), zero4(), zero4(), zero4(), zero4()};
+  // (f) dh1 = (dh2 W2^T) * (h1 > 0): tiles w and w+16, K = 192
 #pragma unroll
-    for (int ks = 0; ks < 6; ++ks) {
-      const bf16x8 bx = lds_b128(dh2s + li * H2_LD + ks * 32 + 8 * g);
+  for (int j = 0; j < 2; ++j) {
+    if (j == 1 && w >= 8) break;
+    f32x4 acc = zero4();
 #pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int nt = w + 4 * j;
-        acc[j] = mfma16(glb_b128(W + (16 * nt + li) * 192 + ks * 32 + 8 * g), bx, acc[j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int n = 16 * (w + 4 * j) + 4 * g;
-      const bf16x4 hv = *reinterpret_cast<const bf16x4*>(h1s + li * H1_LD + n);
-      const bf16x4 o = pack4((float)hv[0] > 0.f ? acc[j][0] : 0.f, (float)hv[1] > 0.f ? acc[j][1] : 0.f,
-                             (float)hv[2] > 0.f ? acc[j][2] : 0.f, (float)hv[3] > 0.f ? acc[j][3] : 0.f);
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh1) + (size_t)(r0 + li) * 384 + n) = o;
-    }
+    for (int ks = 0; ks < 6; ++ks) acc = mfma16(w2d[j][ks], lds_b128(dh2s + li * H2_LD + ks * 32 + 8 * g), acc);
+    const int n = 16 * (w + 16 * j) + 4 * g;
+    const bf16x4 o = relu_mask4(acc, *reinterpret_cast<const bf16x4*>(h1s + li * H1_LD + n));
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh1) + (size_t)(r0 + li) * 384 + n) = o;
   }
+  DMLC_STAMP(DMLC_TK_HEAD, 5);
 }
 
 }  // namespace dmlc
@@ -181,6 +211,6 @@ __global__ __launch_bounds__(256) void k_head(DmlcHeadArgs a) {
 using namespace dmlc;
 
 extern "C" hipError_t dmlc_head(const DmlcHeadArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(k_head, dim3(a->B / 16), dim3(256), 0, s, *a);
+  hipLaunchKernelGGL(k_head, dim3(a->B / 16), dim3(HT), 0, s, *a);
   return hipGetLastError();
 }

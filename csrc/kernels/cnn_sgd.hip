@@ -9,8 +9,15 @@
 // global_step and publishes {step, loss, accuracy, lr} into a device stats ring, so the host never
 // has to synchronise for logging.
 //
+// Block roles (one launch, ranges of blockIdx.x, all 256 threads):
+//   conv2 rows  : 4 weight rows (k = (kh,kw,ci)) x 64 co per block (400 blocks); the g2 slabs are
+//                 split over 4 thread groups (<= 8 loads in flight each) and combined in fixed order;
+//                 shadows w2f (co-major) and w2d (flipped, ci-major).
+//   conv1 rows  : 1 of the 75 HWIO rows per block, g1 slabs split 16 ways.
+//   conv biases : 2 blocks over the per-group partial rows of each conv.
+//   fc          : float4 groups of the contiguous fc region (all segments 64-aligned), 4 per thread.
 // modes: 0 = reduce + apply (single GPU), 1 = reduce only (conv grads -> flat grad, before the DP
-// all-reduce), 2 = apply from the flat grad (after the all-reduce, grad_scale = 1/world),
+// all-reduce; fc blocks are not launched), 2 = apply from the flat grad (after the all-reduce),
 // 3 = refresh the shadows only (after init / checkpoint restore).
 #include "common.h"
 #include "api.h"
@@ -18,107 +25,176 @@
 namespace dmlc {
 
 constexpr int SEG_NUMEL[10] = {4800, 64, 102400, 64, 884736, 384, 73728, 192, 1920, 10};
+constexpr int C2_SPLIT = 4, C2_ROWS = 256 / C2_SPLIT / 16;   // 4 rows x 64 co per block
+constexpr int C2_BLOCKS = 1600 / C2_ROWS;                     // 400
+constexpr int C1_SPLIT = 16;                                  // 1 row x 64 co per block
+constexpr int C1_BLOCKS = 75;
+constexpr int FC_F4_PER_THREAD = 4;
 
-DEV float conv_bias_grad(const float* __restrict__ part, int n, int co, int tid, float* red) {
-  // deterministic sum over n partial rows [n][64] by the whole workgroup (4 threads per channel)
-  (void)co;
-  const int c = tid & 63, qd = tid >> 6;
-  float s = 0.f;
-  for (int i = qd; i < n; i += 4) s += part[i * 64 + c];
-  red[tid] = s;
+DEV float lr_of(const DmlcSgdArgs& a, int64_t step) {
+  return a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
+}
+
+DEV float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
+// Deterministic split reduction of n fp32 slabs (float4 at p + q*stride).  The block's threads are
+// S splits x (256/S) outputs; split sp sums slabs sp, sp+S, ... with up to 8 loads in flight, then
+// split 0 adds the S partial sums in fixed order.  Returns the total on split-0 threads.
+template <int S>
+DEV float4 split_sum(const float* __restrict__ p, size_t stride, int n, float4* lds) {
+  constexpr int T = 256 / S;
+  const int sp = threadIdx.x / T, idx = threadIdx.x % T;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int q = sp;
+  for (; q + 7 * S < n; q += 8 * S) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + (size_t)(q + u * S) * stride);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = add4(s, v[u]);
+  }
+  for (; q < n; q += S) s = add4(s, *reinterpret_cast<const float4*>(p + (size_t)q * stride));
+  lds[threadIdx.x] = s;
   __syncthreads();
-  float r = 0.f;
-  if (tid < 64) r = red[tid] + red[tid + 64] + red[tid + 128] + red[tid + 192];
-  __syncthreads();
-  return r;
+  float4 t = lds[idx];
+#pragma unroll
+  for (int k = 1; k < S; ++k) t = add4(t, lds[k * T + idx]);
+  return t;
+}
+
+DEV float4 sgd4(float* m, float4 g, float lr, float scale, bool apply) {
+  float4 w = *reinterpret_cast<float4*>(m);
+  if (apply) {
+    const float f = lr * scale;
+    w.x -= f * g.x; w.y -= f * g.y; w.z -= f * g.z; w.w -= f * g.w;
+    *reinterpret_cast<float4*>(m) = w;
+  }
+  return w;
+}
+
+DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
+  constexpr int T = 256 / C2_SPLIT;
+  const int idx = threadIdx.x % T, r = idx >> 4, co = (idx & 15) * 4;
+  const int krow = blk * C2_ROWS + r;                 // (kh*5+kw)*64 + ci
+  const size_t e = (size_t)krow * 64 + co;
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.mode == 0 || a.mode == 1) g = split_sum<C2_SPLIT>(a.part2 + e, 1600 * 64, a.g2, lds);
+  if (threadIdx.x >= T) return;
+  if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[2] + e);
+  if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[2] + e) = g; return; }
+  const float4 w = sgd4(a.master + a.off[2] + e, g, lr, a.grad_scale, a.mode != 3);
+  const int ci = krow & 63, khw = krow >> 6;
+  // w2d[ci][((4-kh)*5 + (4-kw))*64 + co] : contiguous in co
+  *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.w2d) + (size_t)ci * 1600 + (24 - khw) * 64 + co) =
+      pack4(w.x, w.y, w.z, w.w);
+  bf16* w2f = reinterpret_cast<bf16*>(a.w2f) + krow;  // w2f[co][krow]
+  w2f[(co + 0) * 1600] = (bf16)w.x; w2f[(co + 1) * 1600] = (bf16)w.y;
+  w2f[(co + 2) * 1600] = (bf16)w.z; w2f[(co + 3) * 1600] = (bf16)w.w;
+}
+
+DEV void conv1_rows(const DmlcSgdArgs& a, int row, float lr, float4* lds) {
+  constexpr int T = 256 / C1_SPLIT;
+  const int co = (threadIdx.x % T) * 4;               // HWIO row = (kh*5+kw)*3 + ci
+  const int ci = row % 3, khw = row / 3, kh = khw / 5, kw = khw - kh * 5;
+  const size_t e = (size_t)row * 64 + co;
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.mode == 0 || a.mode == 1)                     // slab row k'' = kh*16 + kw*3 + ci
+    g = split_sum<C1_SPLIT>(a.part1 + (size_t)(kh * 16 + kw * 3 + ci) * 64 + co, 80 * 64, a.g1, lds);
+  if (threadIdx.x >= T) return;
+  if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[0] + e);
+  if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[0] + e) = g; return; }
+  const float4 w = sgd4(a.master + a.off[0] + e, g, lr, a.grad_scale, a.mode != 3);
+  const int k = kh * 32 + kw * 4 + ci;                // forward shadow layout w1f[co][160]
+  bf16* w1f = reinterpret_cast<bf16*>(a.w1f);
+  w1f[(co + 0) * 160 + k] = (bf16)w.x;
+  w1f[(co + 1) * 160 + k] = (bf16)w.y;
+  w1f[(co + 2) * 160 + k] = (bf16)w.z;
+  w1f[(co + 3) * 160 + k] = (bf16)w.w;
+}
+
+// conv biases: block 0 -> conv1 bias (g1 group partials), block 1 -> conv2 bias (g2 group partials)
+DEV void conv_bias(const DmlcSgdArgs& a, int which, float lr, float4* lds) {
+  const int c = (threadIdx.x % 16) * 4;
+  const int seg = which == 0 ? 1 : 3;
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.mode == 0 || a.mode == 1)
+    g = split_sum<16>((which == 0 ? a.partb1 : a.partb2) + c, 64, which == 0 ? a.g1 : a.g2, lds);
+  if (threadIdx.x >= 16) return;
+  float* gp = a.grad + a.off[seg] + c;
+  if (a.mode == 1) { *reinterpret_cast<float4*>(gp) = g; return; }
+  if (a.mode == 2) g = *reinterpret_cast<const float4*>(gp);
+  sgd4(a.master + a.off[seg] + c, g, lr, a.grad_scale, a.mode != 3);
+}
+
+DEV void fc_block(const DmlcSgdArgs& a, int blk, float lr) {
+  const int base4 = a.off[4] >> 2, end4 = (a.off[9] + 10 + 3) >> 2;
+  const bool apply = a.mode != 3;
+  const float f = lr * a.grad_scale;
+  int i4[FC_F4_PER_THREAD];
+  float4 w[FC_F4_PER_THREAD], g[FC_F4_PER_THREAD];
+#pragma unroll
+  for (int u = 0; u < FC_F4_PER_THREAD; ++u) {
+    i4[u] = base4 + (blk * FC_F4_PER_THREAD + u) * 256 + threadIdx.x;
+    const int ic = i4[u] < end4 ? i4[u] : base4;             // branch-free loads (clamped)
+    w[u] = reinterpret_cast<const float4*>(a.master)[ic];
+    g[u] = reinterpret_cast<const float4*>(a.grad)[ic];
+  }
+#pragma unroll
+  for (int u = 0; u < FC_F4_PER_THREAD; ++u) {
+    const int i = i4[u] * 4;
+    if (i4[u] >= end4) continue;
+    float4 v = w[u];
+    if (apply) {
+      v.x -= f * g[u].x; v.y -= f * g[u].y; v.z -= f * g[u].z; v.w -= f * g[u].w;
+      reinterpret_cast<float4*>(a.master)[i4[u]] = v;
+    }
+    if (i < a.off[5]) {                               // fc1 weight [2304][384]: same layout shadow
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.fc1n) + (i - a.off[4])) = pack4(v.x, v.y, v.z, v.w);
+    } else if (i >= a.off[6] && i < a.off[7]) {      // fc2 weight [384][192]
+      const int j = i - a.off[6], k = j / 192, n = j - k * 192;
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.fc2n) + j) = pack4(v.x, v.y, v.z, v.w);
+      bf16* t = reinterpret_cast<bf16*>(a.fc2t);
+      t[(n + 0) * 384 + k] = (bf16)v.x; t[(n + 1) * 384 + k] = (bf16)v.y;
+      t[(n + 2) * 384 + k] = (bf16)v.z; t[(n + 3) * 384 + k] = (bf16)v.w;
+    } else if (i >= a.off[8] && i < a.off[9]) {      // fc3 weight [192][10]
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int j = i - a.off[8] + c;
+        if (j >= 1920) break;
+        const int k = j / 10, n = j - k * 10;
+        reinterpret_cast<bf16*>(a.fc3t)[n * 192 + k] = (bf16)vv[c];
+        reinterpret_cast<bf16*>(a.fc3d)[k * 32 + n] = (bf16)vv[c];
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
-  __shared__ float red[256];
-  const int tid = threadIdx.x;
+  __shared__ float4 lds[256];
+  DMLC_STAMP(DMLC_TK_SGD, 0);
   const int64_t step = *a.step;
-  float lr = a.lr0;
-  if (a.staircase) lr = a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps));
-  const bool apply = a.mode == 0 || a.mode == 2;
-  const bool reduce = a.mode == 0 || a.mode == 1;
-  const float scale = a.grad_scale;
-  bf16* w1f = reinterpret_cast<bf16*>(a.w1f);
-  bf16* w2f = reinterpret_cast<bf16*>(a.w2f);
-  bf16* w2d = reinterpret_cast<bf16*>(a.w2d);
-  const int end = a.off[9] + 10;
+  const float lr = lr_of(a, step);
+  int blk = blockIdx.x;
+  if (blk < C2_BLOCKS) conv2_rows(a, blk, lr, lds);
+  else if ((blk -= C2_BLOCKS) < C1_BLOCKS) conv1_rows(a, blk, lr, lds);
+  else if ((blk -= C1_BLOCKS) < 2) conv_bias(a, blk, lr, lds);
+  else fc_block(a, blk - 2, lr);
+  DMLC_STAMP(DMLC_TK_SGD, 1);
 
-  for (int i = blockIdx.x * 256 + tid; i < end; i += gridDim.x * 256) {
-    int seg = 9;
-    while (seg > 0 && i < a.off[seg]) --seg;
-    const int j = i - a.off[seg];
-    if (j >= SEG_NUMEL[seg]) continue;       // alignment padding
-    if (seg == 1 || seg == 3) continue;      // conv biases: block 0 below
-    float gv = 0.f;
-    if (seg == 0) {
-      const int co = j & 63, t = j >> 6, ci = t % 3, kw = (t / 3) % 5, kh = t / 15;
-      const int k = kh * 32 + kw * 4 + ci;
-      if (reduce) for (int q = 0; q < a.g1; ++q) gv += a.part1[((size_t)q * 160 + k) * 64 + co];
-      else gv = a.grad[i];
-      if (a.mode == 1) { a.grad[i] = gv; continue; }
-      float wv = a.master[i];
-      if (apply) { wv -= lr * gv * scale; a.master[i] = wv; }
-      w1f[co * 160 + k] = (bf16)wv;
-    } else if (seg == 2) {
-      const int co = j & 63, krow = j >> 6, ci = krow & 63, khw = krow >> 6;
-      const int kh = khw / 5, kw = khw - kh * 5;
-      if (reduce) for (int q = 0; q < a.g2; ++q) gv += a.part2[((size_t)q * 1600 + krow) * 64 + co];
-      else gv = a.grad[i];
-      if (a.mode == 1) { a.grad[i] = gv; continue; }
-      float wv = a.master[i];
-      if (apply) { wv -= lr * gv * scale; a.master[i] = wv; }
-      w2f[co * 1600 + krow] = (bf16)wv;
-      w2d[ci * 1600 + ((4 - kh) * 5 + (4 - kw)) * 64 + co] = (bf16)wv;
-    } else {
-      if (a.mode == 1) continue;             // fc grads are already complete in a.grad
-      float wv = a.master[i];
-      if (apply) { wv -= lr * a.grad[i] * scale; a.master[i] = wv; }
-      const bf16 bv = (bf16)wv;
-      if (seg == 4) {
-        reinterpret_cast<bf16*>(a.fc1n)[j] = bv;
-      } else if (seg == 6) {
-        const int k = j / 192, n = j - k * 192;
-        reinterpret_cast<bf16*>(a.fc2n)[j] = bv;
-        reinterpret_cast<bf16*>(a.fc2t)[n * 384 + k] = bv;
-      } else if (seg == 8) {
-        const int k = j / 10, n = j - k * 10;
-        reinterpret_cast<bf16*>(a.fc3t)[n * 192 + k] = bv;
-        reinterpret_cast<bf16*>(a.fc3d)[k * 32 + n] = bv;
-      }
-    }
-  }
-
-  if (blockIdx.x == 0) {   // conv biases: cooperative deterministic reductions
-    float g1 = 0.f, g3 = 0.f;
-    if (reduce) {
-      g1 = conv_bias_grad(a.partb1, a.g1, 0, tid, red);
-      g3 = conv_bias_grad(a.partb2, a.B, 0, tid, red);
-    }
-    if (tid < 64) {
-      const int i1 = a.off[1] + tid, i3 = a.off[3] + tid;
-      if (a.mode == 1) {
-        a.grad[i1] = g1;
-        a.grad[i3] = g3;
-      } else if (apply) {
-        if (a.mode == 2) { g1 = a.grad[i1]; g3 = a.grad[i3]; }
-        a.master[i1] -= lr * g1 * scale;
-        a.master[i3] -= lr * g3 * scale;
-      }
-    }
-  }
-
-  if (!apply) return;
-  // last-arriver: bump global_step, publish stats, reset the ticket for the next launch
+  if (!(a.mode == 0 || a.mode == 2)) return;
+  // last arriver: bump global_step, publish stats, re-arm the ticket for the next launch (the engine
+  // zeroes it once at creation; every launch that starts also completes, so it stays consistent).
+  // Nothing is published THROUGH the ticket (loss/accuracy partials come from an earlier launch and
+  // the step/stats are consumed by later launches), so no release/acquire fences: an agent-scope
+  // release is an L2 write-back on every XCD, which 700 blocks would pay for nothing.  The only
+  // ordering needed -- every block has read *a.step before the last one bumps it -- is given by the
+  // vmcnt(0) drain before each block's ticket increment.
   __syncthreads();
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (unsigned)gridDim.x - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       float loss = 0.f;
       int corr = 0;
       for (int q = 0; q < a.nhead; ++q) { loss += a.loss_part[q]; corr += a.correct_part[q]; }
@@ -131,6 +207,7 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
       __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  DMLC_STAMP(DMLC_TK_SGD, 2);
 }
 
 }  // namespace dmlc
@@ -138,9 +215,9 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
 using namespace dmlc;
 
 extern "C" hipError_t dmlc_sgd(DmlcSgdArgs* a, hipStream_t s) {
-  const int end = a->off[9] + 10;
-  int blocks = (end + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
+  const int fc4 = ((a->off[9] + 10 + 3) >> 2) - (a->off[4] >> 2);
+  const int fc_blocks = (fc4 + 256 * FC_F4_PER_THREAD - 1) / (256 * FC_F4_PER_THREAD);
+  const int blocks = C2_BLOCKS + C1_BLOCKS + 2 + (a->mode == 1 ? 0 : fc_blocks);
   a->nblocks = blocks;
   hipLaunchKernelGGL(k_sgd, dim3(blocks), dim3(256), 0, s, *a);
   return hipGetLastError();

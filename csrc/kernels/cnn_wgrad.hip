@@ -1,0 +1,296 @@
+// Weight gradients of the two convolutions (TF Conv2DBackpropFilter + BiasAddGrad of
+// /root/reference/cifar10cnn.py:107/:118 via the autodiff of :163; SURVEY.md §2.B N5/N7, §2.C
+// conv5x5_wgrad).  Two kernels, launched on forked streams of the step graph so they run side by
+// side on the chip:
+//
+//   k_conv1_wgrad  dW1[k''][co] = sum_{b,px} X[b,px][k''] dY1[b,px][co],  k'' = kh*16 + kw*3 + ci
+//     * dY1 (the conv1 output gradient) is produced in LDS by the TF-SAME pool1 backward in "2x2
+//       ownership" form from the staged pool1 gradient + argmax bytes (conv_common.h);
+//     * X is kept as 15 channel-planar, column-shifted copies of the padded 28x24 crop (plane
+//       kw*3+ci = Xpad[ci][y][x+kw]) so a K'' tile of 16 is one kernel row (15 taps + 1 zero plane)
+//       and every B fragment is ONE aligned ds_read_b128 of 8 consecutive pixels: K'' = 80 instead
+//       of the 160 a [pixel][4ch] image needs;
+//     * the four waves split the 18 pixel k-steps of an image (not the output), each wave owns the
+//       whole 64x80 tile (20 MFMA accumulators), reduced across waves once per block;
+//   k_conv2_wgrad  dW2[(kh,kw,ci)][co] = sum_{b,px} Xpad[b][px+(kh,kw)][ci] dY2[b,px][co]
+//     * one block per (kh, image group): wave w owns ci tile w x 5 kw x 4 co tiles (20 acc), so per
+//       k-step it reads 10 A + 8 B transposed fragments (ds_read_b64_tr_b16) for 20 MFMAs.
+// Both: the NEXT image's global data is prefetched into registers while the current image is being
+// computed (one exposed memory latency per block instead of one per image); results are fp32
+// split-K partial slabs, one per image group, reduced in fixed order by the SGD kernel.
+#include "conv_common.h"
+
+namespace dmlc {
+
+// ---------------------------------------------------------------------------------------------
+constexpr int W1_DY_LD = 72;                  // dY1 LDS row stride (bf16): 144 B, tr reads conflict-free
+constexpr int W1_PL = 28 * 24 + 8;            // shifted-plane stride (bf16): 1360 B, b128 reads conflict-free
+constexpr int W1_DYT = 576 * W1_DY_LD;        // bf16 elements
+constexpr int W1_XS = 16 * W1_PL;
+constexpr int W1_RAW = 28 * 32 * 4;           // bf16 [28][32][4] padded crop (col c <-> ix = c-2)
+constexpr size_t W1_LDS = (size_t)(W1_DYT + W1_XS + 9216 + W1_RAW) * 2 + 9216 + 4 * 64 * 4;
+
+struct Conv1Input {                            // prefetch of the 28x32 zero-padded crop, 3 bytes/pixel
+  uint32_t v[4];
+  MDEV void load(const uint8_t* img, int cy, int cx, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = tid + i * 256;
+      const int r = p >> 5, c = p & 31, iy = r - 2, ix = c - 2;
+      const bool ok = p < 896 && iy >= 0 && iy < 24 && ix >= 0 && ix < 24;
+      const uint8_t* s = img + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);   // branch-free loads
+      const uint32_t x = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
+      v[i] = ok ? x : 0u;
+    }
+  }
+  MDEV void store(bf16* raw, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = tid + i * 256;
+      if (p < 896)
+        *reinterpret_cast<bf16x4*>(raw + p * 4) =
+            pack4((float)(v[i] & 0xff), (float)((v[i] >> 8) & 0xff), (float)((v[i] >> 16) & 0xff), 0.f);
+    }
+  }
+};
+
+__global__ __launch_bounds__(256, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* dyt = reinterpret_cast<bf16*>(smem);
+  bf16* xs = dyt + W1_DYT;
+  bf16* dps = xs + W1_XS;
+  bf16* raw = dps + 9216;
+  uint8_t* ams = reinterpret_cast<uint8_t*>(raw + W1_RAW);
+  float* red = reinterpret_cast<float*>(ams + 9216);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int grp = blockIdx.x;
+  const int b0 = grp * a.B / a.g1, b1 = (grp + 1) * a.B / a.g1;
+  DMLC_STAMP(DMLC_TK_W1, 0);
+
+  for (int e = tid; e < W1_PL / 8; e += 256) *reinterpret_cast<bf16x8*>(xs + 15 * W1_PL + e * 8) = bf16x8{};
+
+  f32x4 acc[4][5];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int t = 0; t < 5; ++t) acc[ct][t] = zero4();
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+  Conv1Input pin;
+  Prefetch16<1152> pdp;
+  Prefetch16<576> pam;
+  if (b0 < b1) {
+    pin.load(a.data + (size_t)batch_index(a.src, a.B, b0) * 3072, a.cy, a.cx, tid);
+    pdp.load(reinterpret_cast<const bf16*>(a.dp1) + (size_t)b0 * 9216, tid);
+    pam.load(a.am1 + (size_t)b0 * 9216, tid);
+  }
+  for (int b = b0; b < b1; ++b) {
+    __syncthreads();                           // previous image's MFMA reads are done
+    pin.store(raw, tid);
+    pdp.store(dps, tid);
+    pam.store(ams, tid);
+    if (b + 1 < b1) {                          // prefetch the next image while this one computes
+      pin.load(a.data + (size_t)batch_index(a.src, a.B, b + 1) * 3072, a.cy, a.cx, tid);
+      pdp.load(reinterpret_cast<const bf16*>(a.dp1) + (size_t)(b + 1) * 9216, tid);
+      pam.load(a.am1 + (size_t)(b + 1) * 9216, tid);
+    }
+    __syncthreads();
+    if (b == b0) DMLC_STAMP(DMLC_TK_W1, 1);
+    // (a) shifted channel planes: task (yy, x8, kw) -> planes kw*3+{0,1,2}, 8 pixels
+    for (int task = tid; task < 28 * 3 * 5; task += 256) {
+      const int kw = task % 5, r = task / 5, x8 = r % 3, yy = r / 3;
+      const bf16* src = raw + (yy * 32 + x8 * 8 + kw) * 4;
+      bf16x8 o0, o1, o2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bf16x4 v = *reinterpret_cast<const bf16x4*>(src + j * 4);
+        o0[j] = v[0]; o1[j] = v[1]; o2[j] = v[2];
+      }
+      bf16* dst = xs + (kw * 3) * W1_PL + yy * 24 + x8 * 8;
+      *reinterpret_cast<bf16x8*>(dst) = o0;
+      *reinterpret_cast<bf16x8*>(dst + W1_PL) = o1;
+      *reinterpret_cast<bf16x8*>(dst + 2 * W1_PL) = o2;
+    }
+    // (b) pool1 / ReLU backward -> dY1 (bf16, LDS) + bias-grad sums (fp32)
+    for (int task = tid; task < 144 * 8; task += 256) {
+      const int win = task >> 3, c = task & 7, py = win / 12, px = win - py * 12;
+      float o[4][8];
+      pool_bwd_2x2<12>(dps, ams, py, px, c, o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
+        *reinterpret_cast<bf16x8*>(dyt + (y * 24 + x) * W1_DY_LD + c * 8) = to_bf16x8(o[k]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[j] += o[k][j];
+      }
+    }
+    __syncthreads();
+    if (b == b0) DMLC_STAMP(DMLC_TK_W1, 2);
+    // (c) MFMA: this wave's k-steps s = w, w+4, ... of the 18 (32 pixels each)
+    for (int s = w; s < 18; s += 4) {
+      const int rA = 32 * s + 8 * g + q, rB = rA + 4;
+      bf16x8 af[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+        af[ct] = tr_frag(dyt + rA * W1_DY_LD + 16 * ct + 4 * p, dyt + rB * W1_DY_LD + 16 * ct + 4 * p);
+      const int r0 = 32 * s + 8 * g, y = r0 / 24, x0 = r0 - y * 24;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const bf16x8 bx = lds_b128(xs + li * W1_PL + (y + t) * 24 + x0);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(af[ct], bx, acc[ct][t]);
+      }
+    }
+  }
+  // cross-wave reduction (fixed order) through the dY region, then the fp32 slab [80 k''][64 co]
+  __syncthreads();
+  DMLC_STAMP(DMLC_TK_W1, 3);
+  f32x4* fl = reinterpret_cast<f32x4*>(smem);
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int t = 0; t < 5; ++t) fl[(w * 20 + ct * 5 + t) * 64 + lane] = acc[ct][t];
+  block_chunk_sum(bsum, red, tid);
+  __syncthreads();
+  float* out = a.part1 + (size_t)grp * 80 * 64;
+  for (int e = tid; e < 20 * 64; e += 256) {
+    const f32x4 s = ((fl[e] + fl[1280 + e]) + (fl[2560 + e] + fl[3840 + e]));
+    const int tile = e >> 6, ln = e & 63, ct = tile / 5, t = tile - ct * 5;
+    const int co = 16 * ct + 4 * (ln >> 4), kk = 16 * t + (ln & 15);
+    *reinterpret_cast<f32x4*>(out + kk * 64 + co) = s;
+  }
+  if (tid < 64) a.partb1[grp * 64 + tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+  DMLC_STAMP(DMLC_TK_W1, 4);
+}
+
+// ---------------------------------------------------------------------------------------------
+constexpr int W2_LD = 72;                      // 144-B rows: tr reads of rows r / r+8 hit different banks
+constexpr int W2_XT = 12 * 16 * W2_LD;         // rows kh..kh+11 of the padded input, 16 cols
+constexpr int W2_DY = 160 * W2_LD;             // 144 pixels + 16 zero rows
+constexpr size_t W2_LDS = (size_t)(W2_XT + W2_DY) * 2;
+
+__global__ __launch_bounds__(256, 2) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* xt = reinterpret_cast<bf16*>(smem);
+  bf16* dyt = xt + W2_XT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int kh = blockIdx.x % 5, grp = blockIdx.x / 5;
+  const int b0 = grp * a.B / a.g2, b1 = (grp + 1) * a.B / a.g2;
+  DMLC_STAMP(DMLC_TK_W2, 0);
+
+  // zero halo columns (xx = 0,1,14,15) and the 16 padding dY rows once
+  for (int e = tid; e < 12 * 4 * 8; e += 256) {
+    const int c = e & 7, r = e >> 3, yy = r >> 2, k = r & 3, xx = k < 2 ? k : 12 + k;
+    *reinterpret_cast<bf16x8*>(xt + (yy * 16 + xx) * W2_LD + c * 8) = bf16x8{};
+  }
+  for (int e = tid; e < 16 * 8; e += 256)
+    *reinterpret_cast<bf16x8*>(dyt + (144 + (e >> 3)) * W2_LD + (e & 7) * 8) = bf16x8{};
+
+  f32x4 acc[5][4];
+#pragma unroll
+  for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[kw][ct] = zero4();
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // conv2 bias grad (kh == 0 blocks)
+
+  // prefetch: x rows iy = kh-2 .. kh+9 (1152 chunks, invalid rows -> 0) and dY (1152 chunks)
+  constexpr int IT = 5;
+  uint4 vx[IT], vd[IT];
+  auto load = [&](int b) {
+    const uint4* x = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.p1) + (size_t)b * 9216);
+    const uint4* d = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.dy2) + (size_t)b * 9216);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int k = tid + i * 256;
+      const int yy = k / 96, iy = kh + yy - 2;
+      vx[i] = load_sel(x + iy * 96 + (k - yy * 96), x, k < 1152 && iy >= 0 && iy < 12);
+      vd[i] = load_sel(d + k, d, k < 1152);
+    }
+  };
+  if (b0 < b1) load(b0);
+  for (int b = b0; b < b1; ++b) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int k = tid + i * 256;
+      if (k < 1152) {
+        const int yy = k / 96, rem = k - yy * 96, px = rem >> 3, c = rem & 7;
+        *reinterpret_cast<uint4*>(xt + (yy * 16 + px + 2) * W2_LD + c * 8) = vx[i];
+        *reinterpret_cast<uint4*>(dyt + (k >> 3) * W2_LD + (k & 7) * 8) = vd[i];
+        if (kh == 0) {                         // chunk k & 7 == tid & 7: channels 8c..8c+7
+          const uint32_t d4[4] = {vd[i].x, vd[i].y, vd[i].z, vd[i].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { bsum[2 * j] += bf16_lo(d4[j]); bsum[2 * j + 1] += bf16_hi(d4[j]); }
+        }
+      }
+    }
+    if (b + 1 < b1) load(b + 1);
+    __syncthreads();
+    if (b == b0) DMLC_STAMP(DMLC_TK_W2, 1);
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      const int rA = 32 * s + 8 * g + q, rB = rA + 4;
+      bf16x8 bf[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+        bf[ct] = tr_frag(dyt + rA * W2_LD + 16 * ct + 4 * p, dyt + rB * W2_LD + 16 * ct + 4 * p);
+      const int cA = min(rA, 143), cB = min(rB, 143);
+      const int yA = cA / 12, yB = cB / 12;
+      const int pA = yA * 16 + cA - yA * 12, pB = yB * 16 + cB - yB * 12;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        const bf16x8 af = tr_frag(xt + (pA + kw) * W2_LD + 16 * w + 4 * p, xt + (pB + kw) * W2_LD + 16 * w + 4 * p);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[kw][ct] = mfma16(af, bf[ct], acc[kw][ct]);
+      }
+    }
+  }
+  DMLC_STAMP(DMLC_TK_W2, 2);
+  float* out = a.part2 + (size_t)grp * 1600 * 64;
+#pragma unroll
+  for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int krow = (kh * 5 + kw) * 64 + 16 * w + 4 * g + i;
+        out[krow * 64 + 16 * ct + li] = acc[kw][ct][i];
+      }
+  if (kh == 0) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    block_chunk_sum(bsum, red, tid);
+    __syncthreads();
+    if (tid < 64) a.partb2[grp * 64 + tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+  }
+  DMLC_STAMP(DMLC_TK_W2, 3);
+}
+
+}  // namespace dmlc
+
+using namespace dmlc;
+
+namespace {
+bool g_w1 = false;
+}
+
+extern "C" {
+
+hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s) {
+  if (!g_w1) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv1_wgrad),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)W1_LDS);
+    g_w1 = true;
+  }
+  hipLaunchKernelGGL(k_conv1_wgrad, dim3(a->g1), dim3(256), W1_LDS, s, *a);
+  return hipGetLastError();
+}
+
+hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(k_conv2_wgrad, dim3(5 * a->g2), dim3(256), W2_LDS, s, *a);
+  return hipGetLastError();
+}
+
+}  // extern "C"

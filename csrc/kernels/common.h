@@ -21,6 +21,7 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define DEV static __device__ __forceinline__
+#define MDEV __device__ __forceinline__   // member functions
 #define LDS_AS __attribute__((address_space(3)))
 
 DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
@@ -63,3 +64,47 @@ DEV float wave_sum(float v) {
 DEV int swz128(int pix, int chunk) { return pix * 64 + ((chunk ^ (pix & 7)) << 3); }
 
 }  // namespace dmlc
+
+// ---- diagnostic phase timing (build with DMLC_TIMING=1: separate library, never the default) ----
+// DMLC_STAMP(kernel, slot): thread 0 of the block records s_memrealtime (100 MHz) into
+// dmlc_timing_buf[kernel][block][slot]; tools/ktiming.py reads it back.
+#define DMLC_TK_CONV1_FWD 0
+#define DMLC_TK_CONV2_FWD 1
+#define DMLC_TK_GEMM 2
+#define DMLC_TK_HEAD 3
+#define DMLC_TK_DGRAD 4
+#define DMLC_TK_W1 5
+#define DMLC_TK_W2 6
+#define DMLC_TK_SGD 7
+#define DMLC_TK_N 8
+#define DMLC_TK_BLOCKS 1024
+#define DMLC_TK_SLOTS 8
+#ifdef DMLC_TIMING
+extern __device__ unsigned long long dmlc_timing_buf[DMLC_TK_N * DMLC_TK_BLOCKS * DMLC_TK_SLOTS];
+#define DMLC_STAMP(k, slot)                                                                          \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < DMLC_TK_BLOCKS)                                             \
+      dmlc_timing_buf[((k) * DMLC_TK_BLOCKS + blockIdx.x) * DMLC_TK_SLOTS + (slot)] =               \
+          __builtin_amdgcn_s_memrealtime();                                                          \
+  } while (0)
+#else
+#define DMLC_STAMP(k, slot) do {} while (0)
+#endif
+
+// ---- branch-free guarded loads --------------------------------------------------------------------
+// `if (ok) v = *p;` makes hipcc branch around the load and wait vmcnt(0) inside the branch, which
+// serialises every load of an unrolled prefetch.  These load unconditionally from `ok ? p : safe`
+// (a valid address of the same buffer) and select afterwards, so all loads stay in flight together.
+template <class T>
+DEV T load_sel(const T* p, const T* safe, bool ok) {
+  const T v = *(ok ? p : safe);
+  return ok ? v : T{};
+}
+DEV uint4 load_sel(const uint4* p, const uint4* safe, bool ok) {
+  const uint4 v = *(ok ? p : safe);
+  return ok ? v : make_uint4(0, 0, 0, 0);
+}
+DEV float4 load_sel(const float4* p, const float4* safe, bool ok) {
+  const float4 v = *(ok ? p : safe);
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}

@@ -1,0 +1,126 @@
+// Device helpers shared by the convolution kernels (cnn_conv.hip, cnn_wgrad.hip).
+#pragma once
+#include "common.h"
+#include "api.h"
+
+namespace dmlc {
+
+DEV int batch_index(const DmlcIndexSrc& s, int B, int b) {
+  int row = 0;
+  if (s.counter) row = (int)(*s.counter % (int64_t)s.period);
+  return s.idx_base[row * B + b];
+}
+
+// Copy N 16-byte chunks global -> LDS with every load of the thread issued before any store, so
+// the block pays one memory latency instead of one per iteration.
+template <int N>
+DEV void stage16(void* dst, const void* src, int tid) {
+  constexpr int IT = (N + 255) / 256;
+  uint4 v[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int c = tid + i * 256;
+    v[i] = load_sel(reinterpret_cast<const uint4*>(src) + c, reinterpret_cast<const uint4*>(src), c < N);
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int c = tid + i * 256;
+    if (c < N) reinterpret_cast<uint4*>(dst)[c] = v[i];
+  }
+}
+
+// Register prefetch of N 16-byte chunks (thread's share), split in two halves so a kernel can issue
+// the loads of the NEXT item before computing the current one.
+template <int N>
+struct Prefetch16 {
+  static constexpr int IT = (N + 255) / 256;
+  uint4 v[IT];
+  MDEV void load(const void* src, int tid) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int c = tid + i * 256;
+      v[i] = load_sel(reinterpret_cast<const uint4*>(src) + c, reinterpret_cast<const uint4*>(src), c < N);
+    }
+  }
+  MDEV void store(void* dst, int tid) const {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int c = tid + i * 256;
+      if (c < N) reinterpret_cast<uint4*>(dst)[c] = v[i];
+    }
+  }
+};
+
+DEV float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+DEV float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// TF-SAME 3x3/2 max-pool backward, "2x2 ownership" form.  Pooled window (py,px) owns the conv
+// output pixels (2py+dy, 2px+dx), dy,dx in {0,1}; with windows overlapping by one row/column, those
+// pixels receive gradient only from (py,px), its left (py,px-1), upper (py-1,px) and upper-left
+// neighbour, at fixed in-window positions d = 3*dy + dx:
+//   o[3] (2py+1,2px+1) : W d4
+//   o[2] (2py+1,2px)   : W d3 + L d5
+//   o[1] (2py,  2px+1) : W d1 + U d7
+//   o[0] (2py,  2px)   : W d0 + L d2 + U d6 + UL d8
+// (the argmax byte 255 = "pooled <= 0" never matches, giving the ReLU mask for free).  No loops, no
+// atomics, fixed summation order -> deterministic.  dp/am: LDS [HO*HO][64]; chunk c = channels 8c..8c+7.
+template <int HO>
+DEV void pool_bwd_2x2(const bf16* dp, const uint8_t* am, int py, int px, int c, float (&o)[4][8]) {
+  const int base = (py * HO + px) * 64 + c * 8;
+  const uint2 aw = *reinterpret_cast<const uint2*>(am + base);
+  const uint4 vw = *reinterpret_cast<const uint4*>(dp + base);
+  // neighbours outside the grid read the window itself (valid address) and get argmax 255 (no match)
+  const int ol = px > 0 ? 64 : 0, ou = py > 0 ? HO * 64 : 0;
+  uint2 al = *reinterpret_cast<const uint2*>(am + base - ol);
+  uint2 au = *reinterpret_cast<const uint2*>(am + base - ou);
+  uint2 aul = *reinterpret_cast<const uint2*>(am + base - ol - ou);
+  const uint4 vl = *reinterpret_cast<const uint4*>(dp + base - ol);
+  const uint4 vu = *reinterpret_cast<const uint4*>(dp + base - ou);
+  const uint4 vul = *reinterpret_cast<const uint4*>(dp + base - ol - ou);
+  const uint2 none = make_uint2(0xffffffffu, 0xffffffffu);
+  if (!ol) al = none;
+  if (!ou) au = none;
+  if (!ol || !ou) aul = none;
+  const uint32_t vwa[4] = {vw.x, vw.y, vw.z, vw.w}, vla[4] = {vl.x, vl.y, vl.z, vl.w};
+  const uint32_t vua[4] = {vu.x, vu.y, vu.z, vu.w}, vula[4] = {vul.x, vul.y, vul.z, vul.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int sh = (j & 3) * 8;
+    const uint32_t bw = ((j < 4 ? aw.x : aw.y) >> sh) & 0xff, bl = ((j < 4 ? al.x : al.y) >> sh) & 0xff;
+    const uint32_t bu = ((j < 4 ? au.x : au.y) >> sh) & 0xff, bul = ((j < 4 ? aul.x : aul.y) >> sh) & 0xff;
+    const float fw = (j & 1) ? bf16_hi(vwa[j >> 1]) : bf16_lo(vwa[j >> 1]);
+    const float fl = (j & 1) ? bf16_hi(vla[j >> 1]) : bf16_lo(vla[j >> 1]);
+    const float fu = (j & 1) ? bf16_hi(vua[j >> 1]) : bf16_lo(vua[j >> 1]);
+    const float ful = (j & 1) ? bf16_hi(vula[j >> 1]) : bf16_lo(vula[j >> 1]);
+    o[3][j] = bw == 4 ? fw : 0.f;
+    o[2][j] = (bw == 3 ? fw : 0.f) + (bl == 5 ? fl : 0.f);
+    o[1][j] = (bw == 1 ? fw : 0.f) + (bu == 7 ? fu : 0.f);
+    o[0][j] = ((bw == 0 ? fw : 0.f) + (bl == 2 ? fl : 0.f)) + ((bu == 6 ? fu : 0.f) + (bul == 8 ? ful : 0.f));
+  }
+}
+
+DEV bf16x8 to_bf16x8(const float (&v)[8]) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+  return o;
+}
+
+// Reduce per-thread channel sums (thread's chunk = tid & 7) over the workgroup: red[4][64] partials.
+DEV void block_chunk_sum(float (&v)[8], float* red /*[4][64]*/, int tid) {
+  const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float s = v[j];
+    s += __shfl_xor(s, 8);
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    v[j] = s;
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[w * 64 + lane * 8 + j] = v[j];
+  }
+}
+
+}  // namespace dmlc

@@ -28,7 +28,10 @@ OBJ_DIR = os.path.join(REPO, "build", "obj")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-HIP_LIB = os.path.join(LIB_DIR, "libdmlc_hip.so")
+# DMLC_TIMING=1 builds a separate diagnostic library with per-phase s_memrealtime stamps
+# (tools/ktiming.py); the default library never contains them.
+TIMING = os.environ.get("DMLC_TIMING") == "1"
+HIP_LIB = os.path.join(LIB_DIR, "libdmlc_hip_timing.so" if TIMING else "libdmlc_hip.so")
 RT_LIB = os.path.join(LIB_DIR, "_dmlc_rt" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 
 
@@ -102,8 +105,10 @@ def build(hip: bool = True, rt: bool = True, jobs: int | None = None) -> dict:
     if hip:
         hipcc = os.path.join(ROCM, "bin", "hipcc")
         hip_flags = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+        if TIMING:   # the stamp buffer is one __device__ symbol shared by every kernel TU
+            hip_flags += ["-DDMLC_TIMING", "-fgpu-rdc"]
         for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
-            o = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+            o = os.path.join(OBJ_DIR, os.path.basename(src) + (".timing.o" if TIMING else ".o"))
             hip_objs.append(o)
             jobs_list.append((src, headers, o, [hipcc], hip_flags))
         bsrc = os.path.join(CSRC, "bindings", "torch_ops.cpp")
@@ -125,7 +130,8 @@ def build(hip: bool = True, rt: bool = True, jobs: int | None = None) -> dict:
             f.result()
     if hip:
         hipcc = os.path.join(ROCM, "bin", "hipcc")
-        _link(hip_objs, HIP_LIB, [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + torch_link
+        _link(hip_objs, HIP_LIB, [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}"]
+              + (["-fgpu-rdc"] if TIMING else []) + torch_link
               + [f"-L{torch_lib}", "-lc10_hip", "-ltorch_hip"])
         out["hip"] = HIP_LIB
     if rt and rt_objs:

@@ -1,15 +1,16 @@
 """Fused MI355X training engine for the reference CNN (hand-written HIP kernels + HIP graphs + RCCL).
 
 One training step (= one ``mon_sess.run([train_op, loss])`` of /root/reference/cifar10cnn.py:230,
-SURVEY.md §3.3) is eight kernel launches, all reading their inputs from device memory:
+SURVEY.md §3.3) is nine kernel launches, all reading their inputs from device memory:
 
   1 conv1_fwd    uint8 gather + center crop + conv1 + bias + ReLU + pool1 (+argmax)
   2 conv2_fwd    conv2 + bias + ReLU + pool2 (+argmax)
   3 gemm         fc1 forward, split-K fp32 partials
   4 head         fc1 reduce/bias/ReLU, fc2, fc3, ReLU-logits, softmax-xent, accuracy, dlogits→dh2→dh1
   5 gemm (x7)    fc1 dgrad + dW1 + dW2 + dW3 + db1 + db2 + db3 in ONE grouped launch
-  6 conv2_dgrad  pool2/ReLU backward gather + conv2 input-gradient (+ conv2 bias-grad partials)
-  7 conv_wgrad   conv2 and conv1 weight gradients (pool1/ReLU backward fused), split-K partials
+  6 conv2_dgrad  pool2/ReLU backward (2x2-ownership gather) + conv2 input-gradient
+  7 conv1_wgrad  pool1/ReLU backward + conv1 weight/bias gradients, split-K partials    } two graph
+    conv2_wgrad  conv2 weight/bias gradients, split-K partials                          } branches
   8 sgd          partial reduction + SGD + LR schedule + bf16 shadow refresh + global_step++ + stats
 
 The batch index list is read through the device-resident global_step (``perm[step % period]``),
@@ -97,8 +98,8 @@ class FusedCifarEngine:
 
         # --- activations / workspaces -------------------------------------------------------
         self.fc1_split = fc1_split or self._pick_fc1_split(B)
-        self.g1 = g1 or max(1, min(B, B // 2))
-        self.g2 = g2 or max(1, min(B, 24 if B >= 24 else B))
+        self.g1 = g1 or max(1, min(B, B // 2))          # conv1 wgrad: 2 images per block
+        self.g2 = g2 or max(1, min(B, B // 5))          # conv2 wgrad: 5 kh blocks x ~5 images
         self.p1, self.am1 = z(B, 12, 12, 64), z(B, 12, 12, 64, dt=torch.uint8)
         self.p2, self.am2 = z(B, 6, 6, 64), z(B, 6, 6, 64, dt=torch.uint8)
         self.h1part = z(self.fc1_split, B, 384, dt=torch.float32)
@@ -106,9 +107,8 @@ class FusedCifarEngine:
         self.dh1, self.dh2 = z(B, 384), z(B, 192)
         self.dp2 = z(B, 6, 6, 64)
         self.dp1, self.dy2 = z(B, 12, 12, 64), z(B, 144, 64)
-        self.dbias2 = z(B, 64, dt=torch.float32)
-        self.part2 = z(self.g2, 1600, 64, dt=torch.float32)
-        self.part1, self.partb1 = z(self.g1, 160, 64, dt=torch.float32), z(self.g1, 64, dt=torch.float32)
+        self.part2, self.partb2 = z(self.g2, 1600, 64, dt=torch.float32), z(self.g2, 64, dt=torch.float32)
+        self.part1, self.partb1 = z(self.g1, 80, 64, dt=torch.float32), z(self.g1, 64, dt=torch.float32)
         self.loss_part = z(B // 16, dt=torch.float32)
         self.correct_part = z(B // 16, dt=torch.int32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -140,6 +140,7 @@ class FusedCifarEngine:
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.comm_stream = torch.cuda.Stream(device=dev) if world_size > 1 else None
+        self.side_stream = torch.cuda.Stream(device=dev)
         self.host_step = 0
         self.refresh_shadows()
 
@@ -189,12 +190,19 @@ class FusedCifarEngine:
 
     def _conv_backward(self):
         o = self.ops
-        o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2, self.dbias2)
-        o.conv_wgrad(self.p1, self.dy2, self.part2, self.data, self.perm, self.step_t, self.period, self.cy,
-                     self.cx, self.dp1, self.am1, self.part1, self.partb1)
+        o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
+        # the two weight-gradient kernels are independent: fork them onto two streams (two parallel
+        # branches of the captured graph) so they share the chip
+        main = torch.cuda.current_stream(self.device)
+        self.side_stream.wait_stream(main)
+        with torch.cuda.stream(self.side_stream):
+            o.conv2_wgrad(self.p1, self.dy2, self.part2, self.partb2)
+        o.conv1_wgrad(self.data, self.perm, self.step_t, self.period, self.cy, self.cx, self.dp1, self.am1,
+                      self.part1, self.partb1)
+        main.wait_stream(self.side_stream)
 
     def _sgd(self, mode: int, scale: float = 1.0):
-        self.ops.sgd(self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.dbias2,
+        self.ops.sgd(self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.partb2,
                      self.w1f, self.w2f, self.w2d, self.fc1n, self.fc2t, self.fc2n, self.fc3t, self.fc3d,
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                      self.loss_part, self.correct_part, self.stats)

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Per-phase timing of every fused-step kernel from in-kernel s_memrealtime stamps (100 MHz).
+
+  DMLC_TIMING=1 python tools/ktiming.py [--batch 256]
+Builds/loads the diagnostic library (libdmlc_hip_timing.so), runs a few eager steps, and prints for
+each kernel: span (first entry -> last stamp), and per slot the median / max over blocks of the time
+since the block's own entry stamp.  Slot meanings are documented at each DMLC_STAMP call site.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+os.environ["DMLC_TIMING"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import dmlc  # noqa: E402,F401
+from dmlc import _build  # noqa: E402
+from dmlc.engine.fused import FusedCifarEngine  # noqa: E402
+
+NAMES = ["conv1_fwd", "conv2_fwd", "gemm(last)", "head", "conv2_dgrad", "conv1_wgrad", "conv2_wgrad", "sgd"]
+NK, NB, NS = 8, 1024, 8
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    a = ap.parse_args()
+    g = torch.Generator().manual_seed(0)
+    data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
+    labels = torch.randint(0, 10, (50000,), dtype=torch.int32, generator=g)
+    eng = FusedCifarEngine(a.batch, data, labels, device="cuda", lr=1e-4)
+    lib = ctypes.CDLL(_build.HIP_LIB)
+    assert lib.dmlc_timing_enabled() == 1, "not a timing build"
+    for _ in range(5):
+        eng.step()
+    torch.cuda.synchronize()
+    lib.dmlc_timing_clear()
+    eng.step()
+    torch.cuda.synchronize()
+    buf = np.zeros(NK * NB * NS, dtype=np.uint64)
+    assert lib.dmlc_timing_read(buf.ctypes.data_as(ctypes.c_void_p)) == 0
+    t = buf.reshape(NK, NB, NS).astype(np.int64)
+    out = {}
+    base = None
+    for k in range(NK):
+        blocks = t[k][t[k][:, 0] > 0]
+        if len(blocks) == 0:
+            continue
+        ent = blocks[:, 0]
+        if base is None or ent.min() < base:
+            base = ent.min()
+    for k in range(NK):
+        blocks = t[k][t[k][:, 0] > 0]
+        if len(blocks) == 0:
+            continue
+        ent = blocks[:, 0]
+        rec = {"blocks": int(len(blocks)), "start_us": round((ent.min() - base) / 100.0, 2)}
+        last = blocks.max()
+        rec["span_us"] = round((last - ent.min()) / 100.0, 2)
+        rec["entry_spread_us"] = round((ent.max() - ent.min()) / 100.0, 2)
+        slots = {}
+        for sl in range(1, NS):
+            v = blocks[:, sl]
+            ok = v > 0
+            if ok.sum() == 0:
+                continue
+            d = (v[ok] - ent[ok]) / 100.0
+            slots[sl] = [round(float(np.median(d)), 2), round(float(d.max()), 2)]
+        rec["slot_med_max_us"] = slots
+        out[NAMES[k]] = rec
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
