@@ -156,64 +156,85 @@ __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
 constexpr int C2_XIN = 256 * 64;
 constexpr int C2_OUT = 144 * 64;
 
-// Wave w owns c_out tile (w & 3) and the pixel tiles 0..4 (w < 4) or 5..8 (w >= 4).  The weight
-// fragments of the tile live in registers, streamed from L2 one kh ahead; every B fragment is one
-// ds_read_b128 of the swizzled LDS image.  (Blocking two c_out tiles per wave halves the LDS reads
-// but doubles the per-block weight stream from L2, which measured 1.6x slower: L2->CU bandwidth,
-// not LDS, is the tighter limit for a 204 KB weight matrix re-read by every image's block.)
-template <int NTILE>
-DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, f32x4 (&acc)[NTILE], int t0, int ct, int g,
-                    int li) {
-  const bf16* W = Wg + (16 * ct + li) * 1600 + 8 * g;
-  int pb[NTILE];
+// conv2-shaped implicit GEMM core, weights staged through LDS.
+// The 64 x 1600 weight matrix is consumed one kh slice (64 co x 320 k, 42 KB with padded rows) at a
+// time: all 512 threads load the slice for kh+1 from L2 into registers while the MFMAs of slice kh
+// run, then store it to the other LDS buffer -- every weight byte crosses L2->CU once per block
+// (streaming it per wave into registers re-read each co tile 2-4x and was L2-bandwidth bound).
+// Wave w owns c_out tiles 2cp, 2cp+1 (cp = w & 1) and pixel tiles pg, pg+4, pg+8 (< 9), pg = w >> 1:
+// per k-chunk it reads 2 A and 2-3 B fragments (ds_read_b128, conflict-free) for 4-6 MFMAs.
+constexpr int WS_LD = 328;                    // 656-B rows: 16 co rows of a fragment hit distinct banks
+constexpr int WS_ELEMS = 64 * WS_LD;
+constexpr size_t WS_BYTES = 2 * WS_ELEMS * 2;
+
+DEV void ws_load(uint4 (&v)[5], const bf16* __restrict__ Wg, int kh, int tid) {
 #pragma unroll
-  for (int t = 0; t < NTILE; ++t) {
-    const int px = 16 * (t0 + t) + li;
+  for (int i = 0; i < 5; ++i) {
+    const int c = tid + i * NT, row = c / 40, k8 = c - row * 40;
+    v[i] = *reinterpret_cast<const uint4*>(Wg + row * 1600 + kh * 320 + k8 * 8);
+  }
+}
+DEV void ws_store(const uint4 (&v)[5], bf16* ws, int tid) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int c = tid + i * NT, row = c / 40, k8 = c - row * 40;
+    *reinterpret_cast<uint4*>(ws + row * WS_LD + k8 * 8) = v[i];
+  }
+}
+
+template <int NPX>
+DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][NPX], int pg, int cp,
+                    int g, int li, int tid) {
+  int pb[NPX];
+#pragma unroll
+  for (int t = 0; t < NPX; ++t) {
+    const int px = 16 * (pg + 4 * t) + li;
     const int y = px / 12;
     pb[t] = y * 16 + (px - y * 12);
   }
 #pragma unroll
-  for (int t = 0; t < NTILE; ++t) acc[t] = zero4();
-  bf16x8 wc[10], wn[10];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) wc[j] = glb_b128(W + j * 32);
+  for (int t = 0; t < NPX; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
+  uint4 pf[5];
+  ws_load(pf, Wg, 0, tid);
+  ws_store(pf, ws, tid);
+  __syncthreads();
 #pragma unroll
   for (int kh = 0; kh < 5; ++kh) {
-    if (kh < 4) {
-#pragma unroll
-      for (int j = 0; j < 10; ++j) wn[j] = glb_b128(W + (kh + 1) * 320 + j * 32);
-    }
+    ws_load(pf, Wg, kh < 4 ? kh + 1 : 4, tid);        // next slice in flight during this one
+    const bf16* wsb = ws + (kh & 1) * WS_ELEMS + (32 * cp + li) * WS_LD + 8 * g;
 #pragma unroll
     for (int kw = 0; kw < 5; ++kw) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        const bf16x8 a0 = lds_b128(wsb + kw * 64 + s * 32);
+        const bf16x8 a1 = lds_b128(wsb + 16 * WS_LD + kw * 64 + s * 32);
 #pragma unroll
-        for (int t = 0; t < NTILE; ++t) {
+        for (int t = 0; t < NPX; ++t) {
           const bf16x8 bx = lds_b128(xin + swz128(pb[t] + kh * 16 + kw, 4 * s + g));
-          acc[t] = mfma16(wc[kw * 2 + s], bx, acc[t]);
+          acc[0][t] = mfma16(a0, bx, acc[0][t]);
+          acc[1][t] = mfma16(a1, bx, acc[1][t]);
         }
       }
     }
-    if (kh < 4) {
-#pragma unroll
-      for (int j = 0; j < 10; ++j) wc[j] = wn[j];
-    }
+    ws_store(pf, ws + ((kh + 1) & 1) * WS_ELEMS, tid);   // (kh == 4: harmless rewrite of slice 4)
+    __syncthreads();
   }
 }
 
 // fn(co_tile, px_tile, acc) for every finished 16x16 output tile of this wave.
 template <class F>
-DEV void conv2_tiles(const bf16* Wg, const bf16* xin, int w, int g, int li, F&& fn) {
-  if (w < 4) {
-    f32x4 acc[5];
-    conv2_core<5>(Wg, xin, acc, 0, w & 3, g, li);
+DEV void conv2_tiles(const bf16* Wg, const bf16* xin, bf16* ws, int w, int g, int li, int tid, F&& fn) {
+  const int cp = w & 1, pg = w >> 1;
+  if (pg == 0) {
+    f32x4 acc[2][3];
+    conv2_core<3>(Wg, xin, ws, acc, pg, cp, g, li, tid);
 #pragma unroll
-    for (int t = 0; t < 5; ++t) fn(w & 3, t, acc[t]);
+    for (int t = 0; t < 3; ++t) { fn(2 * cp, pg + 4 * t, acc[0][t]); fn(2 * cp + 1, pg + 4 * t, acc[1][t]); }
   } else {
-    f32x4 acc[4];
-    conv2_core<4>(Wg, xin, acc, 5, w & 3, g, li);
+    f32x4 acc[2][2];
+    conv2_core<2>(Wg, xin, ws, acc, pg, cp, g, li, tid);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) fn(w & 3, 5 + t, acc[t]);
+    for (int t = 0; t < 2; ++t) { fn(2 * cp, pg + 4 * t, acc[0][t]); fn(2 * cp + 1, pg + 4 * t, acc[1][t]); }
   }
 }
 
@@ -221,6 +242,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd(DmlcConv2FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* xin = reinterpret_cast<bf16*>(smem);
   bf16* cout = xin + C2_XIN;
+  bf16* ws = cout + C2_OUT;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const bf16* in = reinterpret_cast<const bf16*>(a.in) + (size_t)b * 9216;
@@ -243,12 +265,12 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd(DmlcConv2FwdArgs a) {
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) b4[h][i] = a.bias[16 * (w & 3) + 4 * g + i];
+    for (int i = 0; i < 4; ++i) b4[h][i] = a.bias[32 * (w & 1) + 16 * h + 4 * g + i];
   __syncthreads();
   DMLC_STAMP(DMLC_TK_CONV2_FWD, 1);
 
-  conv2_tiles(reinterpret_cast<const bf16*>(a.w), xin, w, g, li, [&](int ct, int t, const f32x4& acc) {
-    store_relu_tile(cout, 16 * t + li, 16 * ct + 4 * g, acc, b4[0]);
+  conv2_tiles(reinterpret_cast<const bf16*>(a.w), xin, ws, w, g, li, tid, [&](int ct, int t, const f32x4& acc) {
+    store_relu_tile(cout, 16 * t + li, 16 * ct + 4 * g, acc, b4[ct & 1]);
   });
   __syncthreads();
   DMLC_STAMP(DMLC_TK_CONV2_FWD, 2);
@@ -262,6 +284,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
   bf16* outs = dyp + C2_XIN;
   bf16* dp2 = outs + C2_OUT;                                    // [36][64] staged pool2 grad
   uint8_t* am2 = reinterpret_cast<uint8_t*>(dp2 + 2304);        // [36][64] staged argmax
+  bf16* ws = reinterpret_cast<bf16*>(am2 + 2304);               // weight slices (conv2_core)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   DMLC_STAMP(DMLC_TK_DGRAD, 0);
@@ -289,10 +312,10 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
       *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8) = v;
     }
   }
-  __syncthreads();
+  lds_barrier();   // publishes dyp only; the dy2 global stores need not drain here
   DMLC_STAMP(DMLC_TK_DGRAD, 2);
 
-  conv2_tiles(reinterpret_cast<const bf16*>(a.wd), dyp, w, g, li, [&](int ct, int t, const f32x4& acc) {
+  conv2_tiles(reinterpret_cast<const bf16*>(a.wd), dyp, ws, w, g, li, tid, [&](int ct, int t, const f32x4& acc) {
     const int px = 16 * t + li, cb = 16 * ct + 4 * g;
     const bf16x4 v = pack4(acc[0], acc[1], acc[2], acc[3]);
     *reinterpret_cast<bf16x4*>(outs + swz128(px, cb >> 3) + ((cb >> 2) & 1) * 4) = v;
@@ -319,7 +342,7 @@ void allow_lds(const void* f, size_t bytes, bool& done) {
     done = true;
   }
 }
-bool g_c1 = false;
+bool g_c1 = false, g_c2 = false, g_dg = false;
 }  // namespace
 
 extern "C" {
@@ -332,13 +355,15 @@ hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s) {
 }
 
 hipError_t dmlc_conv2_fwd(const DmlcConv2FwdArgs* a, hipStream_t s) {
-  const size_t lds = (C2_XIN + C2_OUT) * 2;
+  const size_t lds = (C2_XIN + C2_OUT) * 2 + WS_BYTES;
+  allow_lds(reinterpret_cast<const void*>(&k_conv2_fwd), lds, g_c2);
   hipLaunchKernelGGL(k_conv2_fwd, dim3(a->B), dim3(NT), lds, s, *a);
   return hipGetLastError();
 }
 
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s) {
-  const size_t lds = (C2_XIN + C2_OUT) * 2 + 2304 * 3;
+  const size_t lds = (C2_XIN + C2_OUT) * 2 + 2304 * 3 + WS_BYTES;
+  allow_lds(reinterpret_cast<const void*>(&k_conv2_dgrad), lds, g_dg);
   hipLaunchKernelGGL(k_conv2_dgrad, dim3(a->B), dim3(NT), lds, s, *a);
   return hipGetLastError();
 }

@@ -42,6 +42,10 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
   const int r0 = blockIdx.x * 16;
   DMLC_STAMP(DMLC_TK_HEAD, 0);
 
+  // the loss wave's labels (counter -> index -> label chain) are fetched at entry
+  int label = 0;
+  if (w == 12 && lane < 16) label = a.labels[head_index(a.src, a.B, r0 + lane)];
+
   // fc2 weight fragments of this wave's output tile (waves 0..11: features 16w..16w+15), in flight
   // while the fc1 partial sums are reduced
   bf16x8 w2f[12];
@@ -51,7 +55,9 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     for (int ks = 0; ks < 12; ++ks) w2f[ks] = glb_b128(W + ks * 32);
   }
 
-  // (a) h1 = relu(sum_s part[s] + b1): 16 x 96 float4, at most 2 per thread, all loads in flight
+  // (a) h1 = relu(sum_s part[s] + b1): 16 x 96 float4, at most 2 per thread.  (Issuing all 2 x 8
+  // split loads up front measured slower than 4 at a time: with 16 blocks the head is bound by the
+  // per-CU L2 bandwidth of its ~0.5 MB of weights + partials, not by load latency.)
   {
     float4 acc[2];
     int e[2];
@@ -86,7 +92,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   DMLC_STAMP(DMLC_TK_HEAD, 1);
 
   // (b) h2 = relu(h1 W2 + b2): C[n][r] = sum_k W2t[n][k] h1[r][k]
@@ -113,7 +119,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   DMLC_STAMP(DMLC_TK_HEAD, 2);
 
   // (c) logits = [relu](h2 W3 + b3): wave 12, one 16x16 tile, K = 192
@@ -133,14 +139,13 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
 
   // (d) softmax cross-entropy, accuracy, dlogits (wave 12, lanes 0..15 = rows)
   if (w == 12) {
     float loss = 0.f, corr = 0.f;
     if (lane < 16) {
       const int b = r0 + lane;
-      const int label = a.labels[head_index(a.src, a.B, b)];
       float m = lg[lane][0];
       int am = 0;
 #pragma unroll
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     }
   }
   if (!a.train) return;
-  __syncthreads();
+  lds_barrier();
   DMLC_STAMP(DMLC_TK_HEAD, 3);
 
   // (e) dh2 = (dl W3^T) * (h2 > 0): C[n][r] = sum_k W3d[n][k] dl[r][k], K = 32 (one step), waves 0..11
@@ -189,7 +194,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     *reinterpret_cast<bf16x4*>(dh2s + li * H2_LD + n) = o;
     *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh2) + (size_t)(r0 + li) * 192 + n) = o;
   }
-  __syncthreads();
+  lds_barrier();
   DMLC_STAMP(DMLC_TK_HEAD, 4);
 
   // (f) dh1 = (dh2 W2^T) * (h1 > 0): tiles w and w+16, K = 192

@@ -53,6 +53,16 @@ DEV bf16x4 pack4(float a, float b, float c, float d) {
   return r;
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is a release/acquire fence + s_barrier,
+// and the release waits vmcnt(0) -- on gfx950 vmcnt counts loads AND stores, so a __syncthreads()
+// placed after global stores also drains every prefetch load in flight.  When the barrier only
+// publishes LDS writes, waiting lgkmcnt(0) is enough and global traffic keeps flowing across it.
+DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -1,0 +1,65 @@
+"""Data-parallel fused engine (two graph segments around the bucketed all-reduce + apply-only SGD)
+vs a single-process fused run on the union batch.  Two ranks share the one GPU of the test box and
+talk over gloo (which all-reduces GPU tensors through the host); on an 8-GPU node the same code
+path runs over RCCL.  SURVEY.md §2.D / §4 'Distributed'."""
+import os
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _data():
+    g = torch.Generator().manual_seed(21)
+    x = torch.randint(0, 256, (1024, 32, 32, 3), dtype=torch.uint8, generator=g)
+    y = torch.randint(0, 10, (1024,), dtype=torch.int32, generator=g)
+    return x, y
+
+
+def _rank(rank, world, port, out, B, steps, graph, comm_dtype):
+    sys.path.insert(0, REPO)
+    import torch.distributed as dist
+    import dmlc  # noqa: F401
+    from dmlc.engine.fused import FusedCifarEngine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    x, y = _data()
+    eng = FusedCifarEngine(B, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
+                           relu_logits=False, comm_dtype=comm_dtype)
+    eng.step()
+    if graph:
+        eng.capture()
+    for _ in range(steps - 1):
+        eng.step()
+    torch.cuda.synchronize()
+    torch.save({"flat": eng.flat_params(), "step": eng.global_step(),
+                "shards": [eng.epoch_permutation(0)]}, os.path.join(out, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("graph,comm_dtype", [(False, "fp32"), (True, "fp32"), (True, "bf16")])
+def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype):
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    from dmlc.engine.fused import FusedCifarEngine
+    B, steps = 32, 3
+    mp.spawn(_rank, args=(2, free_port(), str(tmp_path), B, steps, graph, comm_dtype), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
+    assert r0["step"] == r1["step"] == steps
+    assert torch.equal(r0["flat"], r1["flat"])           # replicas identical after every step
+    # single process, batch 2B made of the two ranks' batches of each step
+    s0, s1 = r0["shards"][0], r1["shards"][0]
+    union = torch.cat([torch.cat([s0[i * B:(i + 1) * B], s1[i * B:(i + 1) * B]]) for i in range(len(s0) // B)])
+    x, y = _data()
+    ref = FusedCifarEngine(2 * B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False)
+    ref.epoch_permutation = lambda epoch: union.to(torch.int32)
+    init = ref.flat_params().clone()
+    for _ in range(steps):
+        ref.step()
+    torch.cuda.synchronize()
+    d_dp, d_ref = r0["flat"] - init, ref.flat_params() - init
+    rel = float((d_dp - d_ref).norm() / d_ref.norm())
+    assert rel < (2e-2 if comm_dtype == "bf16" else 1e-2), rel
