@@ -36,7 +36,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--impl", choices=["fused", "eager"], default="fused")
+    ap.add_argument("--impl", choices=["auto", "fused", "eager"], default="auto",
+                    help="fused = hand-written HIP kernels + HIP graph (cifar_cnn); eager = PyTorch ops")
+    ap.add_argument("--model", choices=["cifar_cnn", "resnet20"], default="cifar_cnn")
+    ap.add_argument("--crop", type=int, default=None, help="input crop (default 24 for cifar_cnn, 32 for resnet20)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--dataset-size", type=int, default=50000)
@@ -60,8 +63,8 @@ def build_fused(args, info, data, labels):
 
 def build_eager(args, info, data, labels):
     from dmlc.engine.eager import EagerTrainer
-    tr = EagerTrainer("cifar_cnn", args.batch, data, labels, device=info.device, world_size=info.world_size,
-                      rank=info.rank, dtype="bf16")
+    tr = EagerTrainer(args.model, args.batch, data, labels, device=info.device, world_size=info.world_size,
+                      rank=info.rank, dtype="bf16", crop=args.crop, lr=0.01 if args.model == "resnet20" else 0.1)
     return tr, tr.step, None
 
 
@@ -70,6 +73,12 @@ def main():
     info = D.init(D.env_info(), device="auto")
     if info.world_size != args.gpus and info.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
+    if args.impl == "auto":
+        args.impl = "fused" if args.model == "cifar_cnn" else "eager"
+    if args.crop is None:
+        args.crop = 24 if args.model == "cifar_cnn" else 32
+    if args.impl == "fused" and (args.model != "cifar_cnn" or args.crop != 24):
+        raise SystemExit("the fused HIP engine implements the reference CNN at the 24x24 crop")
     data, labels = make_data(args.dataset_size, info.device)
     builder = build_fused if args.impl == "fused" else build_eager
     eng, step, capture = builder(args, info, data, labels)
@@ -97,7 +106,7 @@ def main():
     value = gbatch * args.steps / elapsed
     if info.rank == 0:
         line = {
-            "metric": "images/sec (whole node) CIFAR-10 CNN training",
+            "metric": "images/sec (whole node) CIFAR-10 CNN training at 1/2/4/8 MI355X",
             "value": round(value, 1),
             "unit": "images/sec",
             "n_gpus": n,
@@ -110,7 +119,8 @@ def main():
             "dtype": "bf16",
             "data": "synthetic uint8 32x32x3 (50k images, device resident), random labels, random-init weights",
             "config": {
-                "model": "cifar10_cnn (conv5x5-64, pool, conv5x5-64, pool, fc384, fc192, fc10; 24x24 center crop)",
+                "model": ("cifar10_cnn (conv5x5-64, pool, conv5x5-64, pool, fc384, fc192, fc10; 24x24 center crop)"
+                          if args.model == "cifar_cnn" else f"resnet20 ({args.crop}x{args.crop} input)"),
                 "global_batch": gbatch,
                 "per_gpu_batch": args.batch,
                 "seq_len": None,

@@ -181,3 +181,27 @@ def load_model_tensors(tensors: Dict[str, torch.Tensor], flat_size: Optional[int
     step = int(tensors["global_step"]) if "global_step" in tensors else 0
     gen = int(tensors["Variable"]) if "Variable" in tensors else 0
     return flat, step, gen
+
+
+def module_tensors(model, global_step: int, generation_num: int = 0) -> Dict[str, torch.Tensor]:
+    """Checkpoint dict of an eager model with flat buffers (``flat`` + optional ``state``)."""
+    d = {s.name: model.flat.detach().cpu()[s.offset:s.offset + s.numel].view(s.shape).clone() for s in model.specs}
+    for s in getattr(model, "state_specs", []):
+        d[s.name] = model.state.detach().cpu()[s.offset:s.offset + s.numel].view(s.shape).clone()
+    d["global_step"] = torch.tensor(int(global_step), dtype=torch.int64)
+    d["Variable"] = torch.tensor(int(generation_num), dtype=torch.int32)
+    return d
+
+
+@torch.no_grad()
+def load_module_tensors(model, tensors: Dict[str, torch.Tensor]) -> int:
+    """Inverse of :func:`module_tensors`; returns global_step."""
+    for specs, buf in ((model.specs, model.flat), (getattr(model, "state_specs", []), getattr(model, "state", None))):
+        for s in specs:
+            if s.name not in tensors:
+                raise KeyError(f"checkpoint is missing {s.name}")
+            t = tensors[s.name]
+            if tuple(t.shape) != tuple(s.shape):
+                raise ValueError(f"{s.name}: checkpoint shape {tuple(t.shape)} != model shape {s.shape}")
+            buf[s.offset:s.offset + s.numel] = t.reshape(-1).to(buf.device, buf.dtype)
+    return int(tensors["global_step"]) if "global_step" in tensors else 0

@@ -65,11 +65,20 @@ class _FusedAdapter:
     def stats(self) -> Dict[str, float]:
         return self.eng.read_stats(self.eng.host_step)
 
-    def flat(self) -> torch.Tensor:
-        return self.eng.flat_params()
+    def tf_tensors(self) -> Dict[str, torch.Tensor]:
+        return CK.model_tensors(self.eng.flat_params(), self.eng.host_step, 0, specs=self.specs)
 
-    def load(self, flat: torch.Tensor, step: int):
+    def load_tf_tensors(self, tensors):
+        flat, step, _ = CK.load_model_tensors(tensors, flat_size=self.eng.master.numel(), specs=self.specs)
         self.eng.load_flat_params(flat, step)
+
+    def broadcast_from_chief(self, info):
+        """Every rank adopts rank 0's parameters and global_step (after a chief-only restore)."""
+        step = torch.tensor([self.eng.host_step], dtype=torch.int64, device=self.eng.device)
+        D.broadcast_(self.eng.master, info)
+        D.broadcast_(step, info)
+        self.eng.set_step(int(step.item()))
+        self.eng.refresh_shadows()
 
     def evaluate(self, x, y, max_batches=0) -> float:
         return self.eng.evaluate(x, y, max_batches)
@@ -104,11 +113,22 @@ class _EagerAdapter:
         return {"global_step": self.tr.global_step, "loss": float(self.tr.last_loss),
                 "accuracy": float(self.tr.last_acc), "lr": self.tr.lr(self.tr.global_step - 1)}
 
-    def flat(self) -> torch.Tensor:
-        return self.tr.flat_params()
+    def tf_tensors(self) -> Dict[str, torch.Tensor]:
+        return CK.module_tensors(self.tr.model, self.tr.global_step, 0)
 
-    def load(self, flat: torch.Tensor, step: int):
-        self.tr.load_flat_params(flat, step)
+    def load_tf_tensors(self, tensors):
+        self.tr.global_step = CK.load_module_tensors(self.tr.model, tensors)
+
+    def broadcast_from_chief(self, info):
+        dev = info.device if info.backend == "nccl" else torch.device("cpu")
+        m = self.tr.model
+        bufs = [m.flat.data] + ([m.state] if hasattr(m, "state") else [])
+        step = torch.tensor([self.tr.global_step], dtype=torch.int64)
+        for b in bufs + [step]:
+            t = b.to(dev)
+            D.broadcast_(t, info)
+            b.copy_(t.to(b.device))
+        self.tr.global_step = int(step.item())
 
     def evaluate(self, x, y, max_batches=0) -> float:
         return self.tr.evaluate(x, y, max_batches)
@@ -160,32 +180,20 @@ class Session:
 
     # --- checkpoint --------------------------------------------------------------------------------
     def restore(self) -> int:
-        """Chief loads the latest checkpoint in log_dir (if any) and broadcasts it to every rank."""
-        step = torch.zeros(1, dtype=torch.int64)
-        flat = self.engine.flat().clone()
-        have = torch.zeros(1, dtype=torch.int64)
+        """Chief loads the latest checkpoint in log_dir (if any); every rank then adopts the chief's
+        parameters and global_step (one authoritative step counter, D2)."""
         if self.chief and self.cfg.log_dir:
             path = CK.latest_checkpoint(self.cfg.log_dir)
             if path:
-                tensors = CK.read_bundle(path)
-                flat, s, _ = CK.load_model_tensors(tensors, flat_size=flat.numel(), specs=self.engine.specs)
-                step[0] = s
-                have[0] = 1
-                self.log(f"Restored {path} (global_step {s})")
+                self.engine.load_tf_tensors(CK.read_bundle(path))
+                self.log(f"Restored {path} (global_step {self.engine.global_step})")
         if self.info.world_size > 1:
-            dev = self.info.device if self.info.backend == "nccl" else torch.device("cpu")
-            bufs = [t.to(dev) for t in (have, step, flat)]
-            for b in bufs:
-                D.broadcast_(b, self.info)
-            have, step, flat = (b.cpu() for b in bufs)
-        if int(have[0]):
-            self.engine.load(flat, int(step[0]))
-        return int(step[0])
+            self.engine.broadcast_from_chief(self.info)
+        return self.engine.global_step
 
     def save(self, force=False):
         if self.ckpt is not None and (force or self.ckpt.due()):
-            gs = self.engine.global_step
-            self.ckpt.save(gs, CK.model_tensors(self.engine.flat(), gs, 0, specs=self.engine.specs))
+            self.ckpt.save(self.engine.global_step, self.engine.tf_tensors())
 
     # --- main loop -----------------------------------------------------------------------------------
     def run(self) -> Dict[str, float]:

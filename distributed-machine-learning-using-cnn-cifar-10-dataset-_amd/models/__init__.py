@@ -7,5 +7,5 @@ def build_model(name: str, seed: int = 0, relu_logits: bool = True, flat=None):
         return CifarCNN(flat=flat, relu_logits=relu_logits, seed=seed)
     if name in ("resnet20", "resnet-20"):
         from .resnet import ResNet20
-        return ResNet20(seed=seed)
+        return ResNet20(flat=flat, seed=seed)   # standard linear logits (the ReLU-logit quirk is the CNN's)
     raise ValueError(f"unknown model {name!r}")
