@@ -80,6 +80,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--comm_dtype", choices=["fp32", "bf16"], default=d.comm_dtype)
     p.add_argument("--pg_timeout_s", type=float, default=d.pg_timeout_s)
     p.add_argument("--graph", type="bool", default=d.graph)
+    p.add_argument("--trace", choices=["", "roctx", "torch"], default=d.trace)
+    p.add_argument("--trace_steps", type=int, default=d.trace_steps)
     return p
 
 

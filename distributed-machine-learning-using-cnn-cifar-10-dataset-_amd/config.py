@@ -76,6 +76,9 @@ class TrainConfig:
     comm_dtype: str = "fp32"              # gradient all-reduce dtype: fp32 | bf16
     pg_timeout_s: float = 300.0           # process-group timeout (fail-fast on a dead rank)
     graph: bool = True                    # capture the fused step into a HIP graph
+    trace: str = ""                       # '' | 'roctx' (phase ranges for rocprofv3 --marker-trace)
+                                          #    | 'torch' (torch.profiler chrome trace in log_dir)
+    trace_steps: int = 20                 # steps covered by a torch.profiler trace
 
     def replace(self, **kw) -> "TrainConfig":
         return dataclasses.replace(self, **kw)

@@ -161,16 +161,17 @@ class FusedCifarEngine:
     # --- data order ---------------------------------------------------------------------------
     def epoch_permutation(self, epoch: int) -> torch.Tensor:
         """Rank-sharded permutation of the dataset for ``epoch`` (D6: every rank sees a disjoint
-        shard; the same global order on every rank because the seed is shared)."""
-        g = torch.Generator().manual_seed(self.seed * 1000003 + epoch)
-        perm = torch.randperm(self.n_data, generator=g)
+        shard; the same global order on every rank because the seed is shared).  Generated on the
+        device (no host round trip at epoch boundaries)."""
+        g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + epoch)
+        perm = torch.randperm(self.n_data, generator=g, device=self.device)
         shard = perm[self.rank::self.world_size][: self.period * self.B]
         return shard.to(torch.int32)
 
     def _maybe_new_epoch(self):
         epoch = self.host_step // self.period
         if epoch != self.cur_epoch:
-            self.perm.copy_(self.epoch_permutation(epoch), non_blocking=False)
+            self.perm.copy_(self.epoch_permutation(epoch))     # stream-ordered, before the step's graph
             self.cur_epoch = epoch
 
     # --- kernels ------------------------------------------------------------------------------

@@ -31,6 +31,7 @@ from .. import checkpoint as CK
 from .. import config as C
 from ..parallel import dist as D
 from ..utils.events import EventsWriter, MetricsLog
+from ..utils.trace import Tracer
 
 
 # --- engine adapters: one interface over the fused HIP engine and the eager torch engine ------------
@@ -172,6 +173,7 @@ class Session:
         self.ckpt = None
         self.events = None
         self.metrics = MetricsLog(None)
+        self.tracer = Tracer(cfg.trace, cfg.log_dir, cfg.trace_steps, max(0, info.rank))
         if self.chief and cfg.log_dir:
             if cfg.save_checkpoints:
                 self.ckpt = CK.CheckpointManager(cfg.log_dir, cfg.max_to_keep, cfg.checkpoint_secs)
@@ -207,9 +209,12 @@ class Session:
         result = {}
         while eng.global_step < cfg.generations:        # StopAtStepHook(last_step=GENERATIONS)
             _fault_injection(eng.global_step, self.info.rank)
-            eng.step()
+            with self.tracer.range("step"):
+                eng.step()
+            self.tracer.step_done()
             if (i + 1) % cfg.output_every == 0:
-                st = eng.stats()
+                with self.tracer.range("stats"):
+                    st = eng.stats()
                 now = time.time()
                 steps = eng.global_step - last_step
                 ips = steps * cfg.batch_size * self.info.world_size / max(1e-9, now - last_t)
@@ -224,14 +229,17 @@ class Session:
                 last_t, last_step = now, eng.global_step
                 result = dict(st, images_per_sec=ips)
             if (i + 1) % cfg.eval_every == 0:
-                acc = eng.evaluate(*self.test, max_batches=cfg.eval_batches)
+                with self.tracer.range("eval"):
+                    acc = eng.evaluate(*self.test, max_batches=cfg.eval_batches)
                 self.log(" --- Test Accuracy = {:.2f}%.".format(100.0 * acc))
                 self.metrics.write(step=eng.global_step, test_accuracy=acc)
                 result["test_accuracy"] = acc
             if self.ckpt is not None and self.ckpt.due():
-                self.save()
+                with self.tracer.range("checkpoint"):
+                    self.save()
             i += 1
         eng.sync()
+        self.tracer.close()
         self.save(force=True)            # CheckpointSaverHook.end
         result["global_step"] = eng.global_step
         if self.events is not None:

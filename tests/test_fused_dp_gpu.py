@@ -35,7 +35,7 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype):
         eng.step()
     torch.cuda.synchronize()
     torch.save({"flat": eng.flat_params(), "step": eng.global_step(),
-                "shards": [eng.epoch_permutation(0)]}, os.path.join(out, f"r{rank}.pt"))
+                "shards": [eng.epoch_permutation(0).cpu()]}, os.path.join(out, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
