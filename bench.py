@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--crop", type=int, default=None, help="input crop (default 24 for cifar_cnn, 32 for resnet20)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
     ap.add_argument("--dataset-size", type=int, default=50000)
     return ap.parse_args()
 
@@ -56,7 +58,7 @@ def make_data(n, device, seed=0):
 def build_fused(args, info, data, labels):
     from dmlc.engine.fused import FusedCifarEngine
     eng = FusedCifarEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
-                           rank=info.rank, seed=0, comm_dtype=args.comm_dtype)
+                           rank=info.rank, seed=0, comm_dtype=args.comm_dtype, dtype=args.dtype)
     step = eng.step
     return eng, step, (None if args.no_graph else eng.capture)
 
@@ -116,7 +118,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": "synthetic uint8 32x32x3 (50k images, device resident), random labels, random-init weights",
             "config": {
                 "model": ("cifar10_cnn (conv5x5-64, pool, conv5x5-64, pool, fc384, fc192, fc10; 24x24 center crop)"

@@ -67,7 +67,8 @@ void check_data(const Tensor& data) {
 }
 
 void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
-               int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& out, const Tensor& am) {
+               int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& out, const Tensor& am,
+               const c10::optional<Tensor>& amax) {
   const int64_t B = out.size(0);
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
@@ -82,7 +83,42 @@ void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   a.B = (int)B; a.cy = (int)cy; a.cx = (int)cx;
   a.w = w1f.data_ptr(); a.bias = b1.data_ptr<float>();
   a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>();
+  a.amax = nullptr;
+  if (amax.has_value()) {
+    check_numel(*amax, "amax", at::kFloat, 2);
+    a.amax = amax->data_ptr<float>();
+  }
   CHECK_HIP(dmlc_conv1_fwd(&a, stream_of(out)));
+}
+
+void conv2_fwd_fp8(const Tensor& in, const Tensor& w8, const Tensor& b2, const Tensor& amax_x, const Tensor& scale_w,
+                   const c10::optional<Tensor>& counter, const Tensor& out, const Tensor& am) {
+  const int64_t B = in.size(0);
+  check(in, "in", at::kBFloat16, {B, 12, 12, 64});
+  check(w8, "w8", at::kByte, {64, 1600});
+  check_numel(b2, "b2", at::kFloat, 64);
+  check_numel(amax_x, "amax_x", at::kFloat, 2);
+  check_numel(scale_w, "scale_w", at::kFloat, 2);
+  check(out, "out", at::kBFloat16, {B, 6, 6, 64});
+  check(am, "am", at::kByte, {B, 6, 6, 64});
+  c10::DeviceGuard guard(in.device());
+  DmlcConv2FwdFp8Args a;
+  a.in = in.data_ptr(); a.w8 = w8.data_ptr<uint8_t>(); a.bias = b2.data_ptr<float>();
+  a.amax_x = amax_x.data_ptr<float>(); a.scale_w = scale_w.data_ptr<float>();
+  a.counter = nullptr;
+  if (counter.has_value()) {
+    check_numel(*counter, "counter", at::kLong, 1);
+    a.counter = counter->data_ptr<int64_t>();
+  }
+  a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>(); a.B = (int)B;
+  CHECK_HIP(dmlc_conv2_fwd_fp8(&a, stream_of(in)));
+}
+
+void fp8_roundtrip(const Tensor& x, const Tensor& y, double scale) {
+  check_numel(x, "x", at::kFloat, x.numel());
+  check_numel(y, "y", at::kFloat, x.numel());
+  c10::DeviceGuard guard(x.device());
+  CHECK_HIP(dmlc_fp8_roundtrip(x.data_ptr<float>(), y.data_ptr<float>(), (int)x.numel(), (float)scale, stream_of(x)));
 }
 
 void conv2_fwd(const Tensor& in, const Tensor& w2f, const Tensor& b2, const Tensor& out, const Tensor& am) {
@@ -246,7 +282,8 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
          const Tensor& w2f, const Tensor& w2d, const Tensor& fc1n, const Tensor& fc2t, const Tensor& fc2n,
          const Tensor& fc3t, const Tensor& fc3d, const Tensor& step, double lr0, double decay, double decay_steps,
          bool staircase, const Tensor& ticket, const Tensor& loss_part, const Tensor& correct_part,
-         const Tensor& stats) {
+         const Tensor& stats, const c10::optional<Tensor>& w2f8, const c10::optional<Tensor>& amax_w,
+         const c10::optional<Tensor>& scale_w) {
   TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
   TORCH_CHECK(off.size() == 10, "off must have 10 entries");
   static const int64_t numel[10] = {4800, 64, 102400, 64, 884736, 384, 73728, 192, 1920, 10};
@@ -294,6 +331,14 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
   a.nhead = (int)loss_part.numel();
   a.stats = stats.data_ptr<float>(); a.stats_len = (int)stats.size(0);
+  a.w2f8 = nullptr; a.amax_w = nullptr; a.scale_w = nullptr;
+  if (w2f8.has_value()) {
+    TORCH_CHECK(amax_w.has_value() && scale_w.has_value(), "fp8 shadow needs amax_w and scale_w");
+    check(*w2f8, "w2f8", at::kByte, {64, 1600});
+    check_numel(*amax_w, "amax_w", at::kFloat, 2);
+    check_numel(*scale_w, "scale_w", at::kFloat, 2);
+    a.w2f8 = w2f8->data_ptr<uint8_t>(); a.amax_w = amax_w->data_ptr<float>(); a.scale_w = scale_w->data_ptr<float>();
+  }
   CHECK_HIP(dmlc_sgd(&a, stream_of(master)));
 }
 
@@ -301,7 +346,10 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
 
 TORCH_LIBRARY(dmlc, m) {
   m.def("conv1_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
+        "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? amax) -> ()");
+  m.def("conv2_fwd_fp8(Tensor inp, Tensor w8, Tensor b2, Tensor amax_x, Tensor scale_w, Tensor? counter, "
         "Tensor(a!) out, Tensor(b!) am) -> ()");
+  m.def("fp8_roundtrip(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("conv2_fwd(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv1_wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
@@ -316,12 +364,14 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
-        "Tensor(m!) stats) -> ()");
+        "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("conv1_fwd", &conv1_fwd);
   m.impl("conv2_fwd", &conv2_fwd);
+  m.impl("conv2_fwd_fp8", &conv2_fwd_fp8);
+  m.impl("fp8_roundtrip", &fp8_roundtrip);
   m.impl("conv2_dgrad", &conv2_dgrad);
   m.impl("conv1_wgrad", &conv1_wgrad);
   m.impl("conv2_wgrad", &conv2_wgrad);

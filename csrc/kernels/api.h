@@ -28,6 +28,8 @@ struct DmlcConv1FwdArgs {
   const float* bias;        // [64]
   void* out;                // bf16 [B][12][12][64]
   uint8_t* am;              // [B][12][12][64] argmax (0..8) in the pool window, 255 = no gradient
+  float* amax;              // nullable: fp8 path, float[2] running max of the pooled output, slot
+                            //   (step & 1) accumulated (atomic max), slot (step+1) & 1 zeroed
 };
 
 // conv2 5x5 (64->64) + bias + ReLU + maxpool 3x3/2 TF-SAME.  One workgroup per image.
@@ -36,6 +38,21 @@ struct DmlcConv2FwdArgs {
   const void* w;            // bf16 [64 co][1600]  (k = (kh*5+kw)*64 + ci)
   const float* bias;        // [64]
   void* out;                // bf16 [B][6][6][64]  (== [B][2304], NHWC flatten order)
+  uint8_t* am;              // [B][6][6][64]
+  int B;
+};
+
+// conv2 forward on fp8 (OCP e4m3fn) MFMA operands, per-tensor scales (BASELINE config 5).
+// x8 = sat(x * 448 / amax_x[step&1]), w8 = w2f8 (quantised by the SGD kernel with scale_w[step&1]);
+// out = relu(acc / (sx * sw) + b), then the same TF-SAME pool as the bf16 path.
+struct DmlcConv2FwdFp8Args {
+  const void* in;           // bf16 [B][12][12][64]
+  const uint8_t* w8;        // fp8 [64 co][1600]
+  const float* bias;        // [64]
+  const float* amax_x;      // float[2] (conv1 pool output amax, slot step & 1)
+  const float* scale_w;     // float[2] (weight quantisation scale, slot step & 1)
+  const int64_t* counter;   // device global_step (nullable: slot 0)
+  void* out;                // bf16 [B][6][6][64]
   uint8_t* am;              // [B][6][6][64]
   int B;
 };
@@ -132,10 +149,16 @@ struct DmlcSgdArgs {
   const float* loss_part; const int* correct_part; int nhead;
   float* stats; int stats_len;   // ring [stats_len][4] = {step, loss, accuracy, lr}
   int nblocks;
+  // fp8 conv2 shadow (nullable).  Modes 0/2 quantise the updated W2 with sw = 224 / amax_w[step&1]
+  // (2x headroom over the previous weights' amax), store sw to scale_w[(step+1)&1] and the new amax
+  // to amax_w[(step+1)&1]; the last arriver zeroes amax_w[step&1].  Mode 3 uses/stores slot step&1.
+  uint8_t* w2f8; float* amax_w; float* scale_w;
 };
 
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_fwd(const DmlcConv2FwdArgs* a, hipStream_t s);
+hipError_t dmlc_conv2_fwd_fp8(const DmlcConv2FwdFp8Args* a, hipStream_t s);
+hipError_t dmlc_fp8_roundtrip(const float* x, float* y, int n, float scale, hipStream_t s);
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s);
 hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s);

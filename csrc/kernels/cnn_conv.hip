@@ -24,7 +24,6 @@
 
 namespace dmlc {
 
-constexpr int NT = 512;   // 8 waves per image: 2 waves per SIMD hide each other's LDS / memory latency
 
 // ---------------------------------------------------------------------------------------------
 // conv1 input image: 24x24 crop of the uint8 NHWC image at (cy,cx), zero halo of 2, stored as
@@ -40,57 +39,6 @@ DEV void stage_conv1_input(bf16* xin, const uint8_t* src, int cy, int cx, int ti
     const uint8_t* s = src + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);     // branch-free loads
     const float c0 = s[0], c1 = s[1], c2 = s[2];
     *reinterpret_cast<bf16x4*>(xin + p * 4) = ok ? pack4(c0, c1, c2, 0.f) : pack4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
-// Epilogue helper: acc (C[4g+i][px]) + bias -> ReLU -> bf16 -> LDS [px][64] swizzled.
-DEV void store_relu_tile(bf16* cout, int px, int co_base, const f32x4& acc, const float* b4) {
-  const bf16x4 v = pack4(fmaxf(acc[0] + b4[0], 0.f), fmaxf(acc[1] + b4[1], 0.f),
-                         fmaxf(acc[2] + b4[2], 0.f), fmaxf(acc[3] + b4[3], 0.f));
-  const int chunk = co_base >> 3, half = (co_base >> 2) & 1;
-  *reinterpret_cast<bf16x4*>(cout + swz128(px, chunk) + half * 4) = v;
-}
-
-// TF-SAME 3x3/2 max-pool over an LDS image [H*W][64] (swizzled) -> global out [HO*WO][64] bf16 +
-// argmax bytes.  Padding is bottom/right only (in = 2*out), padded cells never win.
-// The inputs are post-ReLU (>= 0), so bf16 bit patterns order like their values: each candidate is a
-// 32-bit key (bits << 16 | 15 - d) and one integer max per element keeps value AND first argmax
-// (ties -> smallest d, like a strict '>' scan).  Sign bits are masked so a -0.0 ranks as 0.
-template <int H>
-DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid) {
-  constexpr int HO = H / 2;
-  for (int task = tid; task < HO * HO * 8; task += NT) {
-    const int q = task >> 3, c = task & 7;
-    const int py = q / HO, px = q - py * HO;
-    uint32_t key[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) key[j] = 0;
-#pragma unroll
-    for (int d = 0; d < 9; ++d) {
-      const int y = 2 * py + d / 3, x = 2 * px + d % 3;
-      if ((d / 3 < 2 || y < H) && (d % 3 < 2 || x < H)) {
-        const uint4 v = *reinterpret_cast<const uint4*>(cout + swz128(y * H + x, c));
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, tag = 15 - d;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          key[2 * i] = max(key[2 * i], ((wv[i] << 16) & 0x7fff0000u) | tag);
-          key[2 * i + 1] = max(key[2 * i + 1], (wv[i] & 0x7fff0000u) | tag);
-        }
-      }
-    }
-    uint4 o;
-    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
-    uint32_t alo = 0, ahi = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ow[i] = (key[2 * i] >> 16) | (key[2 * i + 1] & 0xffff0000u);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t arg = (key[j] >> 16) ? 15 - (key[j] & 15) : 255;
-      if (j < 4) alo |= arg << (8 * j);
-      else ahi |= arg << (8 * (j - 4));
-    }
-    *reinterpret_cast<uint4*>(out + q * 64 + c * 8) = o;
-    *reinterpret_cast<uint2*>(am + q * 64 + c * 8) = make_uint2(alo, ahi);
   }
 }
 
@@ -145,7 +93,17 @@ __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
       store_relu_tile(cout, (pq * 9 + t) * 16 + li, 32 * cp + 16 * h + 4 * g, acc[h][t], b4[h]);
   __syncthreads();
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 2);
-  pool_emit<24>(cout, reinterpret_cast<bf16*>(a.out) + (size_t)b * 9216, a.am + (size_t)b * 9216, tid);
+  uint32_t vmax = 0;
+  pool_emit<24>(cout, reinterpret_cast<bf16*>(a.out) + (size_t)b * 9216, a.am + (size_t)b * 9216, tid, &vmax);
+  if (a.amax) {                                // fp8 path: running max of the pooled activations
+    const int slot = a.src.counter ? (int)(*a.src.counter & 1) : 0;
+    uint32_t m = vmax;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if ((tid & 63) == 0 && m)                  // bf16 bits -> fp32 bits preserve order for x >= 0
+      atomicMax(reinterpret_cast<unsigned int*>(a.amax) + slot, m << 16);
+    if (b == 0 && tid == 0) a.amax[slot ^ 1] = 0.f;
+  }
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 3);
 }
 

@@ -84,6 +84,22 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[2] + e) = g; return; }
   const float4 w = sgd4(a.master + a.off[2] + e, g, lr, a.grad_scale, a.mode != 3);
   const int ci = krow & 63, khw = krow >> 6;
+  if (a.w2f8) {                                       // fp8 shadow for the fp8 conv2 forward
+    const int64_t step = *a.step;
+    const int cur = (int)(step & 1), nxt = a.mode == 3 ? cur : cur ^ 1;
+    const float sw = 224.f / fmaxf(a.amax_w[cur], 1e-20f);
+    const uint32_t q = pk_fp8x4(w.x * sw, w.y * sw, w.z * sw, w.w * sw);
+    uint8_t* w8 = a.w2f8 + krow;
+    w8[(co + 0) * 1600] = (uint8_t)q; w8[(co + 1) * 1600] = (uint8_t)(q >> 8);
+    w8[(co + 2) * 1600] = (uint8_t)(q >> 16); w8[(co + 3) * 1600] = (uint8_t)(q >> 24);
+    if (threadIdx.x == 0) a.scale_w[nxt] = sw;       // identical value from every block
+    if (a.mode != 3) {
+      float m = fmaxf(fmaxf(fabsf(w.x), fabsf(w.y)), fmaxf(fabsf(w.z), fabsf(w.w)));
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned int*>(a.amax_w) + nxt, __float_as_uint(m));
+    }
+  }
   // w2d[ci][((4-kh)*5 + (4-kw))*64 + co] : contiguous in co
   *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.w2d) + (size_t)ci * 1600 + (24 - khw) * 64 + co) =
       pack4(w.x, w.y, w.z, w.w);
@@ -204,6 +220,7 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
       st[2] = (float)corr / (float)a.B;
       st[3] = lr;
       *a.step = step + 1;
+      if (a.w2f8) a.amax_w[step & 1] = 0.f;           // every block has read it; next step's target
       __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

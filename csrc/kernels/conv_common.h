@@ -5,6 +5,8 @@
 
 namespace dmlc {
 
+constexpr int NT = 512;   // per-image conv kernels: 8 waves, 2 per SIMD hide each other's latency
+
 DEV int batch_index(const DmlcIndexSrc& s, int B, int b) {
   int row = 0;
   if (s.counter) row = (int)(*s.counter % (int64_t)s.period);
@@ -121,6 +123,61 @@ DEV void block_chunk_sum(float (&v)[8], float* red /*[4][64]*/, int tid) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[w * 64 + lane * 8 + j] = v[j];
   }
+}
+
+// Epilogue helper: acc (C[4g+i][px]) + bias -> ReLU -> bf16 -> LDS [px][64] swizzled.
+DEV void store_relu_tile(bf16* cout, int px, int co_base, const f32x4& acc, const float* b4) {
+  const bf16x4 v = pack4(fmaxf(acc[0] + b4[0], 0.f), fmaxf(acc[1] + b4[1], 0.f),
+                         fmaxf(acc[2] + b4[2], 0.f), fmaxf(acc[3] + b4[3], 0.f));
+  const int chunk = co_base >> 3, half = (co_base >> 2) & 1;
+  *reinterpret_cast<bf16x4*>(cout + swz128(px, chunk) + half * 4) = v;
+}
+
+// TF-SAME 3x3/2 max-pool over an LDS image [H*W][64] (swizzled) -> global out [HO*WO][64] bf16 +
+// argmax bytes.  Padding is bottom/right only (in = 2*out), padded cells never win.
+// The inputs are post-ReLU (>= 0), so bf16 bit patterns order like their values: each candidate is a
+// 32-bit key (bits << 16 | 15 - d) and one integer max per element keeps value AND first argmax
+// (ties -> smallest d, like a strict '>' scan).  Sign bits are masked so a -0.0 ranks as 0.
+template <int H>
+DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid, uint32_t* vmax = nullptr) {
+  constexpr int HO = H / 2;
+  uint32_t bmax = 0;                           // max pooled bf16 bits of this thread (fp8 scaling)
+  for (int task = tid; task < HO * HO * 8; task += NT) {
+    const int q = task >> 3, c = task & 7;
+    const int py = q / HO, px = q - py * HO;
+    uint32_t key[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) key[j] = 0;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+      const int y = 2 * py + d / 3, x = 2 * px + d % 3;
+      if ((d / 3 < 2 || y < H) && (d % 3 < 2 || x < H)) {
+        const uint4 v = *reinterpret_cast<const uint4*>(cout + swz128(y * H + x, c));
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, tag = 15 - d;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          key[2 * i] = max(key[2 * i], ((wv[i] << 16) & 0x7fff0000u) | tag);
+          key[2 * i + 1] = max(key[2 * i + 1], (wv[i] & 0x7fff0000u) | tag);
+        }
+      }
+    }
+    uint4 o;
+    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+    uint32_t alo = 0, ahi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ow[i] = (key[2 * i] >> 16) | (key[2 * i + 1] & 0xffff0000u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bmax = max(bmax, key[j] >> 16);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t arg = (key[j] >> 16) ? 15 - (key[j] & 15) : 255;
+      if (j < 4) alo |= arg << (8 * j);
+      else ahi |= arg << (8 * (j - 4));
+    }
+    *reinterpret_cast<uint4*>(out + q * 64 + c * 8) = o;
+    *reinterpret_cast<uint2*>(am + q * 64 + c * 8) = make_uint2(alo, ahi);
+  }
+  if (vmax) *vmax = bmax;
 }
 
 }  // namespace dmlc

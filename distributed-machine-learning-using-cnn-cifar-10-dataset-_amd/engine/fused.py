@@ -58,7 +58,7 @@ class FusedCifarEngine:
                  relu_logits: bool = True, crop_offset=(4, 4), world_size: int = 1, rank: int = 0,
                  process_group=None, seed: int = 0, fc1_split: Optional[int] = None, g1: Optional[int] = None,
                  g2: Optional[int] = None, stats_len: int = 4096, comm_dtype: str = "fp32",
-                 capture_comm: bool = False):
+                 capture_comm: bool = False, dtype: str = "bf16"):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -74,6 +74,9 @@ class FusedCifarEngine:
         self.comm_dtype = comm_dtype
         self.capture_comm = capture_comm
         self.seed = seed
+        if dtype not in ("bf16", "fp8"):
+            raise ValueError("fused engine dtype must be bf16 or fp8")
+        self.dtype = dtype
 
         # --- data (device resident) ---------------------------------------------------------
         assert data.dtype == torch.uint8 and tuple(data.shape[1:]) == (32, 32, 3)
@@ -95,6 +98,13 @@ class FusedCifarEngine:
         self.w1f, self.w2f, self.w2d = z(64, 160), z(64, 1600), z(64, 1600)
         self.fc1n, self.fc2t, self.fc2n = z(2304, 384), z(192, 384), z(384, 192)
         self.fc3t, self.fc3d = z(16, 192), z(192, 32)
+        # fp8 conv2 forward (BASELINE config 5): e4m3 weight shadow + delayed per-tensor scales
+        self.fp8 = dtype == "fp8"
+        if self.fp8:
+            self.w2f8 = z(64, 1600, dt=torch.uint8)
+            self.amax_x = z(2, dt=torch.float32)
+            self.amax_w = z(2, dt=torch.float32)
+            self.scale_w = z(2, dt=torch.float32)
 
         # --- activations / workspaces -------------------------------------------------------
         self.fc1_split = fc1_split or self._pick_fc1_split(B)
@@ -152,6 +162,11 @@ class FusedCifarEngine:
         return int(max(1, min(9, round(192 / tiles))))
 
     def refresh_shadows(self):
+        if self.fp8:    # exact amax of the current W2 for the shadow quantisation at this step
+            s = self.host_step & 1
+            w2 = self.master[SEG["conv2_kernel"].offset:SEG["conv2_kernel"].offset + SEG["conv2_kernel"].numel]
+            self.amax_w[s] = w2.abs().max()
+            self.amax_w[s ^ 1] = 0.0
         self._sgd(mode=3)
 
     def set_step(self, step: int):
@@ -177,8 +192,12 @@ class FusedCifarEngine:
     # --- kernels ------------------------------------------------------------------------------
     def _forward(self, idx, counter, period, train=True, logits_out=None):
         o, p, B = self.ops, self.pv, self.B
-        o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1, self.am1)
-        o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
+        o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1, self.am1,
+                    self.amax_x if self.fp8 else None)
+        if self.fp8:
+            o.conv2_fwd_fp8(self.p1, self.w2f8, p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
+        else:
+            o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
         f = self._fc1_fwd
         o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
         o.head(self.h1part, p["full_bias_1"], self.fc2t, p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d,
@@ -206,7 +225,8 @@ class FusedCifarEngine:
         self.ops.sgd(self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.partb2,
                      self.w1f, self.w2f, self.w2d, self.fc1n, self.fc2t, self.fc2n, self.fc3t, self.fc3d,
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
-                     self.loss_part, self.correct_part, self.stats)
+                     self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
+                                                                      if self.fp8 else (None, None, None)))
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -319,6 +339,8 @@ class FusedCifarEngine:
         labels = labels.to(self.device, torch.int32).contiguous()
         saved = (self.data, self.labels)
         self.data, self.labels = data, labels
+        if self.fp8:    # eval launches carry no step counter: they read scale slot 0 (see cnn_fp8.hip)
+            self.scale_w[0] = self.scale_w[self.host_step & 1]
         n = data.shape[0]
         nb = math.ceil(n / self.B)
         if max_batches:
@@ -340,6 +362,8 @@ class FusedCifarEngine:
     @torch.no_grad()
     def forward_logits(self, idx: torch.Tensor) -> torch.Tensor:
         """Logits (fp32 [B,10]) of dataset rows ``idx`` (int32 [B]) — for tests."""
+        if self.fp8:
+            self.scale_w[0] = self.scale_w[self.host_step & 1]
         self._forward(idx.to(self.device, torch.int32).contiguous(), None, 1, train=False, logits_out=self.logits_buf)
         return self.logits_buf.clone()
 

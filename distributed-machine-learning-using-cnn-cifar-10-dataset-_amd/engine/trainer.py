@@ -44,7 +44,8 @@ class _FusedAdapter:
                                     rank=max(0, info.rank), seed=cfg.seed, lr=cfg.learning_rate,
                                     lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                     staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
-                                    crop_offset=((32 - cfg.crop) // 2,) * 2, comm_dtype=cfg.comm_dtype)
+                                    crop_offset=((32 - cfg.crop) // 2,) * 2, comm_dtype=cfg.comm_dtype,
+                                    dtype=cfg.dtype)
         self.graph = cfg.graph
         from ..models import cifar_cnn as M
         self.specs = M.PARAM_SPECS
@@ -142,7 +143,7 @@ class _EagerAdapter:
 def pick_impl(cfg: C.TrainConfig, device: torch.device) -> str:
     if cfg.impl != "auto":
         return cfg.impl
-    if (device.type == "cuda" and cfg.model == "cifar_cnn" and cfg.dtype == "bf16" and cfg.crop == 24
+    if (device.type == "cuda" and cfg.model == "cifar_cnn" and cfg.dtype in ("bf16", "fp8") and cfg.crop == 24
             and cfg.batch_size % 16 == 0 and not cfg.augment):
         return "fused"
     return "eager"

@@ -24,7 +24,9 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype):
     import torch.distributed as dist
     import dmlc  # noqa: F401
     from dmlc.engine.fused import FusedCifarEngine
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    import datetime
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))   # a failing peer must not hang the suite
     x, y = _data()
     eng = FusedCifarEngine(B, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
                            relu_logits=False, comm_dtype=comm_dtype)
@@ -39,6 +41,7 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype):
     dist.destroy_process_group()
 
 
+@pytest.mark.timeout(240)
 @pytest.mark.parametrize("graph,comm_dtype", [(False, "fp32"), (True, "fp32"), (True, "bf16")])
 def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype):
     import torch.multiprocessing as mp
