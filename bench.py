@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--model", choices=["cifar_cnn", "resnet20"], default="cifar_cnn")
     ap.add_argument("--crop", type=int, default=None, help="input crop (default 24 for cifar_cnn, 32 for resnet20)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--eager-graph", action="store_true",
+                    help="capture the eager (PyTorch-op) step into a HIP graph (ResNet-20 path; the "
+                         "framework-default comparison line is measured without it)")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
@@ -66,7 +69,8 @@ def build_fused(args, info, data, labels):
 def build_eager(args, info, data, labels):
     from dmlc.engine.eager import EagerTrainer
     tr = EagerTrainer(args.model, args.batch, data, labels, device=info.device, world_size=info.world_size,
-                      rank=info.rank, dtype="bf16", crop=args.crop, lr=0.01 if args.model == "resnet20" else 0.1)
+                      rank=info.rank, dtype="bf16", crop=args.crop, lr=0.01 if args.model == "resnet20" else 0.1,
+                      graph=args.eager_graph)
     return tr, tr.step, None
 
 
@@ -127,7 +131,8 @@ def main():
                 "per_gpu_batch": args.batch,
                 "seq_len": None,
                 "parallelism": f"dp{n}",
-                "impl": args.impl + ("" if args.impl != "fused" or args.no_graph else "+hipgraph"),
+                "impl": args.impl + ("+hipgraph" if (args.impl == "fused" and not args.no_graph)
+                                     or (args.impl == "eager" and args.eager_graph) else ""),
                 "comm_dtype": args.comm_dtype,
             },
         }

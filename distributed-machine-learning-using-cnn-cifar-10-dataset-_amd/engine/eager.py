@@ -25,7 +25,7 @@ class EagerTrainer:
                  lr: float = C.LEARNING_RATE, lr_decay: float = C.LR_DECAY,
                  decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, relu_logits: bool = True,
                  crop: int = C.CROP_HEIGHT, seed: int = 0, flat_params: Optional[torch.Tensor] = None,
-                 augment: bool = False):
+                 augment: bool = False, graph: bool = False):
         self.device = torch.device(device)
         self.model = build_model(model, seed=seed, relu_logits=relu_logits, flat=flat_params).to(self.device)
         self.B = int(batch_size)
@@ -47,6 +47,11 @@ class EagerTrainer:
         self.last_loss = float("nan")
         self.last_acc = float("nan")
         self.buckets = self.model.grad_buckets() if hasattr(self.model, "grad_buckets") else None
+        # HIP-graph capture of the whole step (single process, GPU, no augmentation): static batch
+        # buffers + a device-resident LR so the captured SGD stays valid across replays
+        self.use_graph = graph and self.device.type == "cuda" and world_size == 1 and not augment
+        self.graph = None
+        self._warm = 0
 
     # ------------------------------------------------------------------------------------------
     def lr(self, step: int) -> float:
@@ -94,26 +99,64 @@ class EagerTrainer:
             if b is None:
                 break
 
-    def step(self):
-        x, y = self.batch(self.global_step)
-        self.model.train()
+    def _fwd_bwd_sgd(self, x, y, lr):
+        """One training step's device work; ``lr`` is a float or a 0-d device tensor."""
         use_amp = self.dtype == "bf16" and self.device.type == "cuda"
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=use_amp):
             logits = self.model(x)
         loss = torch.nn.functional.cross_entropy(logits.float(), y)
-        for p in self.model.parameters():
-            p.grad = None
         loss.backward()
         self._allreduce_grads()
-        lr = self.lr(self.global_step)
         with torch.no_grad():
             for p in self.model.parameters():
                 if p.grad is not None:
-                    p.add_(p.grad, alpha=-lr)
+                    if torch.is_tensor(lr):
+                        p.addcmul_(p.grad, lr, value=-1.0)
+                    else:
+                        p.add_(p.grad, alpha=-lr)
         if hasattr(self.model, "after_step"):
             self.model.after_step()
-        self.last_loss = loss.detach()
-        self.last_acc = (logits.detach().argmax(1) == y).float().mean()
+        return loss.detach(), (logits.detach().argmax(1) == y).float().mean()
+
+    def step(self):
+        x, y = self.batch(self.global_step)
+        self.model.train()
+        if not self.use_graph:
+            for p in self.model.parameters():
+                p.grad = None
+            self.last_loss, self.last_acc = self._fwd_bwd_sgd(x, y, self.lr(self.global_step))
+            self.global_step += 1
+            return
+        if self.graph is None:
+            if self._warm == 0:
+                self._xs, self._ys = x.clone(), y.clone()
+                self._lr_t = torch.zeros((), device=self.device)
+                self._side = torch.cuda.Stream(device=self.device)
+            self._xs.copy_(x)
+            self._ys.copy_(y)
+            self._lr_t.fill_(self.lr(self.global_step))
+            self._side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self._side):          # warm-up off the capture stream
+                for p in self.model.parameters():
+                    p.grad = None
+                self.last_loss, self.last_acc = self._fwd_bwd_sgd(self._xs, self._ys, self._lr_t)
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._warm += 1
+            self.global_step += 1
+            if self._warm == 3:
+                for p in self.model.parameters():
+                    p.grad = None
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):           # records only: the model does not advance here
+                    self._out = self._fwd_bwd_sgd(self._xs, self._ys, self._lr_t)
+                self.graph = g
+                torch.cuda.synchronize(self.device)
+            return
+        self._xs.copy_(x)
+        self._ys.copy_(y)
+        self._lr_t.fill_(self.lr(self.global_step))
+        self.graph.replay()
+        self.last_loss, self.last_acc = self._out
         self.global_step += 1
 
     def flat_params(self) -> torch.Tensor:
