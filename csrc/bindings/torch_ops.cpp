@@ -283,7 +283,8 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
          const Tensor& fc3t, const Tensor& fc3d, const Tensor& step, double lr0, double decay, double decay_steps,
          bool staircase, const Tensor& ticket, const Tensor& loss_part, const Tensor& correct_part,
          const Tensor& stats, const c10::optional<Tensor>& w2f8, const c10::optional<Tensor>& amax_w,
-         const c10::optional<Tensor>& scale_w) {
+         const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize) {
+  TORCH_CHECK(roles >= 0 && roles <= 2, "sgd roles must be 0..2");
   TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
   TORCH_CHECK(off.size() == 10, "off must have 10 entries");
   static const int64_t numel[10] = {4800, 64, 102400, 64, 884736, 384, 73728, 192, 1920, 10};
@@ -332,6 +333,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   a.nhead = (int)loss_part.numel();
   a.stats = stats.data_ptr<float>(); a.stats_len = (int)stats.size(0);
   a.w2f8 = nullptr; a.amax_w = nullptr; a.scale_w = nullptr;
+  a.roles = (int)roles; a.finalize = finalize ? 1 : 0;
   if (w2f8.has_value()) {
     TORCH_CHECK(amax_w.has_value() && scale_w.has_value(), "fp8 shadow needs amax_w and scale_w");
     check(*w2f8, "w2f8", at::kByte, {64, 1600});
@@ -346,7 +348,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
 
 TORCH_LIBRARY(dmlc, m) {
   m.def("conv1_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
-        "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? amax) -> ()");
+        "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? amax=None) -> ()");
   m.def("conv2_fwd_fp8(Tensor inp, Tensor w8, Tensor b2, Tensor amax_x, Tensor scale_w, Tensor? counter, "
         "Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("fp8_roundtrip(Tensor x, Tensor(a!) y, float scale) -> ()");
@@ -364,7 +366,8 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
-        "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w) -> ()");
+        "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles=0, "
+        "bool finalize=True) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

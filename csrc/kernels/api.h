@@ -153,6 +153,11 @@ struct DmlcSgdArgs {
   // (2x headroom over the previous weights' amax), store sw to scale_w[(step+1)&1] and the new amax
   // to amax_w[(step+1)&1]; the last arriver zeroes amax_w[step&1].  Mode 3 uses/stores slot step&1.
   uint8_t* w2f8; float* amax_w; float* scale_w;
+  // block roles launched: 0 all, 1 conv rows + conv biases only, 2 fc only (data-parallel split of
+  // the apply around the bucketed all-reduce); only launches with finalize = 1 bump global_step /
+  // publish stats (their last arriver).
+  int roles;
+  int finalize;
 };
 
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);

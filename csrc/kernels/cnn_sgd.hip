@@ -191,14 +191,14 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
   DMLC_STAMP(DMLC_TK_SGD, 0);
   const int64_t step = *a.step;
   const float lr = lr_of(a, step);
-  int blk = blockIdx.x;
+  int blk = blockIdx.x + (a.roles == 2 ? C2_BLOCKS + C1_BLOCKS + 2 : 0);
   if (blk < C2_BLOCKS) conv2_rows(a, blk, lr, lds);
   else if ((blk -= C2_BLOCKS) < C1_BLOCKS) conv1_rows(a, blk, lr, lds);
   else if ((blk -= C1_BLOCKS) < 2) conv_bias(a, blk, lr, lds);
   else fc_block(a, blk - 2, lr);
   DMLC_STAMP(DMLC_TK_SGD, 1);
 
-  if (!(a.mode == 0 || a.mode == 2)) return;
+  if (!(a.mode == 0 || a.mode == 2) || !a.finalize) return;
   // last arriver: bump global_step, publish stats, re-arm the ticket for the next launch (the engine
   // zeroes it once at creation; every launch that starts also completes, so it stays consistent).
   // Nothing is published THROUGH the ticket (loss/accuracy partials come from an earlier launch and
@@ -234,7 +234,11 @@ using namespace dmlc;
 extern "C" hipError_t dmlc_sgd(DmlcSgdArgs* a, hipStream_t s) {
   const int fc4 = ((a->off[9] + 10 + 3) >> 2) - (a->off[4] >> 2);
   const int fc_blocks = (fc4 + 256 * FC_F4_PER_THREAD - 1) / (256 * FC_F4_PER_THREAD);
-  const int blocks = C2_BLOCKS + C1_BLOCKS + 2 + (a->mode == 1 ? 0 : fc_blocks);
+  const int conv_blocks = C2_BLOCKS + C1_BLOCKS + 2;
+  int blocks = conv_blocks + (a->mode == 1 ? 0 : fc_blocks);
+  if (a->roles == 1) blocks = conv_blocks;
+  if (a->roles == 2) blocks = a->mode == 1 ? 0 : fc_blocks;
+  if (blocks == 0) return hipSuccess;
   a->nblocks = blocks;
   hipLaunchKernelGGL(k_sgd, dim3(blocks), dim3(256), 0, s, *a);
   return hipGetLastError();

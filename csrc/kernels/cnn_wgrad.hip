@@ -28,14 +28,16 @@ constexpr int W1_PL = 28 * 24 + 8;            // shifted-plane stride (bf16): 13
 constexpr int W1_DYT = 576 * W1_DY_LD;        // bf16 elements
 constexpr int W1_XS = 16 * W1_PL;
 constexpr int W1_RAW = 28 * 32 * 4;           // bf16 [28][32][4] padded crop (col c <-> ix = c-2)
-constexpr size_t W1_LDS = (size_t)(W1_DYT + W1_XS + 9216 + W1_RAW) * 2 + 9216 + 4 * 64 * 4;
+constexpr int W1T = 512;                      // 8 waves (2 per SIMD) for the VALU-heavy gather phases
+constexpr size_t W1_LDS = (size_t)(W1_DYT + W1_XS + 9216 + W1_RAW) * 2 + 9216 + (W1T / 64) * 64 * 4;
 
 struct Conv1Input {                            // prefetch of the 28x32 zero-padded crop, 3 bytes/pixel
-  uint32_t v[4];
+  static constexpr int IT = (896 + W1T - 1) / W1T;
+  uint32_t v[IT];
   MDEV void load(const uint8_t* img, int cy, int cx, int tid) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = tid + i * 256;
+    for (int i = 0; i < IT; ++i) {
+      const int p = tid + i * W1T;
       const int r = p >> 5, c = p & 31, iy = r - 2, ix = c - 2;
       const bool ok = p < 896 && iy >= 0 && iy < 24 && ix >= 0 && ix < 24;
       const uint8_t* s = img + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);   // branch-free loads
@@ -45,8 +47,8 @@ struct Conv1Input {                            // prefetch of the 28x32 zero-pad
   }
   MDEV void store(bf16* raw, int tid) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = tid + i * 256;
+    for (int i = 0; i < IT; ++i) {
+      const int p = tid + i * W1T;
       if (p < 896)
         *reinterpret_cast<bf16x4*>(raw + p * 4) =
             pack4((float)(v[i] & 0xff), (float)((v[i] >> 8) & 0xff), (float)((v[i] >> 16) & 0xff), 0.f);
@@ -54,7 +56,7 @@ struct Conv1Input {                            // prefetch of the 28x32 zero-pad
   }
 };
 
-__global__ __launch_bounds__(256, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
+__global__ __launch_bounds__(W1T, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* dyt = reinterpret_cast<bf16*>(smem);
   bf16* xs = dyt + W1_DYT;
@@ -64,22 +66,22 @@ __global__ __launch_bounds__(256, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
   float* red = reinterpret_cast<float*>(ams + 9216);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int grp = blockIdx.x;
+  const int grp = blockIdx.x, ch = w & 1, ks = w >> 1;   // MFMA: co tiles 2ch, 2ch+1; k-steps ks mod 4
   const int b0 = grp * a.B / a.g1, b1 = (grp + 1) * a.B / a.g1;
   DMLC_STAMP(DMLC_TK_W1, 0);
 
-  for (int e = tid; e < W1_PL / 8; e += 256) *reinterpret_cast<bf16x8*>(xs + 15 * W1_PL + e * 8) = bf16x8{};
+  for (int e = tid; e < W1_PL / 8; e += W1T) *reinterpret_cast<bf16x8*>(xs + 15 * W1_PL + e * 8) = bf16x8{};
 
-  f32x4 acc[4][5];
+  f32x4 acc[2][5];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int t = 0; t < 5; ++t) acc[ct][t] = zero4();
+    for (int t = 0; t < 5; ++t) acc[h][t] = zero4();
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
   Conv1Input pin;
-  Prefetch16<1152> pdp;
-  Prefetch16<576> pam;
+  Prefetch16<1152, W1T> pdp;
+  Prefetch16<576, W1T> pam;
   if (b0 < b1) {
     pin.load(a.data + (size_t)batch_index(a.src, a.B, b0) * 3072, a.cy, a.cx, tid);
     pdp.load(reinterpret_cast<const bf16*>(a.dp1) + (size_t)b0 * 9216, tid);
@@ -98,7 +100,7 @@ __global__ __launch_bounds__(256, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
     __syncthreads();
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 1);
     // (a) shifted channel planes: task (yy, x8, kw) -> planes kw*3+{0,1,2}, 8 pixels
-    for (int task = tid; task < 28 * 3 * 5; task += 256) {
+    for (int task = tid; task < 28 * 3 * 5; task += W1T) {
       const int kw = task % 5, r = task / 5, x8 = r % 3, yy = r / 3;
       const bf16* src = raw + (yy * 32 + x8 * 8 + kw) * 4;
       bf16x8 o0, o1, o2;
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(256, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
       *reinterpret_cast<bf16x8*>(dst + 2 * W1_PL) = o2;
     }
     // (b) pool1 / ReLU backward -> dY1 (bf16, LDS) + bias-grad sums (fp32)
-    for (int task = tid; task < 144 * 8; task += 256) {
+    for (int task = tid; task < 144 * 8; task += W1T) {
       const int win = task >> 3, c = task & 7, py = win / 12, px = win - py * 12;
       float o[4][8];
       pool_bwd_2x2<12>(dps, ams, py, px, c, o);
@@ -127,19 +129,21 @@ __global__ __launch_bounds__(256, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
     }
     __syncthreads();
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 2);
-    // (c) MFMA: this wave's k-steps s = w, w+4, ... of the 18 (32 pixels each)
-    for (int s = w; s < 18; s += 4) {
+    // (c) MFMA: this wave's k-steps s = ks, ks+4, ... of the 18 (32 pixels each), co tiles 2ch, 2ch+1
+    for (int s = ks; s < 18; s += 4) {
       const int rA = 32 * s + 8 * g + q, rB = rA + 4;
-      bf16x8 af[4];
+      bf16x8 af[2];
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-        af[ct] = tr_frag(dyt + rA * W1_DY_LD + 16 * ct + 4 * p, dyt + rB * W1_DY_LD + 16 * ct + 4 * p);
+      for (int h = 0; h < 2; ++h) {
+        const int ct = 2 * ch + h;
+        af[h] = tr_frag(dyt + rA * W1_DY_LD + 16 * ct + 4 * p, dyt + rB * W1_DY_LD + 16 * ct + 4 * p);
+      }
       const int r0 = 32 * s + 8 * g, y = r0 / 24, x0 = r0 - y * 24;
 #pragma unroll
       for (int t = 0; t < 5; ++t) {
         const bf16x8 bx = lds_b128(xs + li * W1_PL + (y + t) * 24 + x0);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mfma16(af[ct], bx, acc[ct][t]);
+        for (int h = 0; h < 2; ++h) acc[h][t] = mfma16(af[h], bx, acc[h][t]);
       }
     }
   }
@@ -148,19 +152,24 @@ __global__ __launch_bounds__(256, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
   DMLC_STAMP(DMLC_TK_W1, 3);
   f32x4* fl = reinterpret_cast<f32x4*>(smem);
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int t = 0; t < 5; ++t) fl[(w * 20 + ct * 5 + t) * 64 + lane] = acc[ct][t];
+    for (int t = 0; t < 5; ++t) fl[(ks * 20 + (2 * ch + h) * 5 + t) * 64 + lane] = acc[h][t];
   block_chunk_sum(bsum, red, tid);
   __syncthreads();
   float* out = a.part1 + (size_t)grp * 80 * 64;
-  for (int e = tid; e < 20 * 64; e += 256) {
+  for (int e = tid; e < 20 * 64; e += W1T) {
     const f32x4 s = ((fl[e] + fl[1280 + e]) + (fl[2560 + e] + fl[3840 + e]));
     const int tile = e >> 6, ln = e & 63, ct = tile / 5, t = tile - ct * 5;
     const int co = 16 * ct + 4 * (ln >> 4), kk = 16 * t + (ln & 15);
     *reinterpret_cast<f32x4*>(out + kk * 64 + co) = s;
   }
-  if (tid < 64) a.partb1[grp * 64 + tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+  if (tid < 64) {
+    float sb = 0.f;
+#pragma unroll
+    for (int k = 0; k < W1T / 64; ++k) sb += red[k * 64 + tid];
+    a.partb1[grp * 64 + tid] = sb;
+  }
   DMLC_STAMP(DMLC_TK_W1, 4);
 }
 
@@ -284,7 +293,7 @@ hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)W1_LDS);
     g_w1 = true;
   }
-  hipLaunchKernelGGL(k_conv1_wgrad, dim3(a->g1), dim3(256), W1_LDS, s, *a);
+  hipLaunchKernelGGL(k_conv1_wgrad, dim3(a->g1), dim3(W1T), W1_LDS, s, *a);
   return hipGetLastError();
 }
 

@@ -33,21 +33,21 @@ DEV void stage16(void* dst, const void* src, int tid) {
 
 // Register prefetch of N 16-byte chunks (thread's share), split in two halves so a kernel can issue
 // the loads of the NEXT item before computing the current one.
-template <int N>
+template <int N, int T = 256>
 struct Prefetch16 {
-  static constexpr int IT = (N + 255) / 256;
+  static constexpr int IT = (N + T - 1) / T;
   uint4 v[IT];
   MDEV void load(const void* src, int tid) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int c = tid + i * 256;
+      const int c = tid + i * T;
       v[i] = load_sel(reinterpret_cast<const uint4*>(src) + c, reinterpret_cast<const uint4*>(src), c < N);
     }
   }
   MDEV void store(void* dst, int tid) const {
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int c = tid + i * 256;
+      const int c = tid + i * T;
       if (c < N) reinterpret_cast<uint4*>(dst)[c] = v[i];
     }
   }
@@ -108,8 +108,8 @@ DEV bf16x8 to_bf16x8(const float (&v)[8]) {
   return o;
 }
 
-// Reduce per-thread channel sums (thread's chunk = tid & 7) over the workgroup: red[4][64] partials.
-DEV void block_chunk_sum(float (&v)[8], float* red /*[4][64]*/, int tid) {
+// Reduce per-thread channel sums (thread's chunk = tid & 7) over the workgroup: red[waves][64] partials.
+DEV void block_chunk_sum(float (&v)[8], float* red /*[waves][64]*/, int tid) {
   const int lane = tid & 63, w = tid >> 6;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {

@@ -109,7 +109,8 @@ class FusedCifarEngine:
         # --- activations / workspaces -------------------------------------------------------
         self.fc1_split = fc1_split or self._pick_fc1_split(B)
         self.g1 = g1 or max(1, min(B, B // 2))          # conv1 wgrad: 2 images per block
-        self.g2 = g2 or max(1, min(B, B // 5))          # conv2 wgrad: 5 kh blocks x ~5 images
+        self.g2 = g2 or max(1, min(B, B // 6))          # conv2 wgrad: 5 kh blocks x 6 images (runs
+        #   beside conv1 wgrad, which is the longer branch; fewer groups = fewer slab bytes to reduce)
         self.p1, self.am1 = z(B, 12, 12, 64), z(B, 12, 12, 64, dt=torch.uint8)
         self.p2, self.am2 = z(B, 6, 6, 64), z(B, 6, 6, 64, dt=torch.uint8)
         self.h1part = z(self.fc1_split, B, 384, dt=torch.float32)
@@ -221,12 +222,13 @@ class FusedCifarEngine:
                       self.part1, self.partb1)
         main.wait_stream(self.side_stream)
 
-    def _sgd(self, mode: int, scale: float = 1.0):
+    def _sgd(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True):
         self.ops.sgd(self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.partb2,
                      self.w1f, self.w2f, self.w2d, self.fc1n, self.fc2t, self.fc2n, self.fc3t, self.fc3d,
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                      self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
-                                                                      if self.fp8 else (None, None, None)))
+                                                                      if self.fp8 else (None, None, None)),
+                     roles, finalize)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -249,6 +251,14 @@ class FusedCifarEngine:
     def _seg_apply(self):
         self._sgd(mode=2, scale=1.0)
 
+    def _seg_apply_fc(self):
+        # fc parameters: SGD from the all-reduced fc bucket; runs on the comm stream while the conv
+        # backward still runs on the main stream (it touches no conv weights / conv gradients)
+        self._sgd(mode=2, scale=1.0, roles=2, finalize=False)
+
+    def _seg_apply_conv(self):
+        self._sgd(mode=2, scale=1.0, roles=1, finalize=True)
+
     def compute_gradients(self):
         """Forward + backward only (no update); the full gradient lands in ``self.grad``."""
         self._maybe_new_epoch()
@@ -262,23 +272,29 @@ class FusedCifarEngine:
             self._seg_compute_a()
             self._seg_compute_b()
             return
+        self._dp_step([self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv])
+
+    def _dp_step(self, seg):
+        """Data-parallel step around two all-reduce buckets:
+            main: A = fwd + head + fc backward | B = conv backward + conv-grad reduction
+            comm:        wait A -> all-reduce fc grads -> apply fc  | wait B -> all-reduce conv grads -> apply conv
+        The fc bucket (90 % of the bytes) and the fc SGD overlap the conv backward."""
         main = torch.cuda.current_stream(self.device)
-        fc = self.grad[M.FC_BUCKET_OFFSET:]
-        conv = self.grad[:M.FC_BUCKET_OFFSET]
-        self._seg_compute_a()
+        seg[0]()
         ev = torch.cuda.Event()
         ev.record(main)
         self.comm_stream.wait_event(ev)
         with torch.cuda.stream(self.comm_stream):
-            self._allreduce(fc)
-        self._seg_compute_b()
+            self._allreduce(self.grad[M.FC_BUCKET_OFFSET:])
+            seg[2]()
+        seg[1]()
         ev2 = torch.cuda.Event()
         ev2.record(main)
         self.comm_stream.wait_event(ev2)
         with torch.cuda.stream(self.comm_stream):
-            self._allreduce(conv)
+            self._allreduce(self.grad[:M.FC_BUCKET_OFFSET])
+            seg[3]()
         main.wait_stream(self.comm_stream)
-        self._seg_apply()
 
     # --- graph capture --------------------------------------------------------------------------
     def capture(self):
@@ -292,7 +308,7 @@ class FusedCifarEngine:
         elif self.capture_comm:
             segs = [self._eager_step]
         else:
-            segs = [self._seg_compute_a, self._seg_compute_b, self._seg_apply]
+            segs = [self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv]
         # state (step counter, master weights) must be identical before and after capture: a
         # capture records launches without running them, so nothing changes here.
         for fn in segs:
@@ -314,21 +330,7 @@ class FusedCifarEngine:
         elif len(self.graphs) == 1:
             self.graphs[0].replay()
         else:
-            main = torch.cuda.current_stream(self.device)
-            self.graphs[0].replay()
-            ev = torch.cuda.Event()
-            ev.record(main)
-            self.comm_stream.wait_event(ev)
-            with torch.cuda.stream(self.comm_stream):
-                self._allreduce(self.grad[M.FC_BUCKET_OFFSET:])
-            self.graphs[1].replay()
-            ev2 = torch.cuda.Event()
-            ev2.record(main)
-            self.comm_stream.wait_event(ev2)
-            with torch.cuda.stream(self.comm_stream):
-                self._allreduce(self.grad[:M.FC_BUCKET_OFFSET])
-            main.wait_stream(self.comm_stream)
-            self.graphs[2].replay()
+            self._dp_step([g.replay for g in self.graphs])
         self.host_step += 1
 
     # --- evaluation -----------------------------------------------------------------------------

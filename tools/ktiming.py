@@ -72,6 +72,17 @@ def main():
             d = (v[ok] - ent[ok]) / 100.0
             slots[sl] = [round(float(np.median(d)), 2), round(float(d.max()), 2)]
         rec["slot_med_max_us"] = slots
+        if NAMES[k] == "sgd":      # per block-role breakdown (see cnn_sgd.hip block ranges)
+            roles = {"conv2_rows": (0, 400), "conv1_rows": (400, 475), "conv_bias": (475, 477),
+                     "fc": (477, NB)}
+            raw = t[k]
+            for name, (lo, hi) in roles.items():
+                sub = raw[lo:hi]
+                sub = sub[sub[:, 0] > 0]
+                if len(sub):
+                    d = (sub[:, 1] - sub[:, 0]) / 100.0
+                    rec[f"role_{name}_work_us_med_max"] = [round(float(np.median(d)), 2), round(float(d.max()), 2)]
+                    rec[f"role_{name}_start_us_max"] = round(float((sub[:, 0].max() - ent.min()) / 100.0), 2)
         out[NAMES[k]] = rec
     print(json.dumps(out, indent=1))
 
