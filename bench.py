@@ -59,6 +59,11 @@ def make_data(n, device, seed=0):
 
 
 def build_fused(args, info, data, labels):
+    if args.model == "resnet20":
+        from dmlc.engine.fused_resnet import FusedResNetEngine
+        eng = FusedResNetEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
+                                rank=info.rank, seed=0, lr=0.01, comm_dtype=args.comm_dtype)
+        return eng, eng.step, (None if args.no_graph else eng.capture)
     from dmlc.engine.fused import FusedCifarEngine
     eng = FusedCifarEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
                            rank=info.rank, seed=0, comm_dtype=args.comm_dtype, dtype=args.dtype)
@@ -80,11 +85,13 @@ def main():
     if info.world_size != args.gpus and info.rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
     if args.impl == "auto":
-        args.impl = "fused" if args.model == "cifar_cnn" else "eager"
+        args.impl = "fused" if args.model == "cifar_cnn" or args.dtype == "bf16" else "eager"
     if args.crop is None:
         args.crop = 24 if args.model == "cifar_cnn" else 32
-    if args.impl == "fused" and (args.model != "cifar_cnn" or args.crop != 24):
-        raise SystemExit("the fused HIP engine implements the reference CNN at the 24x24 crop")
+    if args.impl == "fused" and args.model == "cifar_cnn" and args.crop != 24:
+        raise SystemExit("the fused HIP CNN engine implements the reference CNN at the 24x24 crop")
+    if args.impl == "fused" and args.model == "resnet20" and (args.crop != 32 or args.dtype != "bf16"):
+        raise SystemExit("the fused HIP ResNet-20 engine takes full 32x32 images in bf16")
     data, labels = make_data(args.dataset_size, info.device)
     builder = build_fused if args.impl == "fused" else build_eager
     eng, step, capture = builder(args, info, data, labels)

@@ -1,0 +1,94 @@
+// Host-side launch API of the fused ResNet-20 kernels (csrc/kernels/resnet.hip).
+//
+// Conventions: activations NHWC bf16; per-layer BatchNorm statistics are fp64 accumulators
+// (atomicAdd of per-block fp32 partials; zeroed once per step); conv weights have two bf16 shadows:
+//   fwd   w [COUT][KP]  k  = tap*CINP + ci        (tap = kh*3 + kw, CINP = max(CIN, 8), KP = 9*CINP -> x32)
+//   dgrad wd [CIN][KPD] k' = tap'*COUT + co       (tap' = 8 - tap: rotated 180 degrees, KPD = 9*COUT -> x32)
+// Layer l computes z_l = conv_l(x_l) with x_l = a_{l-1}, a = relu(bn(z) [+ shortcut]).
+#pragma once
+#include "api.h"
+
+extern "C" {
+
+struct DmlcRnLayerGeom {    // runtime copy of the compile-time geometry (validated by the binding)
+  int cin, cout, hin, stride;
+};
+
+struct DmlcRnFwdArgs {
+  // input of this conv: the dataset (stem) or the BN-apply of the previous layer
+  const uint8_t* data; DmlcIndexSrc src; int cy, cx;      // stem only
+  const void* z_prev;        // bf16 [B][Hin][Hin][CIN]  pre-BN output of layer l-1
+  const double* stat_prev;   // [2][CIN] sum z, sum z^2 of layer l-1
+  const float* gamma_prev; const float* beta_prev;
+  const void* sc_src;        // nullable: block input feeding the residual of layer l-1 (bf16)
+  int sc_mode;               // 0 none, 1 identity [B][Hin][Hin][CIN], 2 subsample+zero-pad [B][2Hin][2Hin][CIN/2]
+  void* a_out;               // bf16 [B][Hin][Hin][CIN]  materialised a_{l-1} (backward needs it)
+  float inv_n_prev;          // 1 / (B * Hin * Hin)
+  const void* w;             // bf16 [COUT][KP]
+  void* z;                   // bf16 [B][Hout][Hout][COUT]
+  double* stat;              // [2][COUT] accumulators of layer l
+  int B;
+};
+
+struct DmlcRnDgradArgs {
+  // BN backward of layer l (prologue): g_z = gamma*rstd*(g_y - R1/N - xhat*R2/N)
+  const void* gy; const void* z; const double* stat; const double* red; const float* gamma; float inv_n;
+  const void* wd;            // bf16 [CIN][KPD]
+  // epilogue: g_a_{l-1} (+ shortcut) -> g_y_{l-1} = g_a * (a_{l-1} > 0), reductions of layer l-1
+  const void* a_prev; const void* z_prev; const double* stat_prev; float inv_n_prev;
+  const void* gy_sc;         // nullable: g_y of the block's second conv (shortcut gradient)
+  int sc_mode;               // 1 identity, 2 subsample (gy_sc is [B][Hin/2][Hin/2][2*CIN])
+  void* gy_prev;             // bf16 [B][Hin][Hin][CIN]
+  double* red_prev;          // [2][CIN]
+  int B;
+};
+
+struct DmlcRnWgradArgs {
+  const uint8_t* data; DmlcIndexSrc src; int cy, cx;      // stem input
+  const void* x;             // bf16 a_{l-1} [B][Hin][Hin][CIN] (l >= 1)
+  const void* gy; const void* z; const double* stat; const double* red; const float* gamma; float inv_n;
+  float* part;               // [G][KP][COUT] fp32 split-K slabs
+  int G, B;
+};
+
+struct DmlcRnHeadArgs {
+  const void* z; const double* stat; const float* gamma; const float* beta; float inv_n;   // layer 18
+  const void* sc;            // identity shortcut (block input) bf16 [B][8][8][64]
+  const float* fcw; const float* fcb;   // fp32 master views [64][10], [10]
+  const int* labels; DmlcIndexSrc src; float inv_batch;
+  void* gy;                  // bf16 [B][8][8][64] g_y_18
+  double* red;               // [2][64] reductions of layer 18
+  float* fc_part;            // [B][656] per-image dW_fc (640) + db_fc (10) + pad
+  float* loss_img; int* correct_img;    // [B]
+  float* logits_out;         // nullable [B][10]
+  int B;
+};
+
+#define DMLC_RN_LAYERS 19
+struct DmlcRnSgdArgs {
+  float* master; int nparams;
+  float* grad; float grad_scale;   // DP: modes 1 (write) / 2 (read, scaled)
+  // per conv layer
+  int conv_off[DMLC_RN_LAYERS], gamma_off[DMLC_RN_LAYERS], beta_off[DMLC_RN_LAYERS];
+  int cin[DMLC_RN_LAYERS], cout[DMLC_RN_LAYERS];
+  const float* part[DMLC_RN_LAYERS]; int G[DMLC_RN_LAYERS];
+  void* wf[DMLC_RN_LAYERS]; void* wd[DMLC_RN_LAYERS];
+  const double* stat; const double* red;   // [19][2][64] each
+  float* state; int mm_off[DMLC_RN_LAYERS], mv_off[DMLC_RN_LAYERS];   // BN moving statistics
+  float bn_momentum; float inv_n[DMLC_RN_LAYERS];
+  int fcw_off, fcb_off; const float* fc_part; int B;
+  int blk_start[DMLC_RN_LAYERS + 2];   // block ranges (set by the launcher): conv layers, fc, BN
+  int mode;                  // 0 reduce+apply, 1 reduce->grad, 2 apply grad, 3 shadows only
+  int64_t* step; float lr0, decay, decay_steps; int staircase;
+  unsigned int* ticket;
+  const float* loss_img; const int* correct_img;
+  float* stats; int stats_len;
+};
+
+hipError_t dmlc_rn_fwd(const DmlcRnLayerGeom* g, const DmlcRnFwdArgs* a, hipStream_t s);
+hipError_t dmlc_rn_dgrad(const DmlcRnLayerGeom* g, const DmlcRnDgradArgs* a, hipStream_t s);
+hipError_t dmlc_rn_wgrad(const DmlcRnLayerGeom* g, const DmlcRnWgradArgs* a, hipStream_t s);
+hipError_t dmlc_rn_head(const DmlcRnHeadArgs* a, hipStream_t s);
+hipError_t dmlc_rn_sgd(DmlcRnSgdArgs* a, hipStream_t s);
+
+}  // extern "C"

@@ -1,0 +1,839 @@
+// Fused ResNet-20 training kernels for gfx950 (BASELINE.json config 4; SURVEY.md §2.C "Extra
+// kernels not in the reference": conv3x3 fwd/dgrad/wgrad with stride 1/2, train-mode batch-norm,
+// residual add, global average pool).  Model: models/resnet.py (the eager oracle).
+//
+// Design (MI355X-first):
+//   * every 3x3 conv is an implicit GEMM on MFMA 16x16x32 bf16 over an LDS image of ONE zero-padded
+//     input (one image per 256-thread block for fwd/dgrad), no im2col buffer; the K order is
+//     (tap, channel) so each 8-wide B fragment is one 16-byte LDS read (CIN padded to 8 for the stem);
+//   * train-mode BatchNorm never gets its own kernel: a layer's forward kernel writes z and adds
+//     per-block channel sums / sums of squares into fp64 accumulators; the NEXT conv applies
+//     scale/shift + ReLU (+ the option-A residual) while staging its input (and materialises a for
+//     the backward); the backward mirrors it: each dgrad's epilogue produces g_y of the layer below
+//     plus its two BN reductions (sum g_y, sum g_y*xhat), and the consumer rebuilds
+//     g_z = gamma*rstd*(g_y - R1/N - xhat*R2/N) in its prologue;
+//   * stride-2 dgrad is a stride-1 correlation over a zero-inserted LDS image (pad 2/0);
+//   * weight gradients: split-K over image groups x m-chunks, both operands read with
+//     ds_read_b64_tr_b16 from NHWC LDS images (per-lane row addresses absorb stride and taps);
+//   * the SGD kernel reduces the slabs in fixed order, updates BN running statistics, refreshes
+//     both bf16 weight shadows and bumps the device step counter (graph-capturable).
+#include "conv_common.h"
+#include "api_resnet.h"
+
+namespace dmlc {
+namespace rn {
+
+constexpr int RT = 256;
+constexpr double BN_EPS = 1e-3;
+
+__host__ __device__ constexpr int round32(int x) { return (x + 31) / 32 * 32; }
+
+// per-channel BN coefficients from fp64 sums (stat: [0..63] sum, [64..127] sum of squares)
+DEV void bn_stats(const double* stat, int c, float inv_n, float& mean, float& rstd) {
+  const double m = stat[c] * (double)inv_n;
+  double var = stat[64 + c] * (double)inv_n - m * m;
+  var = var > 0.0 ? var : 0.0;
+  mean = (float)m;
+  rstd = (float)(1.0 / sqrt(var + BN_EPS));
+}
+
+DEV float bfv(uint32_t w, int hi) { return hi ? bf16_hi(w) : bf16_lo(w); }
+DEV uint32_t pack2(float a, float b) {
+  const bf16x4 v = pack4(a, b, 0.f, 0.f);
+  uint2 u = __builtin_bit_cast(uint2, v);
+  return u.x;
+}
+
+// fp64 atomic accumulation of 2 x 64 per-block channel partials staged in LDS red[2][64]
+DEV void flush_stats(double* dst, const float* red, int C, int tid) {
+  if (tid < C) {
+    atomicAdd(dst + tid, (double)red[tid]);
+    atomicAdd(dst + 64 + tid, (double)red[64 + tid]);
+  }
+}
+
+// ================================ forward ======================================================
+template <int CIN, int COUT, int HIN, int S>
+struct Fwd {
+  static constexpr int CINP = CIN < 8 ? 8 : CIN;
+  static constexpr int HOUT = HIN / S;
+  static constexpr int PADB = S == 1 ? 1 : 0;
+  static constexpr int HP = HIN + (S == 1 ? 2 : 1);
+  static constexpr int KP = round32(9 * CINP), KS = KP / 32;
+  static constexpr int CT = COUT / 16, WPC = 4 / CT, NPXT = HOUT * HOUT / 16, NPT = NPXT / WPC;
+  static constexpr int NCH = HP * HP * CINP / 8;               // 16-B chunks of the padded image
+  static constexpr int IT = (NCH + RT - 1) / RT;
+  static constexpr size_t LDS = (size_t)HP * HP * CINP * 2 + 4 * 2 * 64 * 4;
+};
+
+template <int CIN, int COUT, int HIN, int S>
+__global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
+  using F = Fwd<CIN, COUT, HIN, S>;
+  constexpr int CINP = F::CINP, HP = F::HP, HOUT = F::HOUT, KP = F::KP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* xs = reinterpret_cast<bf16*>(smem);
+  float* red = reinterpret_cast<float*>(xs + HP * HP * CINP);    // [4][2][64]
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+
+  // ---- prologue: padded input image (stem: dataset gather; else BN-apply of layer l-1) ----
+  if constexpr (CIN == 3) {
+    const uint8_t* img = a.data + (size_t)batch_index(a.src, a.B, b) * 3072;
+    uint32_t px3[F::IT];
+#pragma unroll
+    for (int i = 0; i < F::IT; ++i) {
+      const int e = min(tid + i * RT, F::NCH - 1);
+      const int iy = e / HP - F::PADB, ix = e % HP - F::PADB;
+      const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
+      const uint8_t* s = img + (ok ? ((a.cy + iy) * 32 + a.cx + ix) * 3 : 0);
+      const uint32_t v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
+      px3[i] = ok ? v : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < F::IT; ++i) {
+      const int e = tid + i * RT;
+      if (e < F::NCH) {
+        const uint32_t v = px3[i];
+        uint4 o;
+        o.x = pack2((float)(v & 0xff), (float)((v >> 8) & 0xff));
+        o.y = pack2((float)((v >> 16) & 0xff), 0.f);
+        o.z = 0; o.w = 0;
+        reinterpret_cast<uint4*>(xs)[e] = o;
+      }
+    }
+  } else {
+    constexpr int C8 = CIN / 8;
+    const int c8 = tid % C8;                  // fixed channel chunk of this thread (RT % C8 == 0)
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float mean, rstd;
+      const int c = c8 * 8 + j;
+      bn_stats(a.stat_prev, c, a.inv_n_prev, mean, rstd);
+      sc[j] = a.gamma_prev[c] * rstd;
+      sh[j] = a.beta_prev[c] - mean * sc[j];
+    }
+    const uint4* zp = reinterpret_cast<const uint4*>(a.z_prev) + (size_t)b * HIN * HIN * C8;
+    const uint4* ss = reinterpret_cast<const uint4*>(a.sc_src);
+    uint4 zv[F::IT], sv[F::IT];
+#pragma unroll
+    for (int i = 0; i < F::IT; ++i) {
+      const int e = min(tid + i * RT, F::NCH - 1);
+      const int pp = e / C8, iy = pp / HP - F::PADB, ix = pp % HP - F::PADB;
+      const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
+      const int pin = ok ? iy * HIN + ix : 0;
+      zv[i] = zp[pin * C8 + c8];
+      sv[i] = make_uint4(0, 0, 0, 0);
+      if (a.sc_mode == 1) sv[i] = ss[((size_t)b * HIN * HIN + pin) * C8 + c8];
+      else if (a.sc_mode == 2) {               // option A: x[2y][2x][c] for c < CIN/2, zero above
+        const bool lowc = c8 < C8 / 2;
+        const size_t q = ((size_t)b * 4 * HIN * HIN + (ok ? (2 * iy) * (2 * HIN) + 2 * ix : 0)) * (C8 / 2) + (lowc ? c8 : 0);
+        const uint4 v = ss[q];
+        sv[i] = lowc ? v : make_uint4(0, 0, 0, 0);
+      }
+    }
+    uint4* ao = reinterpret_cast<uint4*>(a.a_out) + (size_t)b * HIN * HIN * C8;
+#pragma unroll
+    for (int i = 0; i < F::IT; ++i) {
+      const int e = tid + i * RT;
+      if (e < F::NCH) {
+        const int pp = e / C8, iy = pp / HP - F::PADB, ix = pp % HP - F::PADB;
+        const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
+        const uint32_t zw[4] = {zv[i].x, zv[i].y, zv[i].z, zv[i].w};
+        const uint32_t sw[4] = {sv[i].x, sv[i].y, sv[i].z, sv[i].w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float y0 = fmaxf(bf16_lo(zw[k]) * sc[2 * k] + sh[2 * k] + bf16_lo(sw[k]), 0.f);
+          const float y1 = fmaxf(bf16_hi(zw[k]) * sc[2 * k + 1] + sh[2 * k + 1] + bf16_hi(sw[k]), 0.f);
+          ow[k] = ok ? pack2(y0, y1) : 0u;
+        }
+        const uint4 o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        reinterpret_cast<uint4*>(xs)[e] = o;
+        if (ok) ao[(iy * HIN + ix) * C8 + c8] = o;
+      }
+    }
+  }
+  // weight fragments of this wave's c_out tile
+  const int ct = w % F::CT, pt0 = w / F::CT;
+  const bf16* W = reinterpret_cast<const bf16*>(a.w) + (16 * ct + li) * KP + 8 * g;
+  bf16x8 wa[F::KS];
+#pragma unroll
+  for (int ks = 0; ks < F::KS; ++ks) wa[ks] = glb_b128(W + 32 * ks);
+  __syncthreads();
+
+  // ---- implicit GEMM: C[co][px] = sum_k W[co][k] X[px][k] ----
+  f32x4 acc[F::NPT];
+#pragma unroll
+  for (int i = 0; i < F::NPT; ++i) acc[i] = zero4();
+#pragma unroll
+  for (int i = 0; i < F::NPT; ++i) {
+    const int px = 16 * (pt0 + F::WPC * i) + li;
+    const int oy = px / HOUT, ox = px - (px / HOUT) * HOUT;
+    const int base = (oy * S) * HP + ox * S;
+#pragma unroll
+    for (int ks = 0; ks < F::KS; ++ks) {
+      const int k0 = 32 * ks + 8 * g;
+      const int tap = min(k0 / CINP, 8), ci0 = k0 % CINP;
+      const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+      const bf16x8 bx = lds_b128(xs + (base + kh * HP + kw) * CINP + ci0);
+      acc[i] = mfma16(wa[ks], bx, acc[i]);
+    }
+  }
+  // ---- epilogue: z (bf16) + BN partial sums ----
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  bf16* zo = reinterpret_cast<bf16*>(a.z) + (size_t)b * HOUT * HOUT * COUT;
+#pragma unroll
+  for (int i = 0; i < F::NPT; ++i) {
+    const int px = 16 * (pt0 + F::WPC * i) + li;
+    *reinterpret_cast<bf16x4*>(zo + px * COUT + 16 * ct + 4 * g) = pack4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[r] += acc[i][r]; s2[r] += acc[i][r] * acc[i][r]; }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) { s1[r] += __shfl_xor(s1[r], o); s2[r] += __shfl_xor(s2[r], o); }
+  if (li == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[(w * 2 + 0) * 64 + 16 * ct + 4 * g + r] = s1[r];
+      red[(w * 2 + 1) * 64 + 16 * ct + 4 * g + r] = s2[r];
+    }
+  }
+  __syncthreads();
+  if (tid < COUT) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww)
+      if (ww % F::CT == tid / 16) { t1 += red[(ww * 2) * 64 + tid]; t2 += red[(ww * 2 + 1) * 64 + tid]; }
+    atomicAdd(a.stat + tid, (double)t1);
+    atomicAdd(a.stat + 64 + tid, (double)t2);
+  }
+}
+
+// ================================ BN backward coefficients ====================================
+// g_z = A*g_y + Bc*z + Cc  with  A = gamma*rstd, Bc = -gamma*rstd^2*R2/N, Cc = -A*R1/N - Bc*mean
+DEV void bnb_coeffs(const double* stat, const double* red, const float* gamma, int c, float inv_n, float& A,
+                    float& Bc, float& Cc) {
+  float mean, rstd;
+  bn_stats(stat, c, inv_n, mean, rstd);
+  const float r1 = (float)(red[c] * (double)inv_n), r2 = (float)(red[64 + c] * (double)inv_n);
+  A = gamma[c] * rstd;
+  Bc = -A * rstd * r2;
+  Cc = -A * r1 - Bc * mean;
+}
+
+// ================================ dgrad ========================================================
+template <int CIN, int COUT, int HIN, int S>
+struct Dg {
+  static constexpr int HOUT = HIN / S;
+  static constexpr int HPD = HIN + 2;
+  static constexpr int KPD = round32(9 * COUT), KS = KPD / 32;
+  static constexpr int CT = CIN / 16, WPC = 4 / CT, NPXT = HIN * HIN / 16, NPT = NPXT / WPC;
+  static constexpr int NCH = HPD * HPD * COUT / 8;
+  static constexpr int IT = (NCH + RT - 1) / RT;
+  static constexpr size_t LDS = (size_t)HPD * HPD * COUT * 2 + 4 * 2 * 64 * 4;
+};
+
+template <int CIN, int COUT, int HIN, int S>
+__global__ __launch_bounds__(RT) void k_rn_dgrad(DmlcRnDgradArgs a) {
+  using D = Dg<CIN, COUT, HIN, S>;
+  constexpr int HOUT = D::HOUT, HPD = D::HPD, KPD = D::KPD, C8 = COUT / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* gs = reinterpret_cast<bf16*>(smem);
+  float* red = reinterpret_cast<float*>(gs + HPD * HPD * COUT);  // [4][2][64]
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+
+  // ---- prologue: g_z of layer l on the (zero-inserted for S = 2) padded grid ----
+  {
+    const int c8 = tid % C8;
+    float A[8], Bc[8], Cc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bnb_coeffs(a.stat, a.red, a.gamma, c8 * 8 + j, a.inv_n, A[j], Bc[j], Cc[j]);
+    const uint4* gyp = reinterpret_cast<const uint4*>(a.gy) + (size_t)b * HOUT * HOUT * C8;
+    const uint4* zp = reinterpret_cast<const uint4*>(a.z) + (size_t)b * HOUT * HOUT * C8;
+    uint4 gv[D::IT], zv[D::IT];
+    bool okv[D::IT];
+#pragma unroll
+    for (int i = 0; i < D::IT; ++i) {
+      const int e = min(tid + i * RT, D::NCH - 1);
+      const int pp = e / C8, py = pp / HPD, px = pp % HPD;
+      int oy, ox;
+      bool ok;
+      if (S == 1) { oy = py - 1; ox = px - 1; ok = oy >= 0 && oy < HOUT && ox >= 0 && ox < HOUT; }
+      else {
+        oy = (py - 2) >> 1; ox = (px - 2) >> 1;
+        ok = py >= 2 && px >= 2 && !((py - 2) & 1) && !((px - 2) & 1) && oy < HOUT && ox < HOUT;
+      }
+      const int q = (ok ? oy * HOUT + ox : 0) * C8 + c8;
+      gv[i] = gyp[q];
+      zv[i] = zp[q];
+      okv[i] = ok && (tid + i * RT) < D::NCH;
+    }
+#pragma unroll
+    for (int i = 0; i < D::IT; ++i) {
+      const int e = tid + i * RT;
+      if (e < D::NCH) {
+        const uint32_t gw[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w}, zw[4] = {zv[i].x, zv[i].y, zv[i].z, zv[i].w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float v0 = A[2 * k] * bf16_lo(gw[k]) + Bc[2 * k] * bf16_lo(zw[k]) + Cc[2 * k];
+          const float v1 = A[2 * k + 1] * bf16_hi(gw[k]) + Bc[2 * k + 1] * bf16_hi(zw[k]) + Cc[2 * k + 1];
+          ow[k] = okv[i] ? pack2(v0, v1) : 0u;
+        }
+        reinterpret_cast<uint4*>(gs)[e] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      }
+    }
+  }
+  const int ct = w % D::CT, pt0 = w / D::CT;
+  const bf16* Wd = reinterpret_cast<const bf16*>(a.wd) + (16 * ct + li) * KPD + 8 * g;
+  bf16x8 wa[D::KS];
+#pragma unroll
+  for (int ks = 0; ks < D::KS; ++ks) wa[ks] = glb_b128(Wd + 32 * ks);
+  __syncthreads();
+
+  // ---- C[ci][px_in] = sum_{tap', co} Wd[ci][tap'*COUT + co] G[(iy+kh')*HPD + ix + kw'][co] ----
+  f32x4 acc[D::NPT];
+#pragma unroll
+  for (int i = 0; i < D::NPT; ++i) acc[i] = zero4();
+#pragma unroll
+  for (int i = 0; i < D::NPT; ++i) {
+    const int px = 16 * (pt0 + D::WPC * i) + li;
+    const int iy = px / HIN, ix = px - (px / HIN) * HIN;
+    const int base = iy * HPD + ix;
+#pragma unroll
+    for (int ks = 0; ks < D::KS; ++ks) {
+      const int k0 = 32 * ks + 8 * g;
+      const int tap = min(k0 / COUT, 8), co0 = k0 % COUT;
+      const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+      const bf16x8 bx = lds_b128(gs + (base + kh * HPD + kw) * COUT + co0);
+      acc[i] = mfma16(wa[ks], bx, acc[i]);
+    }
+  }
+
+  // ---- epilogue: g_a_{l-1} (+ shortcut) -> g_y_{l-1} + its BN reductions ----
+  constexpr int CI8 = CIN / 8;
+  float mean[4], rstd[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bn_stats(a.stat_prev, 16 * ct + 4 * g + r, a.inv_n_prev, mean[r], rstd[r]);
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  const bf16* ap = reinterpret_cast<const bf16*>(a.a_prev) + (size_t)b * HIN * HIN * CIN;
+  const bf16* zpp = reinterpret_cast<const bf16*>(a.z_prev) + (size_t)b * HIN * HIN * CIN;
+  bf16* gyo = reinterpret_cast<bf16*>(a.gy_prev) + (size_t)b * HIN * HIN * CIN;
+  (void)CI8;
+#pragma unroll
+  for (int i = 0; i < D::NPT; ++i) {
+    const int px = 16 * (pt0 + D::WPC * i) + li;
+    const int iy = px / HIN, ix = px - (px / HIN) * HIN;
+    const int c0 = 16 * ct + 4 * g;
+    const uint2 av = *reinterpret_cast<const uint2*>(ap + px * CIN + c0);
+    const uint2 zv = *reinterpret_cast<const uint2*>(zpp + px * CIN + c0);
+    float sc4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.sc_mode == 1) {
+      const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.gy_sc) +
+                                                     ((size_t)b * HIN * HIN + px) * CIN + c0);
+      sc4[0] = bf16_lo(v.x); sc4[1] = bf16_hi(v.x); sc4[2] = bf16_lo(v.y); sc4[3] = bf16_hi(v.y);
+    } else if (a.sc_mode == 2) {
+      const bool even = !(iy & 1) && !(ix & 1);
+      const int HB = HIN / 2;
+      const size_t q = ((size_t)b * HB * HB + (even ? (iy / 2) * HB + ix / 2 : 0)) * (2 * CIN) + c0;
+      const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.gy_sc) + q);
+      if (even) { sc4[0] = bf16_lo(v.x); sc4[1] = bf16_hi(v.x); sc4[2] = bf16_lo(v.y); sc4[3] = bf16_hi(v.y); }
+    }
+    const float av4[4] = {bf16_lo(av.x), bf16_hi(av.x), bf16_lo(av.y), bf16_hi(av.y)};
+    const float zv4[4] = {bf16_lo(zv.x), bf16_hi(zv.x), bf16_lo(zv.y), bf16_hi(zv.y)};
+    float gy[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      gy[r] = av4[r] > 0.f ? acc[i][r] + sc4[r] : 0.f;
+      s1[r] += gy[r];
+      s2[r] += gy[r] * (zv4[r] - mean[r]) * rstd[r];
+    }
+    *reinterpret_cast<bf16x4*>(gyo + px * CIN + c0) = pack4(gy[0], gy[1], gy[2], gy[3]);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) { s1[r] += __shfl_xor(s1[r], o); s2[r] += __shfl_xor(s2[r], o); }
+  if (li == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[(w * 2 + 0) * 64 + 16 * ct + 4 * g + r] = s1[r];
+      red[(w * 2 + 1) * 64 + 16 * ct + 4 * g + r] = s2[r];
+    }
+  }
+  __syncthreads();
+  if (tid < CIN) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww)
+      if (ww % D::CT == tid / 16) { t1 += red[(ww * 2) * 64 + tid]; t2 += red[(ww * 2 + 1) * 64 + tid]; }
+    atomicAdd(a.red_prev + tid, (double)t1);
+    atomicAdd(a.red_prev + 64 + tid, (double)t2);
+  }
+}
+
+// ================================ wgrad ========================================================
+template <int CIN, int COUT, int HIN, int S>
+struct Wg {
+  static constexpr int CINP = CIN < 8 ? 8 : CIN;
+  static constexpr int HOUT = HIN / S;
+  static constexpr int PADB = S == 1 ? 1 : 0;
+  static constexpr int HP = HIN + (S == 1 ? 2 : 1);
+  static constexpr int KP = round32(9 * CINP);
+  static constexpr int MT = KP / 16, MCH = 16, MC = (MT + MCH - 1) / MCH;
+  static constexpr int NT = COUT / 16;
+  static constexpr int NPIX = HOUT * HOUT, KSTEPS = NPIX / 32;
+  static constexpr int GLD = COUT + 8;                            // g_z LDS row stride (bf16)
+  static constexpr int XCH = HP * HP * CINP / 8, XIT = (XCH + RT - 1) / RT;
+  static constexpr int GCH = NPIX * COUT / 8, GIT = (GCH + RT - 1) / RT;
+  static constexpr size_t LDS = (size_t)HP * HP * CINP * 2 + (size_t)NPIX * GLD * 2;
+};
+
+template <int CIN, int COUT, int HIN, int S>
+__global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
+  using G = Wg<CIN, COUT, HIN, S>;
+  constexpr int CINP = G::CINP, HP = G::HP, HOUT = G::HOUT, KP = G::KP, NT = G::NT, GLD = G::GLD;
+  constexpr int C8 = COUT / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* xs = reinterpret_cast<bf16*>(smem);
+  bf16* gz = xs + HP * HP * CINP;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int grp = blockIdx.x, mc = blockIdx.y;
+  const int b0 = grp * a.B / a.G, b1 = (grp + 1) * a.B / a.G;
+
+  float A[8], Bc[8], Cc[8];
+  const int c8 = tid % C8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bnb_coeffs(a.stat, a.red, a.gamma, c8 * 8 + j, a.inv_n, A[j], Bc[j], Cc[j]);
+
+  f32x4 acc[4][NT];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[j][n] = zero4();
+
+  for (int b = b0; b < b1; ++b) {
+    __syncthreads();
+    // x image (padded)
+    if constexpr (CIN == 3) {
+      const uint8_t* img = a.data + (size_t)batch_index(a.src, a.B, b) * 3072;
+      uint32_t px3[G::XIT];
+#pragma unroll
+      for (int i = 0; i < G::XIT; ++i) {
+        const int e = min(tid + i * RT, G::XCH - 1);
+        const int iy = e / HP - G::PADB, ix = e % HP - G::PADB;
+        const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
+        const uint8_t* s = img + (ok ? ((a.cy + iy) * 32 + a.cx + ix) * 3 : 0);
+        const uint32_t v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
+        px3[i] = ok ? v : 0u;
+      }
+#pragma unroll
+      for (int i = 0; i < G::XIT; ++i) {
+        const int e = tid + i * RT;
+        if (e < G::XCH) {
+          const uint32_t v = px3[i];
+          reinterpret_cast<uint4*>(xs)[e] = make_uint4(pack2((float)(v & 0xff), (float)((v >> 8) & 0xff)),
+                                                       pack2((float)((v >> 16) & 0xff), 0.f), 0u, 0u);
+        }
+      }
+    } else {
+      constexpr int X8 = CIN / 8;
+      const uint4* xp = reinterpret_cast<const uint4*>(a.x) + (size_t)b * HIN * HIN * X8;
+      uint4 xv[G::XIT];
+#pragma unroll
+      for (int i = 0; i < G::XIT; ++i) {
+        const int e = min(tid + i * RT, G::XCH - 1);
+        const int pp = e / X8, iy = pp / HP - G::PADB, ix = pp % HP - G::PADB;
+        const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
+        xv[i] = load_sel(xp + (iy * HIN + ix) * X8 + e % X8, xp, ok);
+      }
+#pragma unroll
+      for (int i = 0; i < G::XIT; ++i) {
+        const int e = tid + i * RT;
+        if (e < G::XCH) reinterpret_cast<uint4*>(xs)[e] = xv[i];
+      }
+    }
+    // g_z image [NPIX][GLD]
+    {
+      const uint4* gyp = reinterpret_cast<const uint4*>(a.gy) + (size_t)b * G::NPIX * C8;
+      const uint4* zp = reinterpret_cast<const uint4*>(a.z) + (size_t)b * G::NPIX * C8;
+      uint4 gv[G::GIT], zv[G::GIT];
+#pragma unroll
+      for (int i = 0; i < G::GIT; ++i) {
+        const int e = min(tid + i * RT, G::GCH - 1);
+        gv[i] = gyp[e];
+        zv[i] = zp[e];
+      }
+#pragma unroll
+      for (int i = 0; i < G::GIT; ++i) {
+        const int e = tid + i * RT;
+        if (e < G::GCH) {
+          const uint32_t gw[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w}, zw[4] = {zv[i].x, zv[i].y, zv[i].z, zv[i].w};
+          uint32_t ow[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            ow[k] = pack2(A[2 * k] * bf16_lo(gw[k]) + Bc[2 * k] * bf16_lo(zw[k]) + Cc[2 * k],
+                          A[2 * k + 1] * bf16_hi(gw[k]) + Bc[2 * k + 1] * bf16_hi(zw[k]) + Cc[2 * k + 1]);
+          *reinterpret_cast<uint4*>(gz + (e / C8) * GLD + (e % C8) * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        }
+      }
+    }
+    __syncthreads();
+    // MFMA over this image's pixels
+    for (int s = 0; s < G::KSTEPS; ++s) {
+      const int rA = 32 * s + 8 * g + q, rB = rA + 4;
+      bf16x8 bf[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) bf[n] = tr_frag(gz + rA * GLD + 16 * n + 4 * p, gz + rB * GLD + 16 * n + 4 * p);
+      const int oyA = rA / HOUT, oxA = rA - oyA * HOUT, oyB = rB / HOUT, oxB = rB - oyB * HOUT;
+      const int pA = (oyA * S) * HP + oxA * S, pB = (oyB * S) * HP + oxB * S;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mc * G::MCH + w + 4 * j;
+        if (m < G::MT) {
+          int tap, ci0;
+          if (CINP >= 16) { tap = (16 * m) / CINP; ci0 = (16 * m) % CINP + 4 * p; }
+          else { tap = 2 * m + (p >> 1); ci0 = 4 * (p & 1); }
+          tap = min(tap, 8);
+          const int kh = tap / 3, kw = tap - 3 * (tap / 3), off = kh * HP + kw;
+          const bf16x8 af = tr_frag(xs + (pA + off) * CINP + ci0, xs + (pB + off) * CINP + ci0);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) acc[j][n] = mfma16(af, bf[n], acc[j][n]);
+        }
+      }
+    }
+  }
+  // slab rows k = 16m + 4g + i, cols co = 16n + li
+  float* out = a.part + (size_t)grp * KP * COUT;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = mc * G::MCH + w + 4 * j;
+    if (m < G::MT) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[(16 * m + 4 * g + i) * COUT + 16 * n + li] = acc[j][n][i];
+    }
+  }
+}
+
+// ================================ head =========================================================
+// per image: a18 = relu(bn(z18) + x_in) -> mean pool -> fc 64x10 -> softmax-xent -> backward to g_y18
+__global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
+  __shared__ float pool_part[4][64];
+  __shared__ float pooled[64], dlog[16], gpool[64];
+  __shared__ float redl[2][4][64];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = lane;                           // thread -> channel c, pixels w, w+4, ... (16 each)
+  float mean, rstd;
+  bn_stats(a.stat, c, a.inv_n, mean, rstd);
+  const float sc = a.gamma[c] * rstd, sh = a.beta[c] - mean * sc;
+  const bf16* zp = reinterpret_cast<const bf16*>(a.z) + (size_t)b * 4096;
+  const bf16* sp = reinterpret_cast<const bf16*>(a.sc) + (size_t)b * 4096;
+  float av[16], zv[16];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int px = w + 4 * k;
+    zv[k] = (float)zp[px * 64 + c];
+    av[k] = fmaxf(zv[k] * sc + sh + (float)sp[px * 64 + c], 0.f);
+    s += av[k];
+  }
+  pool_part[w][c] = s;
+  int label = 0;
+  if (tid == 0) label = a.labels[batch_index(a.src, a.B, b)];
+  __syncthreads();
+  if (tid < 64) pooled[tid] = (pool_part[0][tid] + pool_part[1][tid] + pool_part[2][tid] + pool_part[3][tid]) * (1.f / 64.f);
+  __syncthreads();
+  if (tid < 64) {                               // wave 0: logits / softmax / dlogits
+    float lg = 0.f;
+    if (lane < 10) {
+      lg = a.fcb[lane];
+      for (int k = 0; k < 64; ++k) lg += pooled[k] * a.fcw[k * 10 + lane];
+    }
+    const float lgm = lane < 10 ? lg : -INFINITY;
+    float m = lgm;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float e = lane < 10 ? __expf(lg - m) : 0.f;
+    float se = e;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+    const int lab = __shfl(label, 0);
+    // argmax (first max) for accuracy
+    int am = lane < 10 && lg == m ? lane : 64;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o));
+    const float lse = m + __logf(se);
+    const float lgl = __shfl(lg, lab);
+    if (lane == 0) { a.loss_img[b] = lse - lgl; a.correct_img[b] = am == lab ? 1 : 0; }
+    if (lane < 10) {
+      if (a.logits_out) a.logits_out[b * 10 + lane] = lg;
+      dlog[lane] = (e / se - (lane == lab ? 1.f : 0.f)) * a.inv_batch;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float gp = 0.f;
+#pragma unroll
+    for (int n = 0; n < 10; ++n) gp += a.fcw[tid * 10 + n] * dlog[n];
+    gpool[tid] = gp * (1.f / 64.f);
+    float* fp = a.fc_part + (size_t)b * 656;
+#pragma unroll
+    for (int n = 0; n < 10; ++n) fp[tid * 10 + n] = pooled[tid] * dlog[n];
+    if (tid < 10) fp[640 + tid] = dlog[tid];
+  }
+  __syncthreads();
+  const float gpc = gpool[c];
+  bf16* gyo = reinterpret_cast<bf16*>(a.gy) + (size_t)b * 4096;
+  float r1 = 0.f, r2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int px = w + 4 * k;
+    const float gy = av[k] > 0.f ? gpc : 0.f;
+    gyo[px * 64 + c] = (bf16)gy;
+    r1 += gy;
+    r2 += gy * (zv[k] - mean) * rstd;
+  }
+  redl[0][w][c] = r1;
+  redl[1][w][c] = r2;
+  __syncthreads();
+  if (tid < 64) {
+    atomicAdd(a.red + tid, (double)(redl[0][0][tid] + redl[0][1][tid] + redl[0][2][tid] + redl[0][3][tid]));
+    atomicAdd(a.red + 64 + tid, (double)(redl[1][0][tid] + redl[1][1][tid] + redl[1][2][tid] + redl[1][3][tid]));
+  }
+}
+
+// ================================ SGD ==========================================================
+DEV float4 add4r(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
+
+// 64 float4 outputs per block, 4 splits over the slabs (fixed order)
+DEV float4 split4_sum(const float* p, size_t stride, int n, float4* lds) {
+  const int sp = threadIdx.x >> 6, idx = threadIdx.x & 63;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int q = sp;
+  for (; q + 28 < n; q += 32) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + (size_t)(q + 4 * u) * stride);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s = add4r(s, v[u]);
+  }
+  for (; q < n; q += 4) s = add4r(s, *reinterpret_cast<const float4*>(p + (size_t)q * stride));
+  lds[threadIdx.x] = s;
+  __syncthreads();
+  return add4r(add4r(lds[idx], lds[64 + idx]), add4r(lds[128 + idx], lds[192 + idx]));
+}
+
+// modes: 0 reduce slabs + apply (1 GPU); 1 reduce slabs into `grad` (DP, before the all-reduce);
+//        2 apply grad_scale * `grad` (DP, after it); 3 refresh the bf16 shadows from the master only
+__global__ __launch_bounds__(256) void k_rn_sgd(DmlcRnSgdArgs a) {
+  __shared__ float4 lds[256];
+  const int64_t step = *a.step;
+  const float lr = a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
+  const int mode = a.mode;
+  const bool reduce = mode <= 1, apply = mode == 0 || mode == 2;
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  int l = 0;
+  while (l <= DMLC_RN_LAYERS && blk >= a.blk_start[l + 1]) ++l;
+  if (l < DMLC_RN_LAYERS) {
+    const int cin = a.cin[l], cout = a.cout[l], cinp = cin < 8 ? 8 : cin;
+    const int kp = (9 * cinp + 31) / 32 * 32, kpd = (9 * cout + 31) / 32 * 32;
+    const int n4 = 9 * cin * cout / 4, co4n = cout / 4;
+    const int o4 = (blk - a.blk_start[l]) * 64 + (tid & 63);
+    const bool valid = o4 < n4;
+    const int oc = valid ? o4 : 0;
+    const int row = oc / co4n, co = (oc - row * co4n) * 4;          // HWIO row = tap*cin + ci
+    const int tap = row / cin, ci = row - tap * cin, k = tap * cinp + ci;
+    const size_t off = (size_t)a.conv_off[l] + (size_t)row * cout + co;
+    float4 gsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (reduce) gsum = split4_sum(a.part[l] + (size_t)k * cout + co, (size_t)kp * cout, a.G[l], lds);
+    if (tid < 64 && valid) {
+      if (mode == 1) {
+        *reinterpret_cast<float4*>(a.grad + off) = gsum;
+      } else {
+        if (mode == 2) {
+          const float4 gv = *reinterpret_cast<const float4*>(a.grad + off);
+          gsum = make_float4(gv.x * a.grad_scale, gv.y * a.grad_scale, gv.z * a.grad_scale, gv.w * a.grad_scale);
+        }
+        float* m = a.master + off;
+        float4 wv = *reinterpret_cast<float4*>(m);
+        if (apply) {
+          wv.x -= lr * gsum.x; wv.y -= lr * gsum.y; wv.z -= lr * gsum.z; wv.w -= lr * gsum.w;
+          *reinterpret_cast<float4*>(m) = wv;
+        }
+        bf16* wf = reinterpret_cast<bf16*>(a.wf[l]);
+        wf[(co + 0) * kp + k] = (bf16)wv.x; wf[(co + 1) * kp + k] = (bf16)wv.y;
+        wf[(co + 2) * kp + k] = (bf16)wv.z; wf[(co + 3) * kp + k] = (bf16)wv.w;
+        if (a.wd[l])
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.wd[l]) + (size_t)ci * kpd + (8 - tap) * cout + co) =
+              pack4(wv.x, wv.y, wv.z, wv.w);
+      }
+    }
+  } else if (l == DMLC_RN_LAYERS) {              // fc: 164 float4 of [640 dW | 10 db | pad], 4 splits over images
+    const int o4 = (blk - a.blk_start[l]) * 64 + (tid & 63);
+    const bool valid = o4 < 164;
+    float4 gsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (reduce) gsum = split4_sum(a.fc_part + 4 * (valid ? o4 : 0), 656, a.B, lds);
+    if (tid < 64 && valid && mode != 3) {
+      const float gv[4] = {gsum.x, gsum.y, gsum.z, gsum.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = 4 * o4 + j;
+        if (e < 650) {
+          const size_t off = e < 640 ? (size_t)a.fcw_off + e : (size_t)a.fcb_off + e - 640;
+          if (mode == 1) a.grad[off] = gv[j];
+          else a.master[off] -= lr * (mode == 2 ? a.grad[off] * a.grad_scale : gv[j]);
+        }
+      }
+    }
+  } else if (mode != 3) {                        // BN gamma/beta + running statistics (one block)
+    for (int e = tid; e < DMLC_RN_LAYERS * 64; e += 256) {
+      const int L = e / 64, c = e % 64;
+      if (c < a.cout[L]) {
+        const double* st = a.stat + L * 128;
+        const double* rd = a.red + L * 128;
+        const size_t og = (size_t)a.gamma_off[L] + c, ob = (size_t)a.beta_off[L] + c;
+        if (mode == 1) {
+          a.grad[og] = (float)rd[64 + c];
+          a.grad[ob] = (float)rd[c];
+          continue;
+        }
+        a.master[og] -= lr * (mode == 2 ? a.grad[og] * a.grad_scale : (float)rd[64 + c]);
+        a.master[ob] -= lr * (mode == 2 ? a.grad[ob] * a.grad_scale : (float)rd[c]);
+        const double inv = (double)a.inv_n[L];
+        const double mean = st[c] * inv;
+        double var = st[64 + c] * inv - mean * mean;
+        var = var > 0.0 ? var : 0.0;
+        const double nn = 1.0 / inv;
+        const float m = a.bn_momentum;
+        float* mm = a.state + a.mm_off[L] + c;
+        float* mv = a.state + a.mv_off[L] + c;
+        *mm = (1.f - m) * *mm + m * (float)mean;
+        *mv = (1.f - m) * *mv + m * (float)(var * nn / (nn - 1.0));
+      }
+    }
+  }
+  if (!apply) return;
+  __syncthreads();
+  if (tid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (unsigned)gridDim.x - 1) {
+      float loss = 0.f;
+      int corr = 0;
+      for (int q = 0; q < a.B; ++q) { loss += a.loss_img[q]; corr += a.correct_img[q]; }
+      float* st = a.stats + (size_t)(step % a.stats_len) * 4;
+      st[0] = (float)(step + 1);
+      st[1] = loss / (float)a.B;
+      st[2] = (float)corr / (float)a.B;
+      st[3] = lr;
+      *a.step = step + 1;
+      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace rn
+}  // namespace dmlc
+
+using namespace dmlc;
+using namespace dmlc::rn;
+
+namespace {
+
+template <class KFn>
+void set_lds(KFn* f, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+// the ResNet-20 layer shapes (CIN, COUT, HIN, S)
+#define DMLC_RN_SHAPES(X) \
+  X(3, 16, 32, 1)         \
+  X(16, 16, 32, 1)        \
+  X(16, 32, 32, 2)        \
+  X(32, 32, 16, 1)        \
+  X(32, 64, 16, 2)        \
+  X(64, 64, 8, 1)
+
+template <int CI, int CO, int H, int ST>
+hipError_t launch_fwd(const DmlcRnFwdArgs& a, hipStream_t s) {
+  using F = Fwd<CI, CO, H, ST>;
+  static bool once = false;
+  if (!once) { set_lds(&k_rn_fwd<CI, CO, H, ST>, F::LDS); once = true; }
+  hipLaunchKernelGGL((k_rn_fwd<CI, CO, H, ST>), dim3(a.B), dim3(RT), F::LDS, s, a);
+  return hipGetLastError();
+}
+
+template <int CI, int CO, int H, int ST>
+hipError_t launch_dgrad(const DmlcRnDgradArgs& a, hipStream_t s) {
+  if constexpr (CI < 16) {
+    return hipErrorInvalidValue;             // the stem has no input gradient
+  } else {
+    using D = Dg<CI, CO, H, ST>;
+    static bool once = false;
+    if (!once) { set_lds(&k_rn_dgrad<CI, CO, H, ST>, D::LDS); once = true; }
+    hipLaunchKernelGGL((k_rn_dgrad<CI, CO, H, ST>), dim3(a.B), dim3(RT), D::LDS, s, a);
+    return hipGetLastError();
+  }
+}
+
+template <int CI, int CO, int H, int ST>
+hipError_t launch_wgrad(const DmlcRnWgradArgs& a, hipStream_t s) {
+  using G = Wg<CI, CO, H, ST>;
+  static bool once = false;
+  if (!once) { set_lds(&k_rn_wgrad<CI, CO, H, ST>, G::LDS); once = true; }
+  hipLaunchKernelGGL((k_rn_wgrad<CI, CO, H, ST>), dim3(a.G, G::MC), dim3(RT), G::LDS, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t dmlc_rn_fwd(const DmlcRnLayerGeom* g, const DmlcRnFwdArgs* a, hipStream_t s) {
+#define X(CI, CO, H, ST) \
+  if (g->cin == CI && g->cout == CO && g->hin == H && g->stride == ST) return launch_fwd<CI, CO, H, ST>(*a, s);
+  DMLC_RN_SHAPES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t dmlc_rn_dgrad(const DmlcRnLayerGeom* g, const DmlcRnDgradArgs* a, hipStream_t s) {
+#define X(CI, CO, H, ST) \
+  if (CI >= 16 && g->cin == CI && g->cout == CO && g->hin == H && g->stride == ST) return launch_dgrad<CI, CO, H, ST>(*a, s);
+  DMLC_RN_SHAPES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t dmlc_rn_wgrad(const DmlcRnLayerGeom* g, const DmlcRnWgradArgs* a, hipStream_t s) {
+#define X(CI, CO, H, ST) \
+  if (g->cin == CI && g->cout == CO && g->hin == H && g->stride == ST) return launch_wgrad<CI, CO, H, ST>(*a, s);
+  DMLC_RN_SHAPES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t dmlc_rn_head(const DmlcRnHeadArgs* a, hipStream_t s) {
+  hipLaunchKernelGGL(k_rn_head, dim3(a->B), dim3(RT), 0, s, *a);
+  return hipGetLastError();
+}
+
+hipError_t dmlc_rn_sgd(DmlcRnSgdArgs* a, hipStream_t s) {
+  int blocks = 0;
+  for (int l = 0; l < DMLC_RN_LAYERS; ++l) {
+    a->blk_start[l] = blocks;
+    blocks += (9 * a->cin[l] * a->cout[l] / 4 + 63) / 64;
+  }
+  a->blk_start[DMLC_RN_LAYERS] = blocks;          // fc: 3 blocks
+  blocks += 3;
+  a->blk_start[DMLC_RN_LAYERS + 1] = blocks;      // BN parameters + running statistics: 1 block
+  blocks += 1;
+  hipLaunchKernelGGL(k_rn_sgd, dim3(blocks), dim3(256), 0, s, *a);
+  return hipGetLastError();
+}
+
+}  // extern "C"

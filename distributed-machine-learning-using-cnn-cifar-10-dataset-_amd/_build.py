@@ -111,10 +111,11 @@ def build(hip: bool = True, rt: bool = True, jobs: int | None = None) -> dict:
             o = os.path.join(OBJ_DIR, os.path.basename(src) + (".timing.o" if TIMING else ".o"))
             hip_objs.append(o)
             jobs_list.append((src, headers, o, [hipcc], hip_flags))
-        bsrc = os.path.join(CSRC, "bindings", "torch_ops.cpp")
-        o = os.path.join(OBJ_DIR, "torch_ops.cpp.o")
-        hip_objs.append(o)
-        jobs_list.append((bsrc, headers, o, ["g++"], torch_flags))
+        bheaders = headers + glob.glob(os.path.join(CSRC, "bindings", "*.h"))
+        for bsrc in sorted(glob.glob(os.path.join(CSRC, "bindings", "*.cpp"))):
+            o = os.path.join(OBJ_DIR, os.path.basename(bsrc) + ".o")
+            hip_objs.append(o)
+            jobs_list.append((bsrc, bheaders, o, ["g++"], torch_flags))
     if rt:
         rt_headers = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
         import pybind11

@@ -1,0 +1,348 @@
+"""Fused MI355X training engine for ResNet-20 (BASELINE.json config 4; model: models/resnet.py).
+
+Not in the reference (/root/reference/cifar10cnn.py only has the 2-conv CNN); SURVEY.md §2.C lists
+ResNet-20 as the "extra kernels" configuration: conv3x3 stride 1/2, train-mode BatchNorm, residual
+add, global average pool.  One step is 19 forward convs + 1 head + 18 dgrads + 19 wgrads + 1 SGD,
+all HIP kernels of csrc/kernels/resnet.hip, captured as one HIP graph:
+
+  fwd  l=0..18   z_l = conv_l(a_{l-1}); the prologue of conv_l applies BN_{l-1} (+ReLU, + option-A
+                 shortcut) from the fp64 batch statistics conv_{l-1}'s epilogue accumulated, and
+                 materialises a_{l-1} for the backward.  Conv_0 gathers the uint8 batch itself.
+  head           BN_18 + residual + ReLU + global average pool + fc + softmax-xent + its backward
+  bwd  l=18..1   dgrad_l: g_z_l (BN backward, prologue) -> g_a_{l-1} (+ shortcut grad) -> ReLU mask
+                 -> g_y_{l-1} and the BN_{l-1} reductions (epilogue)
+       l=18..0   wgrad_l on a side stream (a second graph branch), split-K fp32 slabs
+  sgd            slab reduction + SGD (conv, BN gamma/beta, fc) + BN running statistics (momentum 0.1)
+                 + bf16 weight shadows + global_step++ + stats ring
+
+Batch statistics are per rank (as in the eager model under DP).  With data parallelism the SGD runs
+in two halves around ONE all-reduce of the 1.1 MB flat gradient (mode 1 -> RCCL -> mode 2).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import config as C
+from ..models import resnet as R
+from ..ops import _ext
+
+OPS = None
+
+
+def _ops():
+    global OPS
+    if OPS is None:
+        _ext.hip()
+        OPS = torch.ops.dmlc
+    return OPS
+
+
+def layer_table():
+    """[(name prefix, cin, cout, hin, stride, shortcut mode used when this layer's output is applied)]
+    in execution order (l = 0..18)."""
+    layers = [("stem", 3, 16, 32, 1)]
+    cin, hin = 16, 32
+    for s, w in enumerate(R.WIDTHS):
+        for b in range(R.BLOCKS):
+            stride = 2 if (s > 0 and b == 0) else 1
+            layers.append((f"stage{s}/block{b}/a", cin, w, hin, stride))
+            hin //= stride
+            layers.append((f"stage{s}/block{b}/b", w, w, hin, 1))
+            cin = w
+    return layers
+
+
+LAYERS = layer_table()
+NL = len(LAYERS)
+assert NL == 19
+
+
+def _kp(cin):
+    return (9 * max(cin, 8) + 31) // 32 * 32
+
+
+def _kpd(cout):
+    return (9 * cout + 31) // 32 * 32
+
+
+def _block_sc_mode(b_layer: int) -> int:
+    """Shortcut mode of the block whose second conv is ``b_layer`` (1 identity, 2 subsample+pad)."""
+    a_layer = b_layer - 1
+    return 2 if LAYERS[a_layer][4] == 2 else 1
+
+
+class FusedResNetEngine:
+    """Owns every device buffer of the fused ResNet-20 step.  Parameters: one flat fp32 buffer in the
+    TF layout of models/resnet.py (HWIO kernels), BN moving statistics in a second flat buffer."""
+
+    def __init__(self, batch_size: int, data: torch.Tensor, labels: torch.Tensor, *, device=None,
+                 flat_params: Optional[torch.Tensor] = None, state: Optional[torch.Tensor] = None,
+                 lr: float = C.LEARNING_RATE, lr_decay: float = C.LR_DECAY,
+                 decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, world_size: int = 1,
+                 rank: int = 0, process_group=None, seed: int = 0, groups: Optional[List[int]] = None,
+                 stats_len: int = 4096, comm_dtype: str = "fp32"):
+        ops = _ops()
+        self.ops = ops
+        self.device = torch.device(device or "cuda")
+        dev = self.device
+        B = int(batch_size)
+        if B < 16 or B % 16 != 0:
+            raise ValueError("fused ResNet engine needs a batch size that is a positive multiple of 16")
+        self.B = B
+        self.world_size, self.rank, self.pg = world_size, rank, process_group
+        self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
+        self.seed, self.comm_dtype = seed, comm_dtype
+
+        assert data.dtype == torch.uint8 and tuple(data.shape[1:]) == (32, 32, 3)
+        self.data = data.to(dev).contiguous()
+        self.labels = labels.to(dev, torch.int32).contiguous()
+        self.n_data = self.data.shape[0]
+        self.shard = self.n_data // world_size
+        self.period = max(1, self.shard // B)
+        self.perm = torch.zeros(self.period * B, dtype=torch.int32, device=dev)
+        self.cur_epoch = -1
+
+        f0, s0 = R.init_flat_params(torch.Generator().manual_seed(seed))
+        if flat_params is not None:
+            f0 = flat_params
+        if state is not None:
+            s0 = state
+        self.master = f0.to(dev, torch.float32).contiguous().clone()
+        self.state = s0.to(dev, torch.float32).contiguous().clone()
+        self.grad = torch.zeros_like(self.master) if world_size > 1 else None
+        P = {s.name[len(R.SCOPE) + 1:]: s for s in R.PARAM_SPECS}
+        S = {s.name[len(R.SCOPE) + 1:]: s for s in R.STATE_SPECS}
+        view = lambda buf, s: buf[s.offset:s.offset + s.numel]
+        self.conv_off = [P[f"{n}/conv/kernel"].offset for n, *_ in LAYERS]
+        self.gamma_off = [P[f"{n}/bn/gamma"].offset for n, *_ in LAYERS]
+        self.beta_off = [P[f"{n}/bn/beta"].offset for n, *_ in LAYERS]
+        self.mm_off = [S[f"{n}/bn/moving_mean"].offset for n, *_ in LAYERS]
+        self.mv_off = [S[f"{n}/bn/moving_variance"].offset for n, *_ in LAYERS]
+        self.gamma = [view(self.master, P[f"{n}/bn/gamma"]) for n, *_ in LAYERS]
+        self.beta = [view(self.master, P[f"{n}/bn/beta"]) for n, *_ in LAYERS]
+        self.fcw_off, self.fcb_off = P["fc/weights"].offset, P["fc/biases"].offset
+        self.fcw, self.fcb = view(self.master, P["fc/weights"]), view(self.master, P["fc/biases"])
+
+        bf = torch.bfloat16
+        z = lambda *s, dt=bf: torch.zeros(*s, dtype=dt, device=dev)
+        self.wf = [z(co, _kp(ci)) for _, ci, co, _, _ in LAYERS]
+        self.wd = [z(co, _kp(ci)) if l == 0 else z(ci, _kpd(co)) for l, (_, ci, co, _, _) in enumerate(LAYERS)]
+        hout = [h // s for _, _, _, h, s in LAYERS]
+        self.z = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout, LAYERS)]
+        self.gy = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout, LAYERS)]
+        self.a = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout[:-1], LAYERS[:-1])]   # a_0 .. a_17
+        self.acc = torch.zeros(2, NL, 128, dtype=torch.float64, device=dev)     # [stat | red] fp64 sums
+        self.stat, self.red = self.acc[0], self.acc[1]
+        self.groups = groups or [self._pick_groups(B, ci, co) for _, ci, co, _, _ in LAYERS]
+        self.part = [z(g, _kp(ci), co, dt=torch.float32) for g, (_, ci, co, _, _) in zip(self.groups, LAYERS)]
+        self.fc_part = z(B, 656, dt=torch.float32)
+        self.loss_img = z(B, dt=torch.float32)
+        self.correct_img = z(B, dt=torch.int32)
+        self.logits_buf = z(B, 10, dt=torch.float32)
+        self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
+
+        self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.side_stream = torch.cuda.Stream(device=dev)
+        self.host_step = 0
+        self.refresh_shadows()
+
+    # ------------------------------------------------------------------------------------------
+    @staticmethod
+    def _pick_groups(B: int, cin: int, cout: int) -> int:
+        """Split-K image groups of one wgrad: about 2.6 MB of fp32 slabs per layer (the SGD kernel
+        reads them back), a power of two in [8, B/2]."""
+        target = 655360 / (_kp(cin) * cout)
+        g = 1 << max(0, int(math.floor(math.log2(max(1.0, target)))))
+        return int(max(1, min(B // 2, max(8, g))))
+
+    def refresh_shadows(self):
+        self._sgd(mode=3)
+
+    def set_step(self, step: int):
+        self.step_t.fill_(int(step))
+        self.host_step = int(step)
+
+    def epoch_permutation(self, epoch: int) -> torch.Tensor:
+        g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + epoch)
+        perm = torch.randperm(self.n_data, generator=g, device=self.device)
+        return perm[self.rank::self.world_size][: self.period * self.B].to(torch.int32)
+
+    def _maybe_new_epoch(self):
+        epoch = self.host_step // self.period
+        if epoch != self.cur_epoch:
+            self.perm.copy_(self.epoch_permutation(epoch))
+            self.cur_epoch = epoch
+
+    # --- kernels ------------------------------------------------------------------------------
+    def _forward(self, idx, counter, period, logits_out=None):
+        o = self.ops
+        self.acc.zero_()
+        for l, (_, ci, co, h, s) in enumerate(LAYERS):
+            if l == 0:
+                o.rn_fwd(ci, co, h, s, self.data, idx, counter, period, 0, 0, None, None, None, None, None, 0, None,
+                         self.wf[0], self.z[0], self.stat[0])
+                continue
+            p = l - 1
+            sc_mode, sc_src = 0, None
+            if p >= 2 and p % 2 == 0:                  # layer p closes a residual block
+                sc_mode = _block_sc_mode(p)
+                sc_src = self.a[p - 2]
+            o.rn_fwd(ci, co, h, s, None, None, None, 1, 0, 0, self.z[p], self.stat[p], self.gamma[p], self.beta[p],
+                     sc_src, sc_mode, self.a[p], self.wf[l], self.z[l], self.stat[l])
+        o.rn_head(self.z[18], self.stat[18], self.gamma[18], self.beta[18], self.a[16], self.fcw, self.fcb,
+                  self.labels, idx, counter, period, 1.0 / (self.B * self.world_size), self.gy[18], self.red[18],
+                  self.fc_part, self.loss_img, self.correct_img, logits_out)
+
+    def _wgrad(self, l):
+        _, ci, co, h, s = LAYERS[l]
+        if l == 0:
+            self.ops.rn_wgrad(ci, co, h, s, self.data, self.perm, self.step_t, self.period, 0, 0, None, self.gy[0],
+                              self.z[0], self.stat[0], self.red[0], self.gamma[0], self.part[0])
+        else:
+            self.ops.rn_wgrad(ci, co, h, s, None, None, None, 1, 0, 0, self.a[l - 1], self.gy[l], self.z[l],
+                              self.stat[l], self.red[l], self.gamma[l], self.part[l])
+
+    def _backward(self):
+        o = self.ops
+        main = torch.cuda.current_stream(self.device)
+        side = self.side_stream
+        for l in range(NL - 1, -1, -1):
+            # gy_l and red_l are complete here (head or dgrad_{l+1}): fork wgrad_l onto the side branch
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                self._wgrad(l)
+            if l == 0:
+                break
+            _, ci, co, h, s = LAYERS[l]
+            p = l - 1
+            sc_mode, gy_sc = 0, None
+            if l % 2 == 1:                             # a-conv: its input also feeds the block shortcut
+                sc_mode = _block_sc_mode(l + 1)
+                gy_sc = self.gy[l + 1]
+            o.rn_dgrad(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
+                       self.a[p], self.z[p], self.stat[p], gy_sc, sc_mode, self.gy[p], self.red[p])
+        main.wait_stream(side)
+
+    def _sgd(self, mode: int, scale: float = 1.0):
+        self.ops.rn_sgd(self.master, self.grad, scale, self.state, self.conv_off, self.gamma_off, self.beta_off,
+                        self.mm_off, self.mv_off, self.fcw_off, self.fcb_off, self.part, self.wf, self.wd, self.stat,
+                        self.red, self.fc_part, self.loss_img, self.correct_img, self.step_t, self.ticket, self.stats,
+                        mode, self.lr0, self.decay, self.decay_steps, self.staircase, R.BN_MOMENTUM)
+
+    def _allreduce(self, t: torch.Tensor):
+        import torch.distributed as dist
+        if self.comm_dtype == "bf16":
+            tb = t.to(torch.bfloat16)
+            dist.all_reduce(tb, group=self.pg)
+            t.copy_(tb)
+        else:
+            dist.all_reduce(t, group=self.pg)
+
+    def _seg_compute(self):
+        self._forward(self.perm, self.step_t, self.period)
+        self._backward()
+        self._sgd(mode=0 if self.world_size == 1 else 1)
+
+    def _seg_apply(self):
+        self._sgd(mode=2, scale=1.0)
+
+    def _eager_step(self):
+        self._seg_compute()
+        if self.world_size > 1:
+            self._allreduce(self.grad)
+            self._seg_apply()
+
+    def compute_gradients(self) -> torch.Tensor:
+        """Forward + backward + slab reduction only (no update); the flat gradient lands in ``grad``."""
+        if self.grad is None:
+            self.grad = torch.zeros_like(self.master)
+        self._maybe_new_epoch()
+        self._forward(self.perm, self.step_t, self.period)
+        self._backward()
+        self._sgd(mode=1)
+        return self.grad
+
+    # --- graph capture --------------------------------------------------------------------------
+    def capture(self):
+        torch.cuda.synchronize(self.device)
+        self.graphs = []
+        pool = torch.cuda.graph_pool_handle()
+        segs = [self._seg_compute] if self.world_size == 1 else [self._seg_compute, self._seg_apply]
+        for fn in segs:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, pool=pool, stream=s):
+                    fn()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self.graphs.append(g)
+        torch.cuda.synchronize(self.device)
+
+    def step(self):
+        self._maybe_new_epoch()
+        if not self.graphs:
+            self._eager_step()
+        elif len(self.graphs) == 1:
+            self.graphs[0].replay()
+        else:
+            self.graphs[0].replay()
+            self._allreduce(self.grad)
+            self.graphs[1].replay()
+        self.host_step += 1
+
+    # --- evaluation -----------------------------------------------------------------------------
+    def eval_model(self):
+        m = R.ResNet20(flat=self.master.detach()).to(self.device)
+        m.state.copy_(self.state)
+        m.eval()
+        return m
+
+    @torch.no_grad()
+    def evaluate(self, data: torch.Tensor, labels: torch.Tensor, max_batches: int = 0) -> float:
+        """Test accuracy with the BN moving statistics (eval-mode forward of the same weights)."""
+        m = self.eval_model()
+        n = data.shape[0]
+        nb = math.ceil(n / self.B)
+        if max_batches:
+            nb = min(nb, max_batches)
+        correct = total = 0
+        for i in range(nb):
+            x = data[i * self.B:(i + 1) * self.B].to(self.device).float()
+            y = labels[i * self.B:(i + 1) * self.B].to(self.device).long()
+            correct += int((m(x).argmax(1) == y).sum())
+            total += y.numel()
+        return correct / max(1, total)
+
+    @torch.no_grad()
+    def forward_logits(self, idx: torch.Tensor) -> torch.Tensor:
+        """Train-mode (batch statistics) logits of dataset rows ``idx`` via the fused kernels — for
+        tests.  Writes activations / statistics but updates nothing."""
+        self._forward(idx.to(self.device, torch.int32).contiguous(), None, 1, logits_out=self.logits_buf)
+        return self.logits_buf.clone()
+
+    # --- state ----------------------------------------------------------------------------------
+    def read_stats(self, step: int) -> Dict[str, float]:
+        row = self.stats[(step - 1) % self.stats.shape[0]].tolist()
+        return {"global_step": int(row[0]), "loss": row[1], "accuracy": row[2], "lr": row[3]}
+
+    def global_step(self) -> int:
+        return int(self.step_t.item())
+
+    def flat_params(self) -> torch.Tensor:
+        return self.master.detach().cpu()
+
+    def load_flat_params(self, flat: torch.Tensor, step: Optional[int] = None, state: Optional[torch.Tensor] = None):
+        self.master.copy_(flat.to(self.device, torch.float32))
+        if state is not None:
+            self.state.copy_(state.to(self.device, torch.float32))
+        if step is not None:
+            self.set_step(step)
+        self.refresh_shadows()

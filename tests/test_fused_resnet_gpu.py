@@ -1,0 +1,183 @@
+"""Fused ResNet-20 HIP kernels (csrc/kernels/resnet.hip) vs the fp32 PyTorch model (models/resnet.py,
+train-mode BatchNorm): forward logits, every parameter gradient, one SGD step incl. BN running
+statistics, graph replay vs eager launches, and a short convergence run."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dmlc.data.cifar import synthetic
+from dmlc.engine.fused_resnet import FusedResNetEngine
+from dmlc.models import resnet as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randint(0, 256, (n, 32, 32, 3), dtype=torch.uint8, generator=g),
+            torch.randint(0, 10, (n,), dtype=torch.int32, generator=g))
+
+
+def _ref(flat, state, data, labels, idx):
+    dev = "cuda"
+    flat = flat.to(dev).clone().requires_grad_(True)
+    st = state.to(dev).clone()
+    x = data[idx.long()].to(dev).float()
+    logits = R.resnet20_forward(x, R._views(flat, R.PARAM_SPECS), R._views(st, R.STATE_SPECS), training=True)
+    loss = F.cross_entropy(logits, labels[idx.long()].to(dev).long())
+    loss.backward()
+    return logits.detach(), loss.detach(), flat.grad.detach().cpu(), st.cpu()
+
+
+def _rel(a, b):
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+def local_layer_errors(eng, data, labels, idx):
+    """Per-kernel numerics: every fused kernel's output vs fp32 PyTorch ops fed with the fused
+    engine's OWN inputs for that kernel (so bf16 error does not compound across 19 layers and ReLU
+    mask flips cannot occur).  Call after ``eng.compute_gradients()``.  Returns {check: rel error}."""
+    from dmlc.engine.fused_resnet import LAYERS, _block_sc_mode
+    dev = eng.device
+    P = {s.name[len(R.SCOPE) + 1:]: s for s in R.PARAM_SPECS}
+    flat = eng.flat_params().to(dev)
+    grad = eng.grad
+    f = lambda t: t.float().permute(0, 3, 1, 2)          # NHWC bf16 -> NCHW fp32
+    out = {}
+    ximg = data[idx.long()].to(dev).float().permute(0, 3, 1, 2)
+
+    def bn_train(z, name):
+        g = flat[P[f"{name}/bn/gamma"].offset:][:z.shape[1]].clone().requires_grad_(True)
+        b = flat[P[f"{name}/bn/beta"].offset:][:z.shape[1]].clone().requires_grad_(True)
+        return F.batch_norm(z, None, None, g, b, training=True, eps=R.BN_EPS), g, b
+
+    for l, (name, ci, co, h, s) in enumerate(LAYERS):
+        spec = P[f"{name}/conv/kernel"]
+        w = flat[spec.offset:spec.offset + spec.numel].view(spec.shape).clone().requires_grad_(True)
+        x = (ximg if l == 0 else f(eng.a[l - 1])).clone().requires_grad_(True)
+        z = R._conv3x3(x, w, s)
+        out[f"fwd{l}"] = _rel(f(eng.z[l]), z)
+        y, g, b = bn_train(f(eng.z[l]), name)
+        y.backward(f(eng.gy[l]))
+        zz = f(eng.z[l]).detach().requires_grad_(True)
+        yz, _, _ = bn_train(zz, name)
+        yz.backward(f(eng.gy[l]))
+        z2 = R._conv3x3(x, w, s)
+        z2.backward(zz.grad)
+        out[f"wgrad{l}"] = _rel(grad[spec.offset:spec.offset + spec.numel].view(spec.shape), w.grad)
+        out[f"gamma{l}"] = _rel(grad[P[f"{name}/bn/gamma"].offset:][:co], g.grad)
+        out[f"beta{l}"] = _rel(grad[P[f"{name}/bn/beta"].offset:][:co], b.grad)
+        if l == 0:
+            continue
+        ga = x.grad.clone()
+        if l % 2 == 1:                                   # a-conv: + shortcut gradient of its block
+            gsc = f(eng.gy[l + 1])
+            if _block_sc_mode(l + 1) == 2:
+                up = torch.zeros_like(ga)
+                up[:, :, ::2, ::2] = gsc[:, :ci]
+                gsc = up
+            ga = ga + gsc
+        gy_prev = ga * (f(eng.a[l - 1]) > 0).float()
+        out[f"dgrad{l}"] = _rel(f(eng.gy[l - 1]), gy_prev)
+    # head: BN_18 + residual + ReLU + pool + fc + xent -> g_y18
+    z18 = f(eng.z[18])
+    y18, _, _ = bn_train(z18, LAYERS[18][0])
+    y18 = y18.detach().requires_grad_(True)
+    a18 = F.relu(y18 + f(eng.a[16]))
+    fw = flat[P["fc/weights"].offset:][:640].view(64, 10)
+    fb = flat[P["fc/biases"].offset:][:10]
+    logits = a18.mean(dim=(2, 3)) @ fw + fb
+    F.cross_entropy(logits, labels[idx.long()].to(dev).long()).backward()
+    out["head"] = _rel(f(eng.gy[18]), y18.grad)
+    return out
+
+
+@pytest.mark.parametrize("B", [16, 128])
+def test_forward_logits_match_reference(B):
+    data, labels = _data(2 * B)
+    eng = FusedResNetEngine(B, data, labels, seed=1)
+    idx = torch.randperm(data.shape[0])[:B].to(torch.int32)
+    got = eng.forward_logits(idx).cpu()
+    ref, loss, _, _ = _ref(eng.flat_params(), eng.state.cpu(), data, labels, idx)
+    assert _rel(got, ref.cpu()) < 5e-2, _rel(got, ref.cpu())
+    # per-image loss / accuracy published by the head kernel
+    assert abs(float(eng.loss_img.mean()) - float(loss)) < 5e-2 * max(1.0, float(loss))
+
+
+@pytest.mark.parametrize("B", [32, 128])
+def test_each_kernel_matches_fp32_ops(B):
+    data, labels = _data(4 * B, seed=3)
+    eng = FusedResNetEngine(B, data, labels, seed=2)
+    eng._maybe_new_epoch()
+    idx = eng.perm[:B].cpu()
+    eng.compute_gradients()
+    errs = local_layer_errors(eng, data, labels, idx)
+    bad = {k: v for k, v in errs.items() if v > 3e-2}
+    assert not bad, bad
+
+
+def test_end_to_end_gradients_close_to_fp32_model():
+    """End to end the bf16 forward drifts ~2-3 % by layer 18, which flips a few ReLU masks, so the
+    deepest gradients agree only to cos ~0.95; this pins that level (a wrong kernel gives ~0)."""
+    B = 64
+    data, labels = _data(4 * B, seed=3)
+    eng = FusedResNetEngine(B, data, labels, seed=2)
+    eng._maybe_new_epoch()
+    idx = eng.perm[:B].cpu()
+    grad = eng.compute_gradients().cpu()
+    _, _, gref, _ = _ref(eng.flat_params(), eng.state.cpu(), data, labels, idx)
+    cos = float(F.cosine_similarity(grad, gref, dim=0))
+    assert cos > 0.9, cos
+    for s in R.PARAM_SPECS:
+        a, b = grad[s.offset:s.offset + s.numel], gref[s.offset:s.offset + s.numel]
+        assert float(F.cosine_similarity(a, b, dim=0)) > 0.8, s.name
+
+
+def test_sgd_step_and_bn_running_stats():
+    B = 64
+    data, labels = _data(4 * B, seed=5)
+    eng = FusedResNetEngine(B, data, labels, seed=4, lr=0.05)
+    before, st0 = eng.flat_params().clone(), eng.state.cpu().clone()
+    eng._maybe_new_epoch()
+    idx = eng.perm[:B].cpu()
+    eng.step()
+    torch.cuda.synchronize()
+    _, loss, gref, st_ref = _ref(before, st0, data, labels, idx)
+    assert eng.global_step() == 1
+    st = eng.read_stats(1)
+    assert abs(st["loss"] - float(loss)) / max(1.0, float(loss)) < 5e-2
+    delta, dref = eng.flat_params() - before, -0.05 * gref
+    assert float(F.cosine_similarity(delta, dref, dim=0)) > 0.98
+    assert _rel(eng.state.cpu(), st_ref) < 2e-2
+
+
+def test_graph_replay_matches_eager_launches():
+    B = 32
+    data, labels = _data(8 * B, seed=7)
+    e1 = FusedResNetEngine(B, data, labels, seed=6, lr=0.02)
+    e2 = FusedResNetEngine(B, data, labels, seed=6, lr=0.02)
+    e2.capture()
+    for _ in range(3):
+        e1.step()
+        e2.step()
+    torch.cuda.synchronize()
+    assert e1.global_step() == e2.global_step() == 3
+    assert _rel(e2.flat_params(), e1.flat_params()) < 1e-3
+    for k in (1, 2, 3):
+        assert abs(e1.read_stats(k)["loss"] - e2.read_stats(k)["loss"]) < 1e-2
+
+
+def test_short_training_reduces_loss():
+    B = 128
+    data, labels = synthetic(32 * B, seed=11, learnable=True)
+    eng = FusedResNetEngine(B, data, labels, seed=3, lr=0.05, staircase=False)
+    eng.capture()
+    for _ in range(60):
+        eng.step()
+    torch.cuda.synchronize()
+    first = sum(eng.read_stats(k)["loss"] for k in range(1, 6)) / 5
+    last = sum(eng.read_stats(k)["loss"] for k in range(56, 61)) / 5
+    assert last < 0.85 * first, (first, last)
+    acc = eng.evaluate(data[:1024], labels[:1024])
+    assert 0.0 <= acc <= 1.0

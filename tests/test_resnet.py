@@ -105,3 +105,23 @@ def test_cli_resnet20_checkpoint_roundtrip(tmp_path):
                         env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
     assert r2.returncode == 0 and "Restored" in r2.stdout, r2.stdout
     assert int(CK.read_bundle(CK.latest_checkpoint(str(tmp_path)))["global_step"]) == 6
+
+
+def test_fused_resnet_layer_table_matches_model():
+    """The fused engine's execution order / shortcut wiring (CPU-checkable part of engine/fused_resnet.py)."""
+    from dmlc.engine import fused_resnet as FR
+    from dmlc.models import resnet as R
+    convs = [s.name for s in R.PARAM_SPECS if s.name.endswith("/conv/kernel")]
+    assert [f"{R.SCOPE}/{n}/conv/kernel" for n, *_ in FR.LAYERS] == convs
+    shapes = {s.name: s.shape for s in R.PARAM_SPECS}
+    for n, ci, co, h, s in FR.LAYERS:
+        assert shapes[f"{R.SCOPE}/{n}/conv/kernel"] == (3, 3, ci, co)
+    assert [l for l, (*_, s) in enumerate(FR.LAYERS) if s == 2] == [7, 13]
+    assert [FR._block_sc_mode(b) for b in range(2, 19, 2)] == [1, 1, 1, 2, 1, 1, 2, 1, 1]
+    # every conv offset is float4-aligned (the SGD kernel updates HWIO rows 4 c_out at a time)
+    P = {s.name: s.offset for s in R.PARAM_SPECS}
+    assert all(P[f"{R.SCOPE}/{n}/conv/kernel"] % 4 == 0 for n, *_ in FR.LAYERS)
+    for B in (16, 256, 1024):
+        for _, ci, co, _, _ in FR.LAYERS:
+            g = FR.FusedResNetEngine._pick_groups(B, ci, co)
+            assert 1 <= g <= B // 2
