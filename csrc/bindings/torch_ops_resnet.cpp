@@ -29,8 +29,8 @@ Geom geom(int64_t cin, int64_t cout, int64_t hin, int64_t stride) {
   TORCH_CHECK(false, "rn: unsupported conv geometry cin=", cin, " cout=", cout, " hin=", hin, " stride=", stride);
 }
 
-// per-layer statistics accumulators: fp64 [2][64] (sum, sum of squares / R1, R2)
-void check_stat(const Tensor& t, const char* n) { check_numel(t, n, at::kDouble, 128); }
+// per-layer statistics accumulators: fp64 [NSLOT][2][64] (sum, sum of squares / R1, R2)
+void check_stat(const Tensor& t, const char* n) { check_numel(t, n, at::kDouble, DMLC_RN_NSLOT * 128); }
 
 void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::optional<Tensor>& data,
             const c10::optional<Tensor>& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
@@ -203,8 +203,8 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
   dev(master, "master"); dev(state, "state");
   TORCH_CHECK(master.scalar_type() == at::kFloat && state.scalar_type() == at::kFloat, "master/state must be fp32");
   const int64_t np = master.numel(), ns = state.numel();
-  check(stat, "stat", at::kDouble, {L, 128});
-  check(red, "red", at::kDouble, {L, 128});
+  check(stat, "stat", at::kDouble, {L, DMLC_RN_NSLOT, 128});
+  check(red, "red", at::kDouble, {L, DMLC_RN_NSLOT, 128});
   check(fc_part, "fc_part", at::kFloat, {B, 656});
   check_numel(correct_img, "correct_img", at::kInt, B);
   check_numel(loss_img, "loss_img", at::kFloat, B);

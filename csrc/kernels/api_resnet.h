@@ -1,7 +1,7 @@
 // Host-side launch API of the fused ResNet-20 kernels (csrc/kernels/resnet.hip).
 //
 // Conventions: activations NHWC bf16; per-layer BatchNorm statistics are fp64 accumulators
-// (atomicAdd of per-block fp32 partials; zeroed once per step); conv weights have two bf16 shadows:
+// (atomicAdd of per-block fp32 partials into one of NSLOT copies; zeroed once per step); conv weights have two bf16 shadows:
 //   fwd   w [COUT][KP]  k  = tap*CINP + ci        (tap = kh*3 + kw, CINP = max(CIN, 8), KP = 9*CINP -> x32)
 //   dgrad wd [CIN][KPD] k' = tap'*COUT + co       (tap' = 8 - tap: rotated 180 degrees, KPD = 9*COUT -> x32)
 // Layer l computes z_l = conv_l(x_l) with x_l = a_{l-1}, a = relu(bn(z) [+ shortcut]).
@@ -18,7 +18,7 @@ struct DmlcRnFwdArgs {
   // input of this conv: the dataset (stem) or the BN-apply of the previous layer
   const uint8_t* data; DmlcIndexSrc src; int cy, cx;      // stem only
   const void* z_prev;        // bf16 [B][Hin][Hin][CIN]  pre-BN output of layer l-1
-  const double* stat_prev;   // [2][CIN] sum z, sum z^2 of layer l-1
+  const double* stat_prev;   // [NSLOT][2][64] sum z, sum z^2 of layer l-1
   const float* gamma_prev; const float* beta_prev;
   const void* sc_src;        // nullable: block input feeding the residual of layer l-1 (bf16)
   int sc_mode;               // 0 none, 1 identity [B][Hin][Hin][CIN], 2 subsample+zero-pad [B][2Hin][2Hin][CIN/2]
@@ -26,7 +26,7 @@ struct DmlcRnFwdArgs {
   float inv_n_prev;          // 1 / (B * Hin * Hin)
   const void* w;             // bf16 [COUT][KP]
   void* z;                   // bf16 [B][Hout][Hout][COUT]
-  double* stat;              // [2][COUT] accumulators of layer l
+  double* stat;              // [NSLOT][2][64] accumulators of layer l
   int B;
 };
 
@@ -39,7 +39,7 @@ struct DmlcRnDgradArgs {
   const void* gy_sc;         // nullable: g_y of the block's second conv (shortcut gradient)
   int sc_mode;               // 1 identity, 2 subsample (gy_sc is [B][Hin/2][Hin/2][2*CIN])
   void* gy_prev;             // bf16 [B][Hin][Hin][CIN]
-  double* red_prev;          // [2][CIN]
+  double* red_prev;          // [NSLOT][2][64]
   int B;
 };
 
@@ -57,7 +57,7 @@ struct DmlcRnHeadArgs {
   const float* fcw; const float* fcb;   // fp32 master views [64][10], [10]
   const int* labels; DmlcIndexSrc src; float inv_batch;
   void* gy;                  // bf16 [B][8][8][64] g_y_18
-  double* red;               // [2][64] reductions of layer 18
+  double* red;               // [NSLOT][2][64] reductions of layer 18
   float* fc_part;            // [B][656] per-image dW_fc (640) + db_fc (10) + pad
   float* loss_img; int* correct_img;    // [B]
   float* logits_out;         // nullable [B][10]
@@ -65,6 +65,7 @@ struct DmlcRnHeadArgs {
 };
 
 #define DMLC_RN_LAYERS 19
+#define DMLC_RN_NSLOT 8      // fp64 statistics accumulators per layer: [NSLOT][2][64] (slot = block & 7)
 struct DmlcRnSgdArgs {
   float* master; int nparams;
   float* grad; float grad_scale;   // DP: modes 1 (write) / 2 (read, scaled)
@@ -73,11 +74,12 @@ struct DmlcRnSgdArgs {
   int cin[DMLC_RN_LAYERS], cout[DMLC_RN_LAYERS];
   const float* part[DMLC_RN_LAYERS]; int G[DMLC_RN_LAYERS];
   void* wf[DMLC_RN_LAYERS]; void* wd[DMLC_RN_LAYERS];
-  const double* stat; const double* red;   // [19][2][64] each
+  const double* stat; const double* red;   // [19][NSLOT][2][64] each
   float* state; int mm_off[DMLC_RN_LAYERS], mv_off[DMLC_RN_LAYERS];   // BN moving statistics
   float bn_momentum; float inv_n[DMLC_RN_LAYERS];
   int fcw_off, fcb_off; const float* fc_part; int B;
-  int blk_start[DMLC_RN_LAYERS + 2];   // block ranges (set by the launcher): conv layers, fc, BN
+  int blk_start[DMLC_RN_LAYERS + 3];   // block ranges (set by the launcher): conv layers, fc, BN layers
+  int split[DMLC_RN_LAYERS + 1];       // slab split factor per conv layer + fc (set by the launcher)
   int mode;                  // 0 reduce+apply, 1 reduce->grad, 2 apply grad, 3 shadows only
   int64_t* step; float lr0, decay, decay_steps; int staircase;
   unsigned int* ticket;

@@ -1,6 +1,6 @@
-// Fused ResNet-20 training kernels for gfx950 (BASELINE.json config 4; SURVEY.md §2.C "Extra
-// kernels not in the reference": conv3x3 fwd/dgrad/wgrad with stride 1/2, train-mode batch-norm,
-// residual add, global average pool).  Model: models/resnet.py (the eager oracle).
+// Fused ResNet-20 training kernels for gfx950 (BASELINE.json config 4; SURVEY.md §2.C "Extra kernels
+// not in the reference": conv3x3 fwd/dgrad/wgrad with stride 1/2, train-mode batch-norm, residual add,
+// global average pool).  Model: models/resnet.py (the eager oracle).
 //
 // Design (MI355X-first):
 //   * every 3x3 conv is an implicit GEMM on MFMA 16x16x32 bf16 over an LDS image of ONE zero-padded
@@ -12,11 +12,16 @@
 //     the backward); the backward mirrors it: each dgrad's epilogue produces g_y of the layer below
 //     plus its two BN reductions (sum g_y, sum g_y*xhat), and the consumer rebuilds
 //     g_z = gamma*rstd*(g_y - R1/N - xhat*R2/N) in its prologue;
+//   * the fp64 accumulators are spread over NSLOT copies (slot = blockIdx & 7, i.e. one per XCD under
+//     round-robin dispatch) so 256 blocks do not serialise on 64 addresses; consumers fold the slots
+//     once per block (64 threads) into LDS coefficient tables;
 //   * stride-2 dgrad is a stride-1 correlation over a zero-inserted LDS image (pad 2/0);
-//   * weight gradients: split-K over image groups x m-chunks, both operands read with
-//     ds_read_b64_tr_b16 from NHWC LDS images (per-lane row addresses absorb stride and taps);
-//   * the SGD kernel reduces the slabs in fixed order, updates BN running statistics, refreshes
-//     both bf16 weight shadows and bumps the device step counter (graph-capturable).
+//   * weight gradients: split-K over image groups x m-chunks, several images staged per barrier, both
+//     operands read with ds_read_b64_tr_b16 from NHWC LDS images (per-lane row addresses absorb stride
+//     and taps);
+//   * the SGD kernel reduces the slabs in fixed order (per-layer split factor so every thread issues
+//     <= 8 loads), updates BN running statistics, refreshes both bf16 weight shadows and bumps the
+//     device step counter (graph-capturable).
 #include "conv_common.h"
 #include "api_resnet.h"
 
@@ -24,32 +29,90 @@ namespace dmlc {
 namespace rn {
 
 constexpr int RT = 256;
+constexpr int NSLOT = DMLC_RN_NSLOT;          // fp64 statistics copies per layer: [NSLOT][2][64]
 constexpr double BN_EPS = 1e-3;
+
+#ifdef RN_EXP_NOATOM   // experiment: drop the BN-statistics atomics (timing only; numerics are wrong)
+#define RN_ATOMIC_ADD(p, v) ((void)(p), (void)(v))
+#else
+#define RN_ATOMIC_ADD(p, v) atomicAdd(p, v)
+#endif
 
 __host__ __device__ constexpr int round32(int x) { return (x + 31) / 32 * 32; }
 
-// per-channel BN coefficients from fp64 sums (stat: [0..63] sum, [64..127] sum of squares)
-DEV void bn_stats(const double* stat, int c, float inv_n, float& mean, float& rstd) {
-  const double m = stat[c] * (double)inv_n;
-  double var = stat[64 + c] * (double)inv_n - m * m;
+// channel c of a slotted accumulator: (sum, sum of squares) or (R1, R2)
+DEV void slot_sums(const double* st, int c, double& s1, double& s2) {
+  double a[NSLOT], b[NSLOT];
+#pragma unroll
+  for (int k = 0; k < NSLOT; ++k) { a[k] = st[k * 128 + c]; b[k] = st[k * 128 + 64 + c]; }
+  s1 = 0.0; s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < NSLOT; ++k) { s1 += a[k]; s2 += b[k]; }
+}
+
+DEV void bn_mean_rstd(const double* stat, int c, float inv_n, float& mean, float& rstd) {
+  double s1, s2;
+  slot_sums(stat, c, s1, s2);
+  const double m = s1 * (double)inv_n;
+  double var = s2 * (double)inv_n - m * m;
   var = var > 0.0 ? var : 0.0;
   mean = (float)m;
   rstd = (float)(1.0 / sqrt(var + BN_EPS));
 }
 
-DEV float bfv(uint32_t w, int hi) { return hi ? bf16_hi(w) : bf16_lo(w); }
-DEV uint32_t pack2(float a, float b) {
-  const bf16x4 v = pack4(a, b, 0.f, 0.f);
-  uint2 u = __builtin_bit_cast(uint2, v);
-  return u.x;
+// BN backward: g_z = A*g_y + Bc*z + Cc  with  A = gamma*rstd, Bc = -gamma*rstd^2*R2/N, Cc = -A*R1/N - Bc*mean
+DEV void bnb_coeffs(const double* stat, const double* red, const float* gamma, int c, float inv_n, float& A,
+                    float& Bc, float& Cc) {
+  float mean, rstd;
+  bn_mean_rstd(stat, c, inv_n, mean, rstd);
+  double r1, r2;
+  slot_sums(red, c, r1, r2);
+  A = gamma[c] * rstd;
+  Bc = -A * rstd * (float)(r2 * (double)inv_n);
+  Cc = -A * (float)(r1 * (double)inv_n) - Bc * mean;
 }
 
-// fp64 atomic accumulation of 2 x 64 per-block channel partials staged in LDS red[2][64]
-DEV void flush_stats(double* dst, const float* red, int C, int tid) {
-  if (tid < C) {
-    atomicAdd(dst + tid, (double)red[tid]);
-    atomicAdd(dst + 64 + tid, (double)red[64 + tid]);
+DEV uint32_t pack2(float a, float b) {
+  const bf16x4 v = pack4(a, b, 0.f, 0.f);
+  return __builtin_bit_cast(uint2, v).x;
+}
+
+// block-level channel reduction of per-lane partials (lanes with equal li share a channel group) and
+// one fp64 atomic per channel into this block's slot
+template <int CT, int C>
+DEV void reduce_flush(float (&s1)[4], float (&s2)[4], float* red, double* dst, int w, int g, int li, int tid) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) { s1[r] += __shfl_xor(s1[r], o); s2[r] += __shfl_xor(s2[r], o); }
+  const int ct = w % CT;
+  if (li == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[(w * 2 + 0) * 64 + 16 * ct + 4 * g + r] = s1[r];
+      red[(w * 2 + 1) * 64 + 16 * ct + 4 * g + r] = s2[r];
+    }
   }
+  __syncthreads();
+  if (tid < C) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww)
+      if (ww % CT == tid / 16) { t1 += red[(ww * 2) * 64 + tid]; t2 += red[(ww * 2 + 1) * 64 + tid]; }
+    double* d = dst + (blockIdx.x & (NSLOT - 1)) * 128;
+    RN_ATOMIC_ADD(d + tid, (double)t1);
+    RN_ATOMIC_ADD(d + 64 + tid, (double)t2);
+  }
+}
+
+// uint8 NHWC pixel (3 channels) -> 8 bf16 lanes (ci 3..7 zero)
+DEV uint4 px_u8_to_bf16x8(uint32_t v) {
+  return make_uint4(pack2((float)(v & 0xff), (float)((v >> 8) & 0xff)), pack2((float)((v >> 16) & 0xff), 0.f), 0u, 0u);
+}
+DEV uint32_t load_px_u8(const uint8_t* img, int cy, int cx, int iy, int ix, bool ok) {
+  const uint8_t* s = img + (ok ? ((cy + iy) * 32 + cx + ix) * 3 : 0);
+  const uint32_t v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
+  return ok ? v : 0u;
 }
 
 // ================================ forward ======================================================
@@ -63,7 +126,8 @@ struct Fwd {
   static constexpr int CT = COUT / 16, WPC = 4 / CT, NPXT = HOUT * HOUT / 16, NPT = NPXT / WPC;
   static constexpr int NCH = HP * HP * CINP / 8;               // 16-B chunks of the padded image
   static constexpr int IT = (NCH + RT - 1) / RT;
-  static constexpr size_t LDS = (size_t)HP * HP * CINP * 2 + 4 * 2 * 64 * 4;
+  static constexpr size_t XB = (size_t)HP * HP * CINP * 2;
+  static constexpr size_t LDS = XB + 4 * 2 * 64 * 4 + 2 * 64 * 4;
 };
 
 template <int CIN, int COUT, int HIN, int S>
@@ -72,7 +136,8 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
   constexpr int CINP = F::CINP, HP = F::HP, HOUT = F::HOUT, KP = F::KP;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* xs = reinterpret_cast<bf16*>(smem);
-  float* red = reinterpret_cast<float*>(xs + HP * HP * CINP);    // [4][2][64]
+  float* red = reinterpret_cast<float*>(smem + F::XB);          // [4][2][64]
+  float* cf = red + 4 * 2 * 64;                                  // [2][64] BN scale / shift of layer l-1
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
 
   // ---- prologue: padded input image (stem: dataset gather; else BN-apply of layer l-1) ----
@@ -83,34 +148,22 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
     for (int i = 0; i < F::IT; ++i) {
       const int e = min(tid + i * RT, F::NCH - 1);
       const int iy = e / HP - F::PADB, ix = e % HP - F::PADB;
-      const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
-      const uint8_t* s = img + (ok ? ((a.cy + iy) * 32 + a.cx + ix) * 3 : 0);
-      const uint32_t v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
-      px3[i] = ok ? v : 0u;
+      px3[i] = load_px_u8(img, a.cy, a.cx, iy, ix, iy >= 0 && iy < HIN && ix >= 0 && ix < HIN);
     }
 #pragma unroll
     for (int i = 0; i < F::IT; ++i) {
       const int e = tid + i * RT;
-      if (e < F::NCH) {
-        const uint32_t v = px3[i];
-        uint4 o;
-        o.x = pack2((float)(v & 0xff), (float)((v >> 8) & 0xff));
-        o.y = pack2((float)((v >> 16) & 0xff), 0.f);
-        o.z = 0; o.w = 0;
-        reinterpret_cast<uint4*>(xs)[e] = o;
-      }
+      if (e < F::NCH) reinterpret_cast<uint4*>(xs)[e] = px_u8_to_bf16x8(px3[i]);
     }
   } else {
     constexpr int C8 = CIN / 8;
     const int c8 = tid % C8;                  // fixed channel chunk of this thread (RT % C8 == 0)
-    float sc[8], sh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    if (tid < CIN) {                          // BN_{l-1} coefficients, once per block
       float mean, rstd;
-      const int c = c8 * 8 + j;
-      bn_stats(a.stat_prev, c, a.inv_n_prev, mean, rstd);
-      sc[j] = a.gamma_prev[c] * rstd;
-      sh[j] = a.beta_prev[c] - mean * sc[j];
+      bn_mean_rstd(a.stat_prev, tid, a.inv_n_prev, mean, rstd);
+      const float sc = a.gamma_prev[tid] * rstd;
+      cf[tid] = sc;
+      cf[64 + tid] = a.beta_prev[tid] - mean * sc;
     }
     const uint4* zp = reinterpret_cast<const uint4*>(a.z_prev) + (size_t)b * HIN * HIN * C8;
     const uint4* ss = reinterpret_cast<const uint4*>(a.sc_src);
@@ -131,6 +184,10 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
         sv[i] = lowc ? v : make_uint4(0, 0, 0, 0);
       }
     }
+    lds_barrier();
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = cf[c8 * 8 + j]; sh[j] = cf[64 + c8 * 8 + j]; }
     uint4* ao = reinterpret_cast<uint4*>(a.a_out) + (size_t)b * HIN * HIN * C8;
 #pragma unroll
     for (int i = 0; i < F::IT; ++i) {
@@ -189,38 +246,7 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s1[r] += acc[i][r]; s2[r] += acc[i][r] * acc[i][r]; }
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) { s1[r] += __shfl_xor(s1[r], o); s2[r] += __shfl_xor(s2[r], o); }
-  if (li == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      red[(w * 2 + 0) * 64 + 16 * ct + 4 * g + r] = s1[r];
-      red[(w * 2 + 1) * 64 + 16 * ct + 4 * g + r] = s2[r];
-    }
-  }
-  __syncthreads();
-  if (tid < COUT) {
-    float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww)
-      if (ww % F::CT == tid / 16) { t1 += red[(ww * 2) * 64 + tid]; t2 += red[(ww * 2 + 1) * 64 + tid]; }
-    atomicAdd(a.stat + tid, (double)t1);
-    atomicAdd(a.stat + 64 + tid, (double)t2);
-  }
-}
-
-// ================================ BN backward coefficients ====================================
-// g_z = A*g_y + Bc*z + Cc  with  A = gamma*rstd, Bc = -gamma*rstd^2*R2/N, Cc = -A*R1/N - Bc*mean
-DEV void bnb_coeffs(const double* stat, const double* red, const float* gamma, int c, float inv_n, float& A,
-                    float& Bc, float& Cc) {
-  float mean, rstd;
-  bn_stats(stat, c, inv_n, mean, rstd);
-  const float r1 = (float)(red[c] * (double)inv_n), r2 = (float)(red[64 + c] * (double)inv_n);
-  A = gamma[c] * rstd;
-  Bc = -A * rstd * r2;
-  Cc = -A * r1 - Bc * mean;
+  reduce_flush<F::CT, COUT>(s1, s2, red, a.stat, w, g, li, tid);
 }
 
 // ================================ dgrad ========================================================
@@ -232,7 +258,8 @@ struct Dg {
   static constexpr int CT = CIN / 16, WPC = 4 / CT, NPXT = HIN * HIN / 16, NPT = NPXT / WPC;
   static constexpr int NCH = HPD * HPD * COUT / 8;
   static constexpr int IT = (NCH + RT - 1) / RT;
-  static constexpr size_t LDS = (size_t)HPD * HPD * COUT * 2 + 4 * 2 * 64 * 4;
+  static constexpr size_t GB = (size_t)HPD * HPD * COUT * 2;
+  static constexpr size_t LDS = GB + 4 * 2 * 64 * 4 + 5 * 64 * 4;
 };
 
 template <int CIN, int COUT, int HIN, int S>
@@ -241,15 +268,22 @@ __global__ __launch_bounds__(RT) void k_rn_dgrad(DmlcRnDgradArgs a) {
   constexpr int HOUT = D::HOUT, HPD = D::HPD, KPD = D::KPD, C8 = COUT / 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* gs = reinterpret_cast<bf16*>(smem);
-  float* red = reinterpret_cast<float*>(gs + HPD * HPD * COUT);  // [4][2][64]
+  float* red = reinterpret_cast<float*>(smem + D::GB);           // [4][2][64]
+  float* cf = red + 4 * 2 * 64;                                   // [5][64]: A, Bc, Cc (layer l); mean, rstd (l-1)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
 
+  if (tid < COUT) {
+    float A, Bc, Cc;
+    bnb_coeffs(a.stat, a.red, a.gamma, tid, a.inv_n, A, Bc, Cc);
+    cf[tid] = A; cf[64 + tid] = Bc; cf[128 + tid] = Cc;
+  } else if (tid >= 128 && tid < 128 + CIN) {
+    float mean, rstd;
+    bn_mean_rstd(a.stat_prev, tid - 128, a.inv_n_prev, mean, rstd);
+    cf[192 + tid - 128] = mean; cf[256 + tid - 128] = rstd;
+  }
   // ---- prologue: g_z of layer l on the (zero-inserted for S = 2) padded grid ----
   {
     const int c8 = tid % C8;
-    float A[8], Bc[8], Cc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bnb_coeffs(a.stat, a.red, a.gamma, c8 * 8 + j, a.inv_n, A[j], Bc[j], Cc[j]);
     const uint4* gyp = reinterpret_cast<const uint4*>(a.gy) + (size_t)b * HOUT * HOUT * C8;
     const uint4* zp = reinterpret_cast<const uint4*>(a.z) + (size_t)b * HOUT * HOUT * C8;
     uint4 gv[D::IT], zv[D::IT];
@@ -270,6 +304,10 @@ __global__ __launch_bounds__(RT) void k_rn_dgrad(DmlcRnDgradArgs a) {
       zv[i] = zp[q];
       okv[i] = ok && (tid + i * RT) < D::NCH;
     }
+    lds_barrier();
+    float A[8], Bc[8], Cc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { A[j] = cf[c8 * 8 + j]; Bc[j] = cf[64 + c8 * 8 + j]; Cc[j] = cf[128 + c8 * 8 + j]; }
 #pragma unroll
     for (int i = 0; i < D::IT; ++i) {
       const int e = tid + i * RT;
@@ -313,20 +351,18 @@ __global__ __launch_bounds__(RT) void k_rn_dgrad(DmlcRnDgradArgs a) {
   }
 
   // ---- epilogue: g_a_{l-1} (+ shortcut) -> g_y_{l-1} + its BN reductions ----
-  constexpr int CI8 = CIN / 8;
+  const int c0 = 16 * ct + 4 * g;
   float mean[4], rstd[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) bn_stats(a.stat_prev, 16 * ct + 4 * g + r, a.inv_n_prev, mean[r], rstd[r]);
+  for (int r = 0; r < 4; ++r) { mean[r] = cf[192 + c0 + r]; rstd[r] = cf[256 + c0 + r]; }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   const bf16* ap = reinterpret_cast<const bf16*>(a.a_prev) + (size_t)b * HIN * HIN * CIN;
   const bf16* zpp = reinterpret_cast<const bf16*>(a.z_prev) + (size_t)b * HIN * HIN * CIN;
   bf16* gyo = reinterpret_cast<bf16*>(a.gy_prev) + (size_t)b * HIN * HIN * CIN;
-  (void)CI8;
 #pragma unroll
   for (int i = 0; i < D::NPT; ++i) {
     const int px = 16 * (pt0 + D::WPC * i) + li;
     const int iy = px / HIN, ix = px - (px / HIN) * HIN;
-    const int c0 = 16 * ct + 4 * g;
     const uint2 av = *reinterpret_cast<const uint2*>(ap + px * CIN + c0);
     const uint2 zv = *reinterpret_cast<const uint2*>(zpp + px * CIN + c0);
     float sc4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -352,29 +388,12 @@ __global__ __launch_bounds__(RT) void k_rn_dgrad(DmlcRnDgradArgs a) {
     }
     *reinterpret_cast<bf16x4*>(gyo + px * CIN + c0) = pack4(gy[0], gy[1], gy[2], gy[3]);
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) { s1[r] += __shfl_xor(s1[r], o); s2[r] += __shfl_xor(s2[r], o); }
-  if (li == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      red[(w * 2 + 0) * 64 + 16 * ct + 4 * g + r] = s1[r];
-      red[(w * 2 + 1) * 64 + 16 * ct + 4 * g + r] = s2[r];
-    }
-  }
-  __syncthreads();
-  if (tid < CIN) {
-    float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww)
-      if (ww % D::CT == tid / 16) { t1 += red[(ww * 2) * 64 + tid]; t2 += red[(ww * 2 + 1) * 64 + tid]; }
-    atomicAdd(a.red_prev + tid, (double)t1);
-    atomicAdd(a.red_prev + 64 + tid, (double)t2);
-  }
+  reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid);
 }
 
 // ================================ wgrad ========================================================
+// Block (grp, mc): images [grp*B/G, (grp+1)*B/G), slab rows of m-tiles [mc*MCH, (mc+1)*MCH); NB images are
+// staged per barrier (LDS budget ~120 KB) so their global loads are all in flight together.
 template <int CIN, int COUT, int HIN, int S>
 struct Wg {
   static constexpr int CINP = CIN < 8 ? 8 : CIN;
@@ -382,125 +401,138 @@ struct Wg {
   static constexpr int PADB = S == 1 ? 1 : 0;
   static constexpr int HP = HIN + (S == 1 ? 2 : 1);
   static constexpr int KP = round32(9 * CINP);
-  static constexpr int MT = KP / 16, MCH = 16, MC = (MT + MCH - 1) / MCH;
+  static constexpr int MT = KP / 16;
+  static constexpr int MC = MT <= 12 ? 1 : (MT <= 24 ? 2 : 3);           // m-chunks (grid.y)
+  static constexpr int MCH = (MT + MC - 1) / MC;
+  static constexpr int MJ = (MCH + 3) / 4;                               // m-tiles per wave
   static constexpr int NT = COUT / 16;
   static constexpr int NPIX = HOUT * HOUT, KSTEPS = NPIX / 32;
-  static constexpr int GLD = COUT + 8;                            // g_z LDS row stride (bf16)
-  static constexpr int XCH = HP * HP * CINP / 8, XIT = (XCH + RT - 1) / RT;
-  static constexpr int GCH = NPIX * COUT / 8, GIT = (GCH + RT - 1) / RT;
-  static constexpr size_t LDS = (size_t)HP * HP * CINP * 2 + (size_t)NPIX * GLD * 2;
+  static constexpr int GLD = COUT + 8;                                   // g_z LDS row stride (bf16)
+  static constexpr int XE = HP * HP * CINP, GE = NPIX * GLD;            // bf16 elements per image
+  static constexpr int XCH = XE / 8, GCH = NPIX * COUT / 8;             // 16-B chunks per image
+  static constexpr int PER_IMG = (XE + GE) * 2;
+  static constexpr int NB = (120 * 1024 / PER_IMG) < 1 ? 1 : ((120 * 1024 / PER_IMG) > 4 ? 4 : 120 * 1024 / PER_IMG);
+  static constexpr int XIT = (NB * XCH + RT - 1) / RT, GIT = (NB * GCH + RT - 1) / RT;
+  static constexpr size_t LDS = (size_t)NB * PER_IMG + 3 * 64 * 4;
 };
 
 template <int CIN, int COUT, int HIN, int S>
 __global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
   using G = Wg<CIN, COUT, HIN, S>;
-  constexpr int CINP = G::CINP, HP = G::HP, HOUT = G::HOUT, KP = G::KP, NT = G::NT, GLD = G::GLD;
+  constexpr int CINP = G::CINP, HP = G::HP, HOUT = G::HOUT, KP = G::KP, NT = G::NT, GLD = G::GLD, NB = G::NB;
   constexpr int C8 = COUT / 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* xs = reinterpret_cast<bf16*>(smem);
-  bf16* gz = xs + HP * HP * CINP;
+  bf16* xs = reinterpret_cast<bf16*>(smem);                       // [NB][XE]
+  bf16* gz = xs + NB * G::XE;                                     // [NB][GE]
+  float* cf = reinterpret_cast<float*>(gz + NB * G::GE);          // [3][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int grp = blockIdx.x, mc = blockIdx.y;
   const int b0 = grp * a.B / a.G, b1 = (grp + 1) * a.B / a.G;
 
-  float A[8], Bc[8], Cc[8];
-  const int c8 = tid % C8;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bnb_coeffs(a.stat, a.red, a.gamma, c8 * 8 + j, a.inv_n, A[j], Bc[j], Cc[j]);
+  if (tid < COUT) {
+    float A, Bc, Cc;
+    bnb_coeffs(a.stat, a.red, a.gamma, tid, a.inv_n, A, Bc, Cc);
+    cf[tid] = A; cf[64 + tid] = Bc; cf[128 + tid] = Cc;
+  }
+  const int c8 = tid % C8;                                        // RT % (C8) == 0 and GCH % C8 == 0
 
-  f32x4 acc[4][NT];
+  f32x4 acc[G::MJ][NT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < G::MJ; ++j)
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[j][n] = zero4();
 
-  for (int b = b0; b < b1; ++b) {
+  for (int bb = b0; bb < b1; bb += NB) {
+    const int nb = min(NB, b1 - bb);
     __syncthreads();
-    // x image (padded)
+    // ---- x images (padded) ----
     if constexpr (CIN == 3) {
-      const uint8_t* img = a.data + (size_t)batch_index(a.src, a.B, b) * 3072;
       uint32_t px3[G::XIT];
 #pragma unroll
       for (int i = 0; i < G::XIT; ++i) {
-        const int e = min(tid + i * RT, G::XCH - 1);
-        const int iy = e / HP - G::PADB, ix = e % HP - G::PADB;
-        const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
-        const uint8_t* s = img + (ok ? ((a.cy + iy) * 32 + a.cx + ix) * 3 : 0);
-        const uint32_t v = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
-        px3[i] = ok ? v : 0u;
+        const int e = min(tid + i * RT, NB * G::XCH - 1);
+        const int im = min(e / G::XCH, nb - 1), e1 = e - (e / G::XCH) * G::XCH;
+        const uint8_t* img = a.data + (size_t)batch_index(a.src, a.B, bb + im) * 3072;
+        const int iy = e1 / HP - G::PADB, ix = e1 % HP - G::PADB;
+        px3[i] = load_px_u8(img, a.cy, a.cx, iy, ix, iy >= 0 && iy < HIN && ix >= 0 && ix < HIN);
       }
 #pragma unroll
       for (int i = 0; i < G::XIT; ++i) {
         const int e = tid + i * RT;
-        if (e < G::XCH) {
-          const uint32_t v = px3[i];
-          reinterpret_cast<uint4*>(xs)[e] = make_uint4(pack2((float)(v & 0xff), (float)((v >> 8) & 0xff)),
-                                                       pack2((float)((v >> 16) & 0xff), 0.f), 0u, 0u);
-        }
+        if (e < NB * G::XCH) reinterpret_cast<uint4*>(xs)[e] = px_u8_to_bf16x8(px3[i]);
       }
     } else {
       constexpr int X8 = CIN / 8;
-      const uint4* xp = reinterpret_cast<const uint4*>(a.x) + (size_t)b * HIN * HIN * X8;
       uint4 xv[G::XIT];
 #pragma unroll
       for (int i = 0; i < G::XIT; ++i) {
-        const int e = min(tid + i * RT, G::XCH - 1);
-        const int pp = e / X8, iy = pp / HP - G::PADB, ix = pp % HP - G::PADB;
+        const int e = min(tid + i * RT, NB * G::XCH - 1);
+        const int im = min(e / G::XCH, nb - 1), e1 = e - (e / G::XCH) * G::XCH;
+        const uint4* xp = reinterpret_cast<const uint4*>(a.x) + (size_t)(bb + im) * HIN * HIN * X8;
+        const int pp = e1 / X8, iy = pp / HP - G::PADB, ix = pp % HP - G::PADB;
         const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
-        xv[i] = load_sel(xp + (iy * HIN + ix) * X8 + e % X8, xp, ok);
+        xv[i] = load_sel(xp + (ok ? (iy * HIN + ix) * X8 + e1 % X8 : 0), xp, ok);
       }
 #pragma unroll
       for (int i = 0; i < G::XIT; ++i) {
         const int e = tid + i * RT;
-        if (e < G::XCH) reinterpret_cast<uint4*>(xs)[e] = xv[i];
+        if (e < NB * G::XCH) reinterpret_cast<uint4*>(xs)[e] = xv[i];
       }
     }
-    // g_z image [NPIX][GLD]
+    // ---- g_z images [NB][NPIX][GLD] ----
     {
-      const uint4* gyp = reinterpret_cast<const uint4*>(a.gy) + (size_t)b * G::NPIX * C8;
-      const uint4* zp = reinterpret_cast<const uint4*>(a.z) + (size_t)b * G::NPIX * C8;
       uint4 gv[G::GIT], zv[G::GIT];
 #pragma unroll
       for (int i = 0; i < G::GIT; ++i) {
-        const int e = min(tid + i * RT, G::GCH - 1);
-        gv[i] = gyp[e];
-        zv[i] = zp[e];
+        const int e = min(tid + i * RT, NB * G::GCH - 1);
+        const int im = min(e / G::GCH, nb - 1), e1 = e - (e / G::GCH) * G::GCH;
+        const size_t off = (size_t)(bb + im) * G::GCH + e1;
+        gv[i] = reinterpret_cast<const uint4*>(a.gy)[off];
+        zv[i] = reinterpret_cast<const uint4*>(a.z)[off];
       }
+      float A[8], Bc[8], Cc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { A[j] = cf[c8 * 8 + j]; Bc[j] = cf[64 + c8 * 8 + j]; Cc[j] = cf[128 + c8 * 8 + j]; }
 #pragma unroll
       for (int i = 0; i < G::GIT; ++i) {
         const int e = tid + i * RT;
-        if (e < G::GCH) {
+        if (e < NB * G::GCH) {
+          const int im = e / G::GCH, e1 = e - im * G::GCH;
           const uint32_t gw[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w}, zw[4] = {zv[i].x, zv[i].y, zv[i].z, zv[i].w};
           uint32_t ow[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k)
             ow[k] = pack2(A[2 * k] * bf16_lo(gw[k]) + Bc[2 * k] * bf16_lo(zw[k]) + Cc[2 * k],
                           A[2 * k + 1] * bf16_hi(gw[k]) + Bc[2 * k + 1] * bf16_hi(zw[k]) + Cc[2 * k + 1]);
-          *reinterpret_cast<uint4*>(gz + (e / C8) * GLD + (e % C8) * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+          *reinterpret_cast<uint4*>(gz + im * G::GE + (e1 / C8) * GLD + (e1 % C8) * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         }
       }
     }
     __syncthreads();
-    // MFMA over this image's pixels
-    for (int s = 0; s < G::KSTEPS; ++s) {
-      const int rA = 32 * s + 8 * g + q, rB = rA + 4;
-      bf16x8 bf[NT];
+    // ---- MFMA over the staged images' pixels ----
+    for (int im = 0; im < nb; ++im) {
+      const bf16* xi = xs + im * G::XE;
+      const bf16* gi = gz + im * G::GE;
+      for (int s = 0; s < G::KSTEPS; ++s) {
+        const int rA = 32 * s + 8 * g + q, rB = rA + 4;
+        bf16x8 bf[NT];
 #pragma unroll
-      for (int n = 0; n < NT; ++n) bf[n] = tr_frag(gz + rA * GLD + 16 * n + 4 * p, gz + rB * GLD + 16 * n + 4 * p);
-      const int oyA = rA / HOUT, oxA = rA - oyA * HOUT, oyB = rB / HOUT, oxB = rB - oyB * HOUT;
-      const int pA = (oyA * S) * HP + oxA * S, pB = (oyB * S) * HP + oxB * S;
+        for (int n = 0; n < NT; ++n) bf[n] = tr_frag(gi + rA * GLD + 16 * n + 4 * p, gi + rB * GLD + 16 * n + 4 * p);
+        const int oyA = rA / HOUT, oxA = rA - oyA * HOUT, oyB = rB / HOUT, oxB = rB - oyB * HOUT;
+        const int pA = (oyA * S) * HP + oxA * S, pB = (oyB * S) * HP + oxB * S;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int m = mc * G::MCH + w + 4 * j;
-        if (m < G::MT) {
-          int tap, ci0;
-          if (CINP >= 16) { tap = (16 * m) / CINP; ci0 = (16 * m) % CINP + 4 * p; }
-          else { tap = 2 * m + (p >> 1); ci0 = 4 * (p & 1); }
-          tap = min(tap, 8);
-          const int kh = tap / 3, kw = tap - 3 * (tap / 3), off = kh * HP + kw;
-          const bf16x8 af = tr_frag(xs + (pA + off) * CINP + ci0, xs + (pB + off) * CINP + ci0);
+        for (int j = 0; j < G::MJ; ++j) {
+          const int m = mc * G::MCH + w + 4 * j;
+          if (w + 4 * j < G::MCH && m < G::MT) {
+            int tap, ci0;
+            if (CINP >= 16) { tap = (16 * m) / CINP; ci0 = (16 * m) % CINP + 4 * p; }
+            else { tap = 2 * m + (p >> 1); ci0 = 4 * (p & 1); }
+            tap = min(tap, 8);
+            const int kh = tap / 3, kw = tap - 3 * (tap / 3), off = kh * HP + kw;
+            const bf16x8 af = tr_frag(xi + (pA + off) * CINP + ci0, xi + (pB + off) * CINP + ci0);
 #pragma unroll
-          for (int n = 0; n < NT; ++n) acc[j][n] = mfma16(af, bf[n], acc[j][n]);
+            for (int n = 0; n < NT; ++n) acc[j][n] = mfma16(af, bf[n], acc[j][n]);
+          }
         }
       }
     }
@@ -508,9 +540,9 @@ __global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
   // slab rows k = 16m + 4g + i, cols co = 16n + li
   float* out = a.part + (size_t)grp * KP * COUT;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < G::MJ; ++j) {
     const int m = mc * G::MCH + w + 4 * j;
-    if (m < G::MT) {
+    if (w + 4 * j < G::MCH && m < G::MT) {
 #pragma unroll
       for (int n = 0; n < NT; ++n)
 #pragma unroll
@@ -523,27 +555,37 @@ __global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
 // per image: a18 = relu(bn(z18) + x_in) -> mean pool -> fc 64x10 -> softmax-xent -> backward to g_y18
 __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   __shared__ float pool_part[4][64];
-  __shared__ float pooled[64], dlog[16], gpool[64];
+  __shared__ float pooled[64], dlog[16], gpool[64], cf[2][64];
   __shared__ float redl[2][4][64];
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c = lane;                           // thread -> channel c, pixels w, w+4, ... (16 each)
-  float mean, rstd;
-  bn_stats(a.stat, c, a.inv_n, mean, rstd);
-  const float sc = a.gamma[c] * rstd, sh = a.beta[c] - mean * sc;
+  if (tid < 64) {
+    float mean, rstd;
+    bn_mean_rstd(a.stat, tid, a.inv_n, mean, rstd);
+    cf[0][tid] = mean; cf[1][tid] = rstd;
+  }
   const bf16* zp = reinterpret_cast<const bf16*>(a.z) + (size_t)b * 4096;
   const bf16* sp = reinterpret_cast<const bf16*>(a.sc) + (size_t)b * 4096;
-  float av[16], zv[16];
-  float s = 0.f;
+  float zv[16], sv[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int px = w + 4 * k;
     zv[k] = (float)zp[px * 64 + c];
-    av[k] = fmaxf(zv[k] * sc + sh + (float)sp[px * 64 + c], 0.f);
+    sv[k] = (float)sp[px * 64 + c];
+  }
+  int label = 0;
+  if (tid == 0) label = a.labels[batch_index(a.src, a.B, b)];
+  __syncthreads();
+  const float mean = cf[0][c], rstd = cf[1][c];
+  const float sc = a.gamma[c] * rstd, sh = a.beta[c] - mean * sc;
+  float av[16];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    av[k] = fmaxf(zv[k] * sc + sh + sv[k], 0.f);
     s += av[k];
   }
   pool_part[w][c] = s;
-  int label = 0;
-  if (tid == 0) label = a.labels[batch_index(a.src, a.B, b)];
   __syncthreads();
   if (tid < 64) pooled[tid] = (pool_part[0][tid] + pool_part[1][tid] + pool_part[2][tid] + pool_part[3][tid]) * (1.f / 64.f);
   __syncthreads();
@@ -562,8 +604,7 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
     const int lab = __shfl(label, 0);
-    // argmax (first max) for accuracy
-    int am = lane < 10 && lg == m ? lane : 64;
+    int am = lane < 10 && lg == m ? lane : 64;  // first maximum (accuracy)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o));
     const float lse = m + __logf(se);
@@ -601,56 +642,65 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   redl[1][w][c] = r2;
   __syncthreads();
   if (tid < 64) {
-    atomicAdd(a.red + tid, (double)(redl[0][0][tid] + redl[0][1][tid] + redl[0][2][tid] + redl[0][3][tid]));
-    atomicAdd(a.red + 64 + tid, (double)(redl[1][0][tid] + redl[1][1][tid] + redl[1][2][tid] + redl[1][3][tid]));
+    double* d = a.red + (b & (NSLOT - 1)) * 128;
+    RN_ATOMIC_ADD(d + tid, (double)(redl[0][0][tid] + redl[0][1][tid] + redl[0][2][tid] + redl[0][3][tid]));
+    RN_ATOMIC_ADD(d + 64 + tid, (double)(redl[1][0][tid] + redl[1][1][tid] + redl[1][2][tid] + redl[1][3][tid]));
   }
 }
 
 // ================================ SGD ==========================================================
 DEV float4 add4r(float4 x, float4 y) { return make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w); }
 
-// 64 float4 outputs per block, 4 splits over the slabs (fixed order)
-DEV float4 split4_sum(const float* p, size_t stride, int n, float4* lds) {
-  const int sp = threadIdx.x >> 6, idx = threadIdx.x & 63;
+// thread (sp = tid / O, idx = tid % O) sums slabs q = sp, sp+S, ...; the block folds the S splits
+// in fixed order -> threads tid < O return the total of output idx (deterministic)
+DEV float4 split_reduce(const float* p, size_t stride, int n, int S, float4* lds) {
+  const int O = RT / S, sp = threadIdx.x / O, idx = threadIdx.x - sp * O;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   int q = sp;
-  for (; q + 28 < n; q += 32) {
+  for (; q + 7 * S < n; q += 8 * S) {
     float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + (size_t)(q + 4 * u) * stride);
+    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + (size_t)(q + u * S) * stride);
 #pragma unroll
     for (int u = 0; u < 8; ++u) s = add4r(s, v[u]);
   }
-  for (; q < n; q += 4) s = add4r(s, *reinterpret_cast<const float4*>(p + (size_t)q * stride));
+  for (; q < n; q += S) s = add4r(s, *reinterpret_cast<const float4*>(p + (size_t)q * stride));
   lds[threadIdx.x] = s;
   __syncthreads();
-  return add4r(add4r(lds[idx], lds[64 + idx]), add4r(lds[128 + idx], lds[192 + idx]));
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (threadIdx.x < O)
+    for (int k = 0; k < S; ++k) t = add4r(t, lds[k * O + idx]);
+  return t;
 }
 
 // modes: 0 reduce slabs + apply (1 GPU); 1 reduce slabs into `grad` (DP, before the all-reduce);
 //        2 apply grad_scale * `grad` (DP, after it); 3 refresh the bf16 shadows from the master only
-__global__ __launch_bounds__(256) void k_rn_sgd(DmlcRnSgdArgs a) {
-  __shared__ float4 lds[256];
+// blocks: [conv layer 0..18 | fc | BN layer 0..18]
+__global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
+  __shared__ float4 lds[RT];
+  __shared__ float lred[2][4];
   const int64_t step = *a.step;
   const float lr = a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
   const int mode = a.mode;
   const bool reduce = mode <= 1, apply = mode == 0 || mode == 2;
   const int blk = blockIdx.x, tid = threadIdx.x;
+  constexpr int NL = DMLC_RN_LAYERS;
   int l = 0;
-  while (l <= DMLC_RN_LAYERS && blk >= a.blk_start[l + 1]) ++l;
-  if (l < DMLC_RN_LAYERS) {
+  while (l < NL + 1 && blk >= a.blk_start[l + 1]) ++l;
+  if (l < NL) {                                  // conv layer l
+    const int S = a.split[l], O = RT / S;
     const int cin = a.cin[l], cout = a.cout[l], cinp = cin < 8 ? 8 : cin;
     const int kp = (9 * cinp + 31) / 32 * 32, kpd = (9 * cout + 31) / 32 * 32;
     const int n4 = 9 * cin * cout / 4, co4n = cout / 4;
-    const int o4 = (blk - a.blk_start[l]) * 64 + (tid & 63);
+    const int o4 = (blk - a.blk_start[l]) * O + tid % O;
     const bool valid = o4 < n4;
     const int oc = valid ? o4 : 0;
     const int row = oc / co4n, co = (oc - row * co4n) * 4;          // HWIO row = tap*cin + ci
     const int tap = row / cin, ci = row - tap * cin, k = tap * cinp + ci;
     const size_t off = (size_t)a.conv_off[l] + (size_t)row * cout + co;
     float4 gsum = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (reduce) gsum = split4_sum(a.part[l] + (size_t)k * cout + co, (size_t)kp * cout, a.G[l], lds);
-    if (tid < 64 && valid) {
+    if (reduce) gsum = split_reduce(a.part[l] + (size_t)k * cout + co, (size_t)kp * cout, a.G[l], S, lds);
+    if (tid < O && valid) {
       if (mode == 1) {
         *reinterpret_cast<float4*>(a.grad + off) = gsum;
       } else {
@@ -672,12 +722,13 @@ __global__ __launch_bounds__(256) void k_rn_sgd(DmlcRnSgdArgs a) {
               pack4(wv.x, wv.y, wv.z, wv.w);
       }
     }
-  } else if (l == DMLC_RN_LAYERS) {              // fc: 164 float4 of [640 dW | 10 db | pad], 4 splits over images
-    const int o4 = (blk - a.blk_start[l]) * 64 + (tid & 63);
+  } else if (l == NL) {                          // fc: 164 float4 of [640 dW | 10 db | pad], split over images
+    const int S = a.split[NL], O = RT / S;
+    const int o4 = (blk - a.blk_start[l]) * O + tid % O;
     const bool valid = o4 < 164;
     float4 gsum = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (reduce) gsum = split4_sum(a.fc_part + 4 * (valid ? o4 : 0), 656, a.B, lds);
-    if (tid < 64 && valid && mode != 3) {
+    if (reduce) gsum = split_reduce(a.fc_part + 4 * (valid ? o4 : 0), 656, a.B, S, lds);
+    if (tid < O && valid && mode != 3) {
       const float gv[4] = {gsum.x, gsum.y, gsum.z, gsum.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -689,23 +740,24 @@ __global__ __launch_bounds__(256) void k_rn_sgd(DmlcRnSgdArgs a) {
         }
       }
     }
-  } else if (mode != 3) {                        // BN gamma/beta + running statistics (one block)
-    for (int e = tid; e < DMLC_RN_LAYERS * 64; e += 256) {
-      const int L = e / 64, c = e % 64;
-      if (c < a.cout[L]) {
-        const double* st = a.stat + L * 128;
-        const double* rd = a.red + L * 128;
-        const size_t og = (size_t)a.gamma_off[L] + c, ob = (size_t)a.beta_off[L] + c;
-        if (mode == 1) {
-          a.grad[og] = (float)rd[64 + c];
-          a.grad[ob] = (float)rd[c];
-          continue;
-        }
-        a.master[og] -= lr * (mode == 2 ? a.grad[og] * a.grad_scale : (float)rd[64 + c]);
-        a.master[ob] -= lr * (mode == 2 ? a.grad[ob] * a.grad_scale : (float)rd[c]);
+  } else if (mode != 3) {                        // BN layer L: gamma/beta + running statistics
+    const int L = blk - a.blk_start[NL + 1];
+    const int c = tid;
+    if (c < a.cout[L]) {
+      const size_t og = (size_t)a.gamma_off[L] + c, ob = (size_t)a.beta_off[L] + c;
+      double r1, r2;
+      slot_sums(a.red + (size_t)L * NSLOT * 128, c, r1, r2);
+      if (mode == 1) {
+        a.grad[og] = (float)r2;
+        a.grad[ob] = (float)r1;
+      } else {
+        a.master[og] -= lr * (mode == 2 ? a.grad[og] * a.grad_scale : (float)r2);
+        a.master[ob] -= lr * (mode == 2 ? a.grad[ob] * a.grad_scale : (float)r1);
+        double s1, s2;
+        slot_sums(a.stat + (size_t)L * NSLOT * 128, c, s1, s2);
         const double inv = (double)a.inv_n[L];
-        const double mean = st[c] * inv;
-        double var = st[64 + c] * inv - mean * mean;
+        const double mean = s1 * inv;
+        double var = s2 * inv - mean * mean;
         var = var > 0.0 ? var : 0.0;
         const double nn = 1.0 / inv;
         const float m = a.bn_momentum;
@@ -715,20 +767,28 @@ __global__ __launch_bounds__(256) void k_rn_sgd(DmlcRnSgdArgs a) {
         *mv = (1.f - m) * *mv + m * (float)(var * nn / (nn - 1.0));
       }
     }
+    if (L == 0 && apply) {                       // batch loss / accuracy -> stats ring (fields 1, 2)
+      float ls = 0.f, cs = 0.f;
+      for (int q = tid; q < a.B; q += RT) { ls += a.loss_img[q]; cs += (float)a.correct_img[q]; }
+      ls = wave_sum(ls);
+      cs = wave_sum(cs);
+      if ((tid & 63) == 0) { lred[0][tid >> 6] = ls; lred[1][tid >> 6] = cs; }
+      __syncthreads();
+      if (tid == 0) {
+        float* st = a.stats + (size_t)(step % a.stats_len) * 4;
+        st[1] = (lred[0][0] + lred[0][1] + lred[0][2] + lred[0][3]) / (float)a.B;
+        st[2] = (lred[1][0] + lred[1][1] + lred[1][2] + lred[1][3]) / (float)a.B;
+      }
+    }
   }
   if (!apply) return;
   __syncthreads();
   if (tid == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == (unsigned)gridDim.x - 1) {
-      float loss = 0.f;
-      int corr = 0;
-      for (int q = 0; q < a.B; ++q) { loss += a.loss_img[q]; corr += a.correct_img[q]; }
+    if (t == (unsigned)gridDim.x - 1) {          // last block: publish the step
       float* st = a.stats + (size_t)(step % a.stats_len) * 4;
       st[0] = (float)(step + 1);
-      st[1] = loss / (float)a.B;
-      st[2] = (float)corr / (float)a.B;
       st[3] = lr;
       *a.step = step + 1;
       __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -822,17 +882,27 @@ hipError_t dmlc_rn_head(const DmlcRnHeadArgs* a, hipStream_t s) {
   return hipGetLastError();
 }
 
+static int split_for(int n) {                 // slabs per thread <= 8
+  int S = 4;
+  while (S < 64 && S * 8 < n) S <<= 1;
+  return S;
+}
+
 hipError_t dmlc_rn_sgd(DmlcRnSgdArgs* a, hipStream_t s) {
   int blocks = 0;
   for (int l = 0; l < DMLC_RN_LAYERS; ++l) {
+    a->split[l] = split_for(a->G[l]);
     a->blk_start[l] = blocks;
-    blocks += (9 * a->cin[l] * a->cout[l] / 4 + 63) / 64;
+    const int O = RT / a->split[l];
+    blocks += (9 * a->cin[l] * a->cout[l] / 4 + O - 1) / O;
   }
-  a->blk_start[DMLC_RN_LAYERS] = blocks;          // fc: 3 blocks
-  blocks += 3;
-  a->blk_start[DMLC_RN_LAYERS + 1] = blocks;      // BN parameters + running statistics: 1 block
-  blocks += 1;
-  hipLaunchKernelGGL(k_rn_sgd, dim3(blocks), dim3(256), 0, s, *a);
+  a->split[DMLC_RN_LAYERS] = split_for(a->B);
+  a->blk_start[DMLC_RN_LAYERS] = blocks;                     // fc
+  blocks += (164 + RT / a->split[DMLC_RN_LAYERS] - 1) / (RT / a->split[DMLC_RN_LAYERS]);
+  a->blk_start[DMLC_RN_LAYERS + 1] = blocks;                 // BN, one block per layer
+  blocks += DMLC_RN_LAYERS;
+  a->blk_start[DMLC_RN_LAYERS + 2] = blocks;
+  hipLaunchKernelGGL(k_rn_sgd, dim3(blocks), dim3(RT), 0, s, *a);
   return hipGetLastError();
 }
 

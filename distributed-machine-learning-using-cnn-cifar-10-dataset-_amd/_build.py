@@ -31,7 +31,12 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 # DMLC_TIMING=1 builds a separate diagnostic library with per-phase s_memrealtime stamps
 # (tools/ktiming.py); the default library never contains them.
 TIMING = os.environ.get("DMLC_TIMING") == "1"
-HIP_LIB = os.path.join(LIB_DIR, "libdmlc_hip_timing.so" if TIMING else "libdmlc_hip.so")
+# DMLC_VARIANT="name:-DFLAG ..." builds an experiment library libdmlc_hip_<name>.so with extra hipcc
+# flags (A/B kernel variants on the GPU box without touching the production library)
+_VAR = os.environ.get("DMLC_VARIANT", "")
+VARIANT, VARIANT_FLAGS = (_VAR.split(":", 1)[0], _VAR.split(":", 1)[1].split()) if _VAR else ("", [])
+_SUFFIX = "_timing" if TIMING else (f"_{VARIANT}" if VARIANT else "")
+HIP_LIB = os.path.join(LIB_DIR, f"libdmlc_hip{_SUFFIX}.so")
 RT_LIB = os.path.join(LIB_DIR, "_dmlc_rt" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 
 
@@ -107,8 +112,9 @@ def build(hip: bool = True, rt: bool = True, jobs: int | None = None) -> dict:
         hip_flags = ["-std=c++17", "-O3", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
         if TIMING:   # the stamp buffer is one __device__ symbol shared by every kernel TU
             hip_flags += ["-DDMLC_TIMING", "-fgpu-rdc"]
+        hip_flags += VARIANT_FLAGS
         for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
-            o = os.path.join(OBJ_DIR, os.path.basename(src) + (".timing.o" if TIMING else ".o"))
+            o = os.path.join(OBJ_DIR, os.path.basename(src) + (f"{_SUFFIX.replace('_', '.')}.o" if _SUFFIX else ".o"))
             hip_objs.append(o)
             jobs_list.append((src, headers, o, [hipcc], hip_flags))
         bheaders = headers + glob.glob(os.path.join(CSRC, "bindings", "*.h"))

@@ -55,6 +55,7 @@ def layer_table():
     return layers
 
 
+NSLOT = 8            # DMLC_RN_NSLOT
 LAYERS = layer_table()
 NL = len(LAYERS)
 assert NL == 19
@@ -83,7 +84,7 @@ class FusedResNetEngine:
                  lr: float = C.LEARNING_RATE, lr_decay: float = C.LR_DECAY,
                  decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, world_size: int = 1,
                  rank: int = 0, process_group=None, seed: int = 0, groups: Optional[List[int]] = None,
-                 stats_len: int = 4096, comm_dtype: str = "fp32"):
+                 stats_len: int = 4096, comm_dtype: str = "fp32", wgrad_branch: Optional[bool] = None):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -134,7 +135,8 @@ class FusedResNetEngine:
         self.z = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout, LAYERS)]
         self.gy = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout, LAYERS)]
         self.a = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout[:-1], LAYERS[:-1])]   # a_0 .. a_17
-        self.acc = torch.zeros(2, NL, 128, dtype=torch.float64, device=dev)     # [stat | red] fp64 sums
+        # [stat | red] fp64 sums, NSLOT copies per layer (see csrc/kernels/resnet.hip)
+        self.acc = torch.zeros(2, NL, NSLOT, 128, dtype=torch.float64, device=dev)
         self.stat, self.red = self.acc[0], self.acc[1]
         self.groups = groups or [self._pick_groups(B, ci, co) for _, ci, co, _, _ in LAYERS]
         self.part = [z(g, _kp(ci), co, dt=torch.float32) for g, (_, ci, co, _, _) in zip(self.groups, LAYERS)]
@@ -148,17 +150,27 @@ class FusedResNetEngine:
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.side_stream = torch.cuda.Stream(device=dev)
+        if wgrad_branch is None:
+            import os
+            wgrad_branch = os.environ.get("DMLC_RN_WGRAD_BRANCH", "1") == "1"
+        self.wgrad_branch = wgrad_branch     # wgrads on a second stream / graph branch
         self.host_step = 0
         self.refresh_shadows()
 
     # ------------------------------------------------------------------------------------------
     @staticmethod
     def _pick_groups(B: int, cin: int, cout: int) -> int:
-        """Split-K image groups of one wgrad: about 2.6 MB of fp32 slabs per layer (the SGD kernel
-        reads them back), a power of two in [8, B/2]."""
-        target = 655360 / (_kp(cin) * cout)
-        g = 1 << max(0, int(math.floor(math.log2(max(1.0, target)))))
-        return int(max(1, min(B // 2, max(8, g))))
+        """Split-K image groups of one wgrad (grid = groups x m-chunks): enough blocks to fill the chip
+        (``DMLC_RN_WG_BLOCKS``, default 256) while the fp32 slabs the SGD kernel reads back stay under
+        ``DMLC_RN_SLAB_MB`` (default 8 MB) per layer.  A power of two in [8, B]."""
+        import os
+        blocks = int(os.environ.get("DMLC_RN_WG_BLOCKS", "256"))
+        cap = float(os.environ.get("DMLC_RN_SLAB_MB", "8")) * 2 ** 20
+        mt = _kp(cin) // 16
+        mc = 1 if mt <= 12 else (2 if mt <= 24 else 3)      # Wg<>::MC in resnet.hip
+        lim = min(blocks / mc, cap / (_kp(cin) * cout * 4))
+        g = 1 << max(0, int(math.floor(math.log2(max(1.0, lim)))))
+        return int(max(1, min(B, max(8, g))))
 
     def refresh_shadows(self):
         self._sgd(mode=3)
@@ -210,12 +222,13 @@ class FusedResNetEngine:
     def _backward(self):
         o = self.ops
         main = torch.cuda.current_stream(self.device)
-        side = self.side_stream
+        side = self.side_stream if self.wgrad_branch else main
         for l in range(NL - 1, -1, -1):
             # gy_l and red_l are complete here (head or dgrad_{l+1}): fork wgrad_l onto the side branch
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
+            if side is not main:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
             with torch.cuda.stream(side):
                 self._wgrad(l)
             if l == 0:
@@ -228,7 +241,8 @@ class FusedResNetEngine:
                 gy_sc = self.gy[l + 1]
             o.rn_dgrad(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
                        self.a[p], self.z[p], self.stat[p], gy_sc, sc_mode, self.gy[p], self.red[p])
-        main.wait_stream(side)
+        if side is not main:
+            main.wait_stream(side)
 
     def _sgd(self, mode: int, scale: float = 1.0):
         self.ops.rn_sgd(self.master, self.grad, scale, self.state, self.conv_off, self.gamma_off, self.beta_off,

@@ -53,7 +53,7 @@ def test_resnet_dp2_matches_mean_of_rank_gradients(tmp_path, graph):
     for k in (0, 1):
         ref = FusedResNetEngine(B, x, y, device="cuda:0", seed=5, lr=LR)
         shard = r[k]["shard"]
-        ref.epoch_permutation = lambda epoch, s=shard: s.to(torch.int32)
+        ref.epoch_permutation = lambda epoch, s=shard: torch.cat([s, s]).to(torch.int32)   # row 0 = this rank's batch
         init = ref.flat_params().clone()
         grads.append(ref.compute_gradients().cpu().clone())
     expect = -LR * (grads[0] + grads[1]) / 2
