@@ -124,4 +124,4 @@ def test_fused_resnet_layer_table_matches_model():
     for B in (16, 256, 1024):
         for _, ci, co, _, _ in FR.LAYERS:
             g = FR.FusedResNetEngine._pick_groups(B, ci, co)
-            assert 1 <= g <= B // 2
+            assert 1 <= g <= B and g & (g - 1) == 0
