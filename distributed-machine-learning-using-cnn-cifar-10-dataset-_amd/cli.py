@@ -62,7 +62,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--output_every", type=int, default=d.output_every)
     p.add_argument("--eval_every", type=int, default=d.eval_every)
     p.add_argument("--eval_batches", type=int, default=d.eval_batches)
-    p.add_argument("--crop", type=int, default=d.crop)
+    p.add_argument("--crop", type=int, default=None,
+                   help="center crop (default 24 = the reference for cifar_cnn, 32 = full images for resnet20)")
     p.add_argument("--relu_logits", type="bool", default=d.relu_logits)
     p.add_argument("--augment", type="bool", default=d.augment)
     p.add_argument("--synthetic", type="bool", nargs="?", const=True, default=d.synthetic)
@@ -89,6 +90,8 @@ def parse(argv: Optional[List[str]] = None) -> Tuple[C.TrainConfig, List[str]]:
     """Parse flags -> (TrainConfig, unparsed args).  Unknown flags are returned, not rejected."""
     ns, unparsed = build_parser().parse_known_args(argv)
     fields = {f.name for f in dataclasses.fields(C.TrainConfig)}
+    if ns.crop is None:
+        ns.crop = 32 if ns.model == "resnet20" else C.CROP_HEIGHT
     cfg = C.TrainConfig(**{k: v for k, v in vars(ns).items() if k in fields})
     return cfg, unparsed
 

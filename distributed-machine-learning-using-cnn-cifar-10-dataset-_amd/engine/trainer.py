@@ -89,6 +89,40 @@ class _FusedAdapter:
         torch.cuda.synchronize(self.eng.device)
 
 
+class _FusedResNetAdapter(_FusedAdapter):
+    """ResNet-20 on the fused HIP engine (engine/fused_resnet.py): parameters + BN moving statistics
+    checkpointed under the same names as the eager model."""
+
+    def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, data, labels):
+        from .fused_resnet import FusedResNetEngine
+        from ..models import resnet as R
+        self.eng = FusedResNetEngine(cfg.batch_size, data, labels, device=info.device, world_size=info.world_size,
+                                     rank=max(0, info.rank), seed=cfg.seed, lr=cfg.learning_rate,
+                                     lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
+                                     staircase=cfg.lr_schedule == "staircase", comm_dtype=cfg.comm_dtype)
+        self.graph = cfg.graph
+        self.specs, self.state_specs = R.PARAM_SPECS, R.STATE_SPECS
+
+    def tf_tensors(self) -> Dict[str, torch.Tensor]:
+        d = CK.model_tensors(self.eng.flat_params(), self.eng.host_step, 0, specs=self.specs)
+        st = self.eng.state.detach().cpu()
+        d.update({s.name: st[s.offset:s.offset + s.numel].view(s.shape).clone() for s in self.state_specs})
+        return d
+
+    def load_tf_tensors(self, tensors):
+        flat, step, _ = CK.load_model_tensors(tensors, flat_size=self.eng.master.numel(), specs=self.specs)
+        state = torch.zeros_like(self.eng.state, device="cpu")
+        for s in self.state_specs:
+            if s.name not in tensors:
+                raise KeyError(f"checkpoint is missing {s.name}")
+            state[s.offset:s.offset + s.numel] = tensors[s.name].float().reshape(-1)
+        self.eng.load_flat_params(flat, step, state=state)
+
+    def broadcast_from_chief(self, info):
+        D.broadcast_(self.eng.state, info)
+        super().broadcast_from_chief(info)
+
+
 class _EagerAdapter:
     kind = "eager"
 
@@ -146,6 +180,9 @@ def pick_impl(cfg: C.TrainConfig, device: torch.device) -> str:
     if (device.type == "cuda" and cfg.model == "cifar_cnn" and cfg.dtype in ("bf16", "fp8") and cfg.crop == 24
             and cfg.batch_size % 16 == 0 and not cfg.augment):
         return "fused"
+    if (device.type == "cuda" and cfg.model == "resnet20" and cfg.dtype == "bf16" and cfg.crop == 32
+            and cfg.batch_size % 16 == 0 and not cfg.augment):
+        return "fused"
     return "eager"
 
 
@@ -169,7 +206,8 @@ class Session:
         tr_x, tr_y, te_x, te_y = _load_data(cfg, info)
         self.test = (te_x, te_y)
         impl = pick_impl(cfg, info.device)
-        self.engine = (_FusedAdapter if impl == "fused" else _EagerAdapter)(cfg, info, tr_x, tr_y)
+        fused = _FusedResNetAdapter if cfg.model == "resnet20" else _FusedAdapter
+        self.engine = (fused if impl == "fused" else _EagerAdapter)(cfg, info, tr_x, tr_y)
         self.impl = impl
         self.ckpt = None
         self.events = None
@@ -204,6 +242,8 @@ class Session:
         self.restore()
         self.save(force=True)            # CheckpointSaverHook.after_create_session
         eng.start()
+        self.log(f"[dmlc] engine={self.impl} model={cfg.model} dtype={cfg.dtype} batch={cfg.batch_size} "
+                 f"world={self.info.world_size} device={self.info.device}")
         self.log("Starting Training")
         i = 0
         last_t, last_step = time.time(), eng.global_step

@@ -181,3 +181,30 @@ def test_short_training_reduces_loss():
     assert last < 0.85 * first, (first, last)
     acc = eng.evaluate(data[:1024], labels[:1024])
     assert 0.0 <= acc <= 1.0
+
+
+def test_cli_fused_resnet20_checkpoint_resume(tmp_path):
+    """cifar10cnn.py --model=resnet20 on the GPU picks the fused engine; the checkpoint holds the
+    parameters + BN moving statistics under the eager model's names, and a rerun resumes from it."""
+    import os
+    import subprocess
+    import sys
+    from dmlc import checkpoint as CK
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(repo, "cifar10cnn.py"), "--model=resnet20", "--synthetic",
+           "--synthetic_size=1024", "--batch_size=64", "--generations=6", "--output_every=3", "--eval_every=6",
+           "--eval_batches=2", "--learning_rate=0.05", f"--log_dir={tmp_path}"]
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "engine=fused model=resnet20" in r.stdout, r.stdout[-2000:]
+    t = CK.read_bundle(CK.latest_checkpoint(str(tmp_path)))
+    assert int(t["global_step"]) == 6
+    m = R.ResNet20()
+    assert CK.load_module_tensors(m, t) == 6
+    mv = t["resnet20/stem/bn/moving_variance"]
+    assert not torch.allclose(mv, torch.ones_like(mv))          # running stats were updated and saved
+    r2 = subprocess.run(cmd[:-6] + ["--generations=9", "--output_every=3", "--eval_every=100", "--eval_batches=1",
+                                    "--learning_rate=0.05", f"--log_dir={tmp_path}"],
+                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r2.returncode == 0 and "Restored" in r2.stdout, r2.stdout[-3000:]
+    assert int(CK.read_bundle(CK.latest_checkpoint(str(tmp_path)))["global_step"]) == 9
