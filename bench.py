@@ -45,6 +45,9 @@ def parse():
                     help="capture the eager (PyTorch-op) step into a HIP graph (ResNet-20 path; the "
                          "framework-default comparison line is measured without it)")
     ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default="auto",
+                    help="gradient all-reduce (N>1): auto = xGMI peer-to-peer kernel when it self-tests "
+                         "and measures faster than RCCL, else RCCL")
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
     ap.add_argument("--dataset-size", type=int, default=50000)
@@ -62,11 +65,13 @@ def build_fused(args, info, data, labels):
     if args.model == "resnet20":
         from dmlc.engine.fused_resnet import FusedResNetEngine
         eng = FusedResNetEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
-                                rank=info.rank, seed=0, lr=0.01, comm_dtype=args.comm_dtype)
+                                rank=info.rank, seed=0, lr=0.01, comm_dtype=args.comm_dtype,
+                                allreduce=args.allreduce)
         return eng, eng.step, (None if args.no_graph else eng.capture)
     from dmlc.engine.fused import FusedCifarEngine
     eng = FusedCifarEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
-                           rank=info.rank, seed=0, comm_dtype=args.comm_dtype, dtype=args.dtype)
+                           rank=info.rank, seed=0, comm_dtype=args.comm_dtype, dtype=args.dtype,
+                           allreduce=args.allreduce)
     step = eng.step
     return eng, step, (None if args.no_graph else eng.capture)
 
@@ -112,6 +117,8 @@ def main():
     D.barrier(info)
     torch.cuda.synchronize()
     elapsed = D.all_max(time.perf_counter() - t0, info)
+    if hasattr(eng, "check_comm"):
+        eng.check_comm()
 
     n = info.world_size
     ms = elapsed * 1000.0 / args.steps
@@ -141,6 +148,7 @@ def main():
                 "impl": args.impl + ("+hipgraph" if (args.impl == "fused" and not args.no_graph)
                                      or (args.impl == "eager" and args.eager_graph) else ""),
                 "comm_dtype": args.comm_dtype,
+                "comm": getattr(eng, "comm_info", None),
             },
         }
         print(json.dumps(line), flush=True)

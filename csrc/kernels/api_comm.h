@@ -1,0 +1,36 @@
+// Host-side API of the xGMI peer-to-peer all-reduce (csrc/kernels/xgmi_allreduce.hip).
+//
+// One context per process (= per GPU rank).  It owns a device data buffer that every peer maps
+// through HIP IPC, plus a small signal block (uncached device memory) used for the cross-GPU
+// barriers.  The all-reduce is an ordinary kernel launch on the caller's stream: its barrier epochs
+// live in device memory, so the launch can be captured into a HIP graph and replayed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DMLC_XGMI_MAX_RANKS 8
+#define DMLC_XGMI_MAX_BLOCKS 128
+#define DMLC_XGMI_HANDLE_BYTES 64   // sizeof(hipIpcMemHandle_t)
+
+extern "C" {
+
+// Create the context: allocate `numel` fp32 elements (zeroed) + the signal block.
+// Returns a context id >= 0, or -1 (error string via dmlc_xgmi_last_error()).
+int dmlc_xgmi_create(int rank, int world, int64_t numel);
+float* dmlc_xgmi_buffer(int ctx);
+int64_t dmlc_xgmi_numel(int ctx);
+// 2 * DMLC_XGMI_HANDLE_BYTES bytes: IPC handle of the data buffer, then of the signal block.
+int dmlc_xgmi_handles(int ctx, uint8_t* out);
+// all_handles: world * 2 * DMLC_XGMI_HANDLE_BYTES bytes in rank order (own entry ignored).
+int dmlc_xgmi_open(int ctx, const uint8_t* all_handles);
+// Sum-all-reduce elements [offset, offset + numel) of the buffer across the ranks, in place.
+// offset and numel must be multiples of 4 (16-byte vectors).  Deterministic: element i's sum is
+// computed by one owner rank in fixed rank order and pushed to every peer, so replicas stay
+// bit-identical.
+hipError_t dmlc_xgmi_allreduce(int ctx, int64_t offset, int64_t numel, int blocks, hipStream_t s);
+// Sticky error word of the context (device memory): bit 0 = a barrier timed out.
+int dmlc_xgmi_error(int ctx);
+void dmlc_xgmi_destroy(int ctx);
+const char* dmlc_xgmi_last_error();
+
+}  // extern "C"

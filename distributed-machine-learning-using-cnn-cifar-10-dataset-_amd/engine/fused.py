@@ -58,7 +58,7 @@ class FusedCifarEngine:
                  relu_logits: bool = True, crop_offset=(4, 4), world_size: int = 1, rank: int = 0,
                  process_group=None, seed: int = 0, fc1_split: Optional[int] = None, g1: Optional[int] = None,
                  g2: Optional[int] = None, stats_len: int = 4096, comm_dtype: str = "fp32",
-                 capture_comm: bool = False, dtype: str = "bf16"):
+                 capture_comm: bool = False, dtype: str = "bf16", allreduce: str = "auto"):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -92,7 +92,21 @@ class FusedCifarEngine:
         if flat_params is None:
             flat_params = M.init_flat_params(torch.Generator().manual_seed(seed))
         self.master = flat_params.to(dev, torch.float32).contiguous().clone()
-        self.grad = torch.zeros_like(self.master)
+        # gradient all-reduce: xGMI peer-to-peer kernel over an IPC-shared grad buffer when every
+        # rank can map every peer and it measures faster than RCCL (parallel/xgmi.py), else RCCL
+        self.xgmi, self.comm_info = None, {"allreduce": "rccl" if world_size > 1 else "none"}
+        self._buckets = {True: (M.FC_BUCKET_OFFSET, self.master.numel() - M.FC_BUCKET_OFFSET),
+                         False: (0, M.FC_BUCKET_OFFSET)}
+        if world_size > 1 and dev.type == "cuda" and comm_dtype == "fp32" and allreduce != "rccl":
+            from ..parallel import xgmi as X
+            self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev,
+                                                 [self._buckets[True], self._buckets[False]], mode=allreduce,
+                                                 group=process_group)
+        if self.xgmi is not None:
+            self.grad = self.xgmi.buf[:self.master.numel()]
+            self.grad.zero_()
+        else:
+            self.grad = torch.zeros_like(self.master)
         bf = torch.bfloat16
         z = lambda *s, dt=bf: torch.zeros(*s, dtype=dt, device=dev)
         self.w1f, self.w2f, self.w2d = z(64, 160), z(64, 1600), z(64, 1600)
@@ -239,6 +253,18 @@ class FusedCifarEngine:
         else:
             dist.all_reduce(t, group=self.pg)
 
+    def _allreduce_bucket(self, fc: bool):
+        off, n = self._buckets[fc]
+        if self.xgmi is not None:
+            self.xgmi.all_reduce(off, n)
+        else:
+            self._allreduce(self.grad[off:off + n])
+
+    def check_comm(self):
+        """Raise if the xGMI all-reduce saw a peer stop participating (sticky device error word)."""
+        if self.xgmi is not None:
+            self.xgmi.check()
+
     # segments of one step: each is a capturable list of launches on the current stream
     def _seg_compute_a(self):
         self._forward(self.perm, self.step_t, self.period, train=True)
@@ -285,27 +311,28 @@ class FusedCifarEngine:
         ev.record(main)
         self.comm_stream.wait_event(ev)
         with torch.cuda.stream(self.comm_stream):
-            self._allreduce(self.grad[M.FC_BUCKET_OFFSET:])
+            self._allreduce_bucket(fc=True)
             seg[2]()
         seg[1]()
         ev2 = torch.cuda.Event()
         ev2.record(main)
         self.comm_stream.wait_event(ev2)
         with torch.cuda.stream(self.comm_stream):
-            self._allreduce(self.grad[:M.FC_BUCKET_OFFSET])
+            self._allreduce_bucket(fc=False)
             seg[3]()
         main.wait_stream(self.comm_stream)
 
     # --- graph capture --------------------------------------------------------------------------
     def capture(self):
-        """Capture the step into HIP graph(s).  N=1: one graph.  N>1: compute graphs around eager
-        RCCL collectives (or one graph including the collectives when capture_comm=True)."""
+        """Capture the step into HIP graph(s).  N=1: one graph.  N>1 over xGMI: one graph holding
+        compute, both all-reduce kernels and the two SGD halves on two streams.  N>1 over RCCL:
+        compute graphs around eager RCCL collectives (or one graph when capture_comm=True)."""
         torch.cuda.synchronize(self.device)
         self.graphs = []
         pool = torch.cuda.graph_pool_handle()
         if self.world_size == 1:
             segs = [self._eager_step]
-        elif self.capture_comm:
+        elif self.capture_comm or self.xgmi is not None:
             segs = [self._eager_step]
         else:
             segs = [self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv]

@@ -84,7 +84,8 @@ class FusedResNetEngine:
                  lr: float = C.LEARNING_RATE, lr_decay: float = C.LR_DECAY,
                  decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, world_size: int = 1,
                  rank: int = 0, process_group=None, seed: int = 0, groups: Optional[List[int]] = None,
-                 stats_len: int = 4096, comm_dtype: str = "fp32", wgrad_branch: Optional[bool] = None):
+                 stats_len: int = 4096, comm_dtype: str = "fp32", wgrad_branch: Optional[bool] = None,
+                 allreduce: str = "auto"):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -113,7 +114,18 @@ class FusedResNetEngine:
             s0 = state
         self.master = f0.to(dev, torch.float32).contiguous().clone()
         self.state = s0.to(dev, torch.float32).contiguous().clone()
-        self.grad = torch.zeros_like(self.master) if world_size > 1 else None
+        # gradient all-reduce (N>1): xGMI peer-to-peer kernel over an IPC-shared buffer when it
+        # self-tests and measures faster than RCCL (parallel/xgmi.py), else RCCL
+        self.xgmi, self.comm_info = None, {"allreduce": "rccl" if world_size > 1 else "none"}
+        if world_size > 1 and dev.type == "cuda" and comm_dtype == "fp32" and allreduce != "rccl":
+            from ..parallel import xgmi as X
+            self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev,
+                                                 [(0, self.master.numel())], mode=allreduce, group=process_group)
+        if self.xgmi is not None:
+            self.grad = self.xgmi.buf[:self.master.numel()]
+            self.grad.zero_()
+        else:
+            self.grad = torch.zeros_like(self.master) if world_size > 1 else None
         P = {s.name[len(R.SCOPE) + 1:]: s for s in R.PARAM_SPECS}
         S = {s.name[len(R.SCOPE) + 1:]: s for s in R.STATE_SPECS}
         view = lambda buf, s: buf[s.offset:s.offset + s.numel]
@@ -252,12 +264,20 @@ class FusedResNetEngine:
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
+        if self.xgmi is not None:
+            self.xgmi.all_reduce(0, t.numel())
+            return
         if self.comm_dtype == "bf16":
             tb = t.to(torch.bfloat16)
             dist.all_reduce(tb, group=self.pg)
             t.copy_(tb)
         else:
             dist.all_reduce(t, group=self.pg)
+
+    def check_comm(self):
+        """Raise if the xGMI all-reduce saw a peer stop participating (sticky device error word)."""
+        if self.xgmi is not None:
+            self.xgmi.check()
 
     def _seg_compute(self):
         self._forward(self.perm, self.step_t, self.period)
@@ -288,7 +308,12 @@ class FusedResNetEngine:
         torch.cuda.synchronize(self.device)
         self.graphs = []
         pool = torch.cuda.graph_pool_handle()
-        segs = [self._seg_compute] if self.world_size == 1 else [self._seg_compute, self._seg_apply]
+        if self.world_size == 1:
+            segs = [self._seg_compute]
+        elif self.xgmi is not None:          # the all-reduce is a kernel: the whole step is one graph
+            segs = [self._eager_step]
+        else:
+            segs = [self._seg_compute, self._seg_apply]
         for fn in segs:
             g = torch.cuda.CUDAGraph()
             s = torch.cuda.Stream(device=self.device)

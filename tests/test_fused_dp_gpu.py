@@ -1,7 +1,8 @@
 """Data-parallel fused engine (two graph segments around the bucketed all-reduce + apply-only SGD)
 vs a single-process fused run on the union batch.  Two ranks share the one GPU of the test box and
 talk over gloo (which all-reduces GPU tensors through the host); on an 8-GPU node the same code
-path runs over RCCL.  SURVEY.md §2.D / §4 'Distributed'."""
+path runs over RCCL.  allreduce="xgmi" runs the IPC peer-to-peer all-reduce kernel instead
+(parallel/xgmi.py; the two ranks map each other's gradient buffer on the shared GPU).  SURVEY.md §2.D / §4 'Distributed'."""
 import os
 import sys
 
@@ -19,7 +20,7 @@ def _data():
     return x, y
 
 
-def _rank(rank, world, port, out, B, steps, graph, comm_dtype):
+def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce):
     sys.path.insert(0, REPO)
     import torch.distributed as dist
     import dmlc  # noqa: F401
@@ -29,7 +30,8 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype):
                             timeout=datetime.timedelta(seconds=60))   # a failing peer must not hang the suite
     x, y = _data()
     eng = FusedCifarEngine(B, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
-                           relu_logits=False, comm_dtype=comm_dtype)
+                           relu_logits=False, comm_dtype=comm_dtype, allreduce=allreduce)
+    assert eng.comm_info["allreduce"] == ("xgmi" if allreduce == "xgmi" else "rccl"), eng.comm_info
     eng.step()
     if graph:
         eng.capture()
@@ -42,13 +44,15 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype):
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("graph,comm_dtype", [(False, "fp32"), (True, "fp32"), (True, "bf16")])
-def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype):
+@pytest.mark.parametrize("graph,comm_dtype,allreduce", [(False, "fp32", "rccl"), (True, "fp32", "rccl"),
+                                                        (True, "bf16", "rccl"), (False, "fp32", "xgmi"),
+                                                        (True, "fp32", "xgmi")])
+def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype, allreduce):
     import torch.multiprocessing as mp
     from dmlc.cli import free_port
     from dmlc.engine.fused import FusedCifarEngine
     B, steps = 32, 3
-    mp.spawn(_rank, args=(2, free_port(), str(tmp_path), B, steps, graph, comm_dtype), nprocs=2, join=True)
+    mp.spawn(_rank, args=(2, free_port(), str(tmp_path), B, steps, graph, comm_dtype, allreduce), nprocs=2, join=True)
     r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
     assert r0["step"] == r1["step"] == steps
