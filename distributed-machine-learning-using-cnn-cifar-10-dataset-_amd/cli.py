@@ -79,6 +79,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--save_checkpoints", type="bool", default=d.save_checkpoints)
     p.add_argument("--metrics_file", type=str, default=d.metrics_file)
     p.add_argument("--comm_dtype", choices=["fp32", "bf16"], default=d.comm_dtype)
+    p.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default=d.allreduce,
+                   help="gradient all-reduce: xGMI peer-to-peer kernel (auto: when it self-tests and "
+                        "measures faster than RCCL) or RCCL")
     p.add_argument("--pg_timeout_s", type=float, default=d.pg_timeout_s)
     p.add_argument("--graph", type="bool", default=d.graph)
     p.add_argument("--trace", choices=["", "roctx", "torch"], default=d.trace)

@@ -45,7 +45,7 @@ class _FusedAdapter:
                                     lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                     staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
                                     crop_offset=((32 - cfg.crop) // 2,) * 2, comm_dtype=cfg.comm_dtype,
-                                    dtype=cfg.dtype)
+                                    dtype=cfg.dtype, allreduce=cfg.allreduce)
         self.graph = cfg.graph
         from ..models import cifar_cnn as M
         self.specs = M.PARAM_SPECS
@@ -99,7 +99,8 @@ class _FusedResNetAdapter(_FusedAdapter):
         self.eng = FusedResNetEngine(cfg.batch_size, data, labels, device=info.device, world_size=info.world_size,
                                      rank=max(0, info.rank), seed=cfg.seed, lr=cfg.learning_rate,
                                      lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
-                                     staircase=cfg.lr_schedule == "staircase", comm_dtype=cfg.comm_dtype)
+                                     staircase=cfg.lr_schedule == "staircase", comm_dtype=cfg.comm_dtype,
+                                     allreduce=cfg.allreduce)
         self.graph = cfg.graph
         self.specs, self.state_specs = R.PARAM_SPECS, R.STATE_SPECS
 

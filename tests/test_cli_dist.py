@@ -38,6 +38,20 @@ def test_bool_flags():
         cli.parse(["--relu_logits=maybe"])
 
 
+def test_allreduce_flag():
+    assert cli.parse([])[0].allreduce == "auto"
+    assert cli.parse(["--allreduce=xgmi"])[0].allreduce == "xgmi"
+    with pytest.raises(SystemExit):
+        cli.parse(["--allreduce=mpi"])
+
+
+def test_xgmi_selection_is_rccl_without_gpu():
+    """CPU / world 1: the selector never builds the IPC path (no device kernels off-GPU)."""
+    from dmlc.parallel import xgmi
+    ar, info = xgmi.select(1024, 0, 1, torch.device("cpu"), [(0, 1024)])
+    assert ar is None and info["allreduce"] == "rccl"
+
+
 def test_role_mapping():
     base = dict(ps_hosts="localhost:2222", worker_hosts="localhost:2223,localhost:2224,otherhost:2225")
     r = cli.resolve_role(TrainConfig(job_name="worker", task_index=1, **base), env={})
