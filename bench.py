@@ -105,18 +105,25 @@ def main():
         step()
     if capture is not None:
         capture()
-    for _ in range(max(0, args.warmup - 3)):
-        step()
+    # run(n): n complete steps, chained K per graph replay inside an epoch (fused CNN engine)
+    run = getattr(eng, "run", None) if capture is not None else None
+    if run is None:
+        def run(n):
+            for _ in range(n):
+                step()
+    run(max(0, args.warmup - 3))
     torch.cuda.synchronize()
     D.barrier(info)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run(args.steps)
     torch.cuda.synchronize()
     D.barrier(info)
     torch.cuda.synchronize()
     elapsed = D.all_max(time.perf_counter() - t0, info)
+    if hasattr(eng, "global_step"):     # every timed step really ran: the device step counter agrees
+        want = max(1, min(3, args.warmup)) + max(0, args.warmup - 3) + args.steps
+        assert eng.global_step() == want, (eng.global_step(), want)
     if hasattr(eng, "check_comm"):
         eng.check_comm()
 

@@ -134,6 +134,32 @@ void conv2_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const
   CHECK_HIP(dmlc_conv2_wgrad(&a, stream_of(p1)));
 }
 
+void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
+           int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
+           const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2) {
+  const int64_t B = dp1.size(0), g1 = part1.size(0), g2 = part2.size(0);
+  check_data(data);
+  TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
+  TORCH_CHECK(g1 >= 1 && g1 <= B && g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
+  check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+  check(am1, "am1", at::kByte, {B, 12, 12, 64});
+  check(part1, "part1", at::kFloat, {g1, 80, 64});
+  check(partb1, "partb1", at::kFloat, {g1, 64});
+  check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
+  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
+  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+  check(partb2, "partb2", at::kFloat, {g2, 64});
+  c10::DeviceGuard guard(dp1.device());
+  DmlcWgradArgs a;
+  a.w1.data = data.data_ptr<uint8_t>(); a.w1.src = index_src(idx, counter, period, B);
+  a.w1.cy = (int)cy; a.w1.cx = (int)cx;
+  a.w1.dp1 = dp1.data_ptr(); a.w1.am1 = am1.data_ptr<uint8_t>();
+  a.w1.part1 = part1.data_ptr<float>(); a.w1.partb1 = partb1.data_ptr<float>(); a.w1.g1 = (int)g1; a.w1.B = (int)B;
+  a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr<float>();
+  a.w2.partb2 = partb2.data_ptr<float>(); a.w2.g2 = (int)g2; a.w2.B = (int)B;
+  CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
+}
+
 // params per problem (12 ints): M, N, K, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit, relu, nvalid
 void gemm_grouped(at::TensorList A, at::TensorList Bm, at::TensorList C, const c10::List<c10::optional<Tensor>>& bias,
                   at::IntArrayRef params) {
@@ -308,6 +334,8 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("conv1_wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor(a!) part1, Tensor(b!) partb1) -> ()");
   m.def("conv2_wgrad(Tensor p1, Tensor dy2, Tensor(a!) part2, Tensor(b!) partb2) -> ()");
+  m.def("wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
+        "Tensor(a!) part1, Tensor(b!) partb1, Tensor p1, Tensor dy2, Tensor(c!) part2, Tensor(d!) partb2) -> ()");
   m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params) -> ()");
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
@@ -329,6 +357,7 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("conv2_dgrad", &conv2_dgrad);
   m.impl("conv1_wgrad", &conv1_wgrad);
   m.impl("conv2_wgrad", &conv2_wgrad);
+  m.impl("wgrad", &wgrad);
   m.impl("gemm_grouped", &gemm_grouped);
   m.impl("head", &head);
   m.impl("sgd", &sgd);

@@ -90,6 +90,12 @@ struct DmlcConv2WgradArgs {
   int B;
 };
 
+// Both weight gradients in one launch (blocks [0,g1): conv1; then conv2 as 4-wave halves).
+struct DmlcWgradArgs {
+  DmlcConv1WgradArgs w1;
+  DmlcConv2WgradArgs w2;
+};
+
 // Grouped bf16 GEMM: up to 8 independent problems in one launch, 64x64 tiles, MFMA 16x16x32.
 //   a_kmajor=1: A(m,k) = A[m*lda + k]; 0: A(m,k) = A[k*lda + m]
 //   b_kmajor=1: B(k,n) = B[n*ldb + k]; 0: B(k,n) = B[k*ldb + n]
@@ -167,6 +173,7 @@ hipError_t dmlc_fp8_roundtrip(const float* x, float* y, int n, float scale, hipS
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s);
 hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s);
+hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s);
 hipError_t dmlc_gemm_grouped(DmlcGemmGroup* g, hipStream_t s);
 hipError_t dmlc_head(const DmlcHeadArgs* a, hipStream_t s);
 hipError_t dmlc_sgd(DmlcSgdArgs* a, hipStream_t s);

@@ -56,8 +56,7 @@ struct Conv1Input {                            // prefetch of the 28x32 zero-pad
   }
 };
 
-__global__ __launch_bounds__(W1T, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* smem) {
   bf16* dyt = reinterpret_cast<bf16*>(smem);
   bf16* xs = dyt + W1_DYT;
   bf16* dps = xs + W1_XS;
@@ -66,7 +65,7 @@ __global__ __launch_bounds__(W1T, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
   float* red = reinterpret_cast<float*>(ams + 9216);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int grp = blockIdx.x, ch = w & 1, ks = w >> 1;   // MFMA: co tiles 2ch, 2ch+1; k-steps ks mod 4
+  const int ch = w & 1, ks = w >> 1;                     // MFMA: co tiles 2ch, 2ch+1; k-steps ks mod 4
   const int b0 = grp * a.B / a.g1, b1 = (grp + 1) * a.B / a.g1;
   DMLC_STAMP(DMLC_TK_W1, 0);
 
@@ -173,20 +172,38 @@ __global__ __launch_bounds__(W1T, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
   DMLC_STAMP(DMLC_TK_W1, 4);
 }
 
+__global__ __launch_bounds__(W1T, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv1_wgrad_block(a, blockIdx.x, smem);
+}
+
 // ---------------------------------------------------------------------------------------------
 constexpr int W2_LD = 72;                      // 144-B rows: tr reads of rows r / r+8 hit different banks
 constexpr int W2_XT = 12 * 16 * W2_LD;         // rows kh..kh+11 of the padded input, 16 cols
 constexpr int W2_DY = 160 * W2_LD;             // 144 pixels + 16 zero rows
 constexpr size_t W2_LDS = (size_t)(W2_XT + W2_DY) * 2;
 
-__global__ __launch_bounds__(256, 2) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// HALVES = 1: one image group per 4-wave block (blk = kh + 5 * group).  HALVES = 2: an 8-wave block
+// runs two independent 4-wave halves on groups 2*pair and 2*pair+1 (blk = kh + 5 * pair), each with
+// its own LDS region; both halves step through max(#images) iterations so their barriers line up.
+template <int HALVES>
+DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* smem_all) {
+  const int half = HALVES == 2 ? (int)(threadIdx.x >> 8) : 0;
+  char* smem = smem_all + half * W2_LDS;
   bf16* xt = reinterpret_cast<bf16*>(smem);
   bf16* dyt = xt + W2_XT;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x & 255, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int kh = blockIdx.x % 5, grp = blockIdx.x / 5;
-  const int b0 = grp * a.B / a.g2, b1 = (grp + 1) * a.B / a.g2;
+  const int kh = blk % 5, grp = (blk / 5) * HALVES + half;
+  const bool valid = grp < a.g2;
+  const int b0 = valid ? grp * a.B / a.g2 : 0, b1 = valid ? (grp + 1) * a.B / a.g2 : 0;
+  int nmax = b1 - b0;
+  if (HALVES == 2) {                            // both halves' image counts (uniform over the block)
+    const int g0 = (blk / 5) * 2, gb = g0 + 1;
+    const int n0 = g0 < a.g2 ? (g0 + 1) * a.B / a.g2 - g0 * a.B / a.g2 : 0;
+    const int n1 = gb < a.g2 ? (gb + 1) * a.B / a.g2 - gb * a.B / a.g2 : 0;
+    nmax = max(n0, n1);
+  }
   DMLC_STAMP(DMLC_TK_W2, 0);
 
   // zero halo columns (xx = 0,1,14,15) and the 16 padding dY rows once
@@ -219,12 +236,14 @@ __global__ __launch_bounds__(256, 2) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
     }
   };
   if (b0 < b1) load(b0);
-  for (int b = b0; b < b1; ++b) {
+  for (int it = 0; it < nmax; ++it) {
+    const int b = b0 + it;
+    const bool act = b < b1;                   // uniform per half (waves of one half agree)
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int k = tid + i * 256;
-      if (k < 1152) {
+      if (act && k < 1152) {
         const int yy = k / 96, rem = k - yy * 96, px = rem >> 3, c = rem & 7;
         *reinterpret_cast<uint4*>(xt + (yy * 16 + px + 2) * W2_LD + c * 8) = vx[i];
         *reinterpret_cast<uint4*>(dyt + (k >> 3) * W2_LD + (k & 7) * 8) = vd[i];
@@ -237,7 +256,8 @@ __global__ __launch_bounds__(256, 2) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
     }
     if (b + 1 < b1) load(b + 1);
     __syncthreads();
-    if (b == b0) DMLC_STAMP(DMLC_TK_W2, 1);
+    if (it == 0) DMLC_STAMP(DMLC_TK_W2, 1);
+    if (!act) continue;
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
       const int rA = 32 * s + 8 * g + q, rB = rA + 4;
@@ -257,24 +277,42 @@ __global__ __launch_bounds__(256, 2) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
     }
   }
   DMLC_STAMP(DMLC_TK_W2, 2);
-  float* out = a.part2 + (size_t)grp * 1600 * 64;
+  if (valid) {
+    float* out = a.part2 + (size_t)grp * 1600 * 64;
 #pragma unroll
-  for (int kw = 0; kw < 5; ++kw)
+    for (int kw = 0; kw < 5; ++kw)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+      for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int krow = (kh * 5 + kw) * 64 + 16 * w + 4 * g + i;
-        out[krow * 64 + 16 * ct + li] = acc[kw][ct][i];
-      }
+        for (int i = 0; i < 4; ++i) {
+          const int krow = (kh * 5 + kw) * 64 + 16 * w + 4 * g + i;
+          out[krow * 64 + 16 * ct + li] = acc[kw][ct][i];
+        }
+  }
   if (kh == 0) {
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);
     block_chunk_sum(bsum, red, tid);
     __syncthreads();
-    if (tid < 64) a.partb2[grp * 64 + tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+    if (valid && tid < 64)
+      a.partb2[grp * 64 + tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
   }
   DMLC_STAMP(DMLC_TK_W2, 3);
+}
+
+__global__ __launch_bounds__(256, 2) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  conv2_wgrad_block<1>(a, blockIdx.x, smem);
+}
+
+// Both weight gradients in ONE launch (no stream fork/join in the step graph): blocks [0, g1) run
+// the conv1 body (8 waves), the rest run the conv2 body as two 4-wave halves.  One block per CU
+// (LDS), so g1 + 5 * ceil(g2 / 2) <= 256 keeps every block resident in a single wave of blocks.
+constexpr size_t WG_LDS = W1_LDS > 2 * W2_LDS ? W1_LDS : 2 * W2_LDS;
+__global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if ((int)blockIdx.x < a.w1.g1) conv1_wgrad_block(a.w1, blockIdx.x, smem);
+  else conv2_wgrad_block<2>(a.w2, blockIdx.x - a.w1.g1, smem);
 }
 
 }  // namespace dmlc
@@ -299,6 +337,18 @@ hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s) {
 
 hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s) {
   hipLaunchKernelGGL(k_conv2_wgrad, dim3(5 * a->g2), dim3(256), W2_LDS, s, *a);
+  return hipGetLastError();
+}
+
+hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)WG_LDS);
+    attr = true;
+  }
+  const int blocks = a->w1.g1 + 5 * ((a->w2.g2 + 1) / 2);
+  hipLaunchKernelGGL(k_wgrad, dim3(blocks), dim3(W1T), WG_LDS, s, *a);
   return hipGetLastError();
 }
 

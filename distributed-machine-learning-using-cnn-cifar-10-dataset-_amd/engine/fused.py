@@ -9,8 +9,8 @@ SURVEY.md §3.3) is nine kernel launches, all reading their inputs from device m
   4 head         fc1 reduce/bias/ReLU, fc2, fc3, ReLU-logits, softmax-xent, accuracy, dlogits→dh2→dh1
   5 gemm (x7)    fc1 dgrad + dW1 + dW2 + dW3 + db1 + db2 + db3 in ONE grouped launch
   6 conv2_dgrad  pool2/ReLU backward (2x2-ownership gather) + conv2 input-gradient
-  7 conv1_wgrad  pool1/ReLU backward + conv1 weight/bias gradients, split-K partials    } two graph
-    conv2_wgrad  conv2 weight/bias gradients, split-K partials                          } branches
+  7 wgrad        ONE launch, two block roles: pool1/ReLU backward + conv1 weight/bias gradients,
+                 and conv2 weight/bias gradients (8-wave blocks as two 4-wave halves); split-K slabs
   8 sgd          partial reduction + SGD + LR schedule + bf16 shadow refresh + global_step++ + stats
 
 The batch index list is read through the device-resident global_step (``perm[step % period]``),
@@ -122,9 +122,16 @@ class FusedCifarEngine:
 
         # --- activations / workspaces -------------------------------------------------------
         self.fc1_split = fc1_split or self._pick_fc1_split(B)
-        self.g1 = g1 or max(1, min(B, B // 2))          # conv1 wgrad: 2 images per block
-        self.g2 = g2 or max(1, min(B, B // 6))          # conv2 wgrad: 5 kh blocks x 6 images (runs
-        #   beside conv1 wgrad, which is the longer branch; fewer groups = fewer slab bytes to reduce)
+        # both weight gradients run in ONE launch (ops.wgrad: no stream fork/join in the graph);
+        # DMLC_SPLIT_WGRAD=1 runs them as two kernels on forked streams instead (A/B comparisons)
+        import os
+        self.merged_wgrad = os.environ.get("DMLC_SPLIT_WGRAD", "0") != "1"
+        self.g2 = g2 or max(1, min(B, B // 6))          # conv2 wgrad: 5 kh blocks x ~6 images per group
+        #   (fewer groups = fewer slab bytes for the SGD kernel to reduce)
+        if self.merged_wgrad:                            # conv1 groups fill the CUs the conv2 halves leave
+            self.g1 = g1 or max(1, min(B, 256 - 5 * ((self.g2 + 1) // 2)))
+        else:
+            self.g1 = g1 or max(1, min(B, B // 2))      # conv1 wgrad: 2 images per block
         self.p1, self.am1 = z(B, 12, 12, 64), z(B, 12, 12, 64, dt=torch.uint8)
         self.p2, self.am2 = z(B, 6, 6, 64), z(B, 6, 6, 64, dt=torch.uint8)
         self.h1part = z(self.fc1_split, B, 384, dt=torch.float32)
@@ -164,6 +171,7 @@ class FusedCifarEngine:
                     + _gemm_params(16, 8, B, 16, 0, 8, 0, 1, 3, nvalid=10)))       # db3
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.multi = None                  # (k, graph of k chained steps), see capture()
         self.comm_stream = torch.cuda.Stream(device=dev) if world_size > 1 else None
         self.side_stream = torch.cuda.Stream(device=dev)
         self.host_step = 0
@@ -226,6 +234,10 @@ class FusedCifarEngine:
     def _conv_backward(self):
         o = self.ops
         o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
+        if self.merged_wgrad:
+            o.wgrad(self.data, self.perm, self.step_t, self.period, self.cy, self.cx, self.dp1, self.am1,
+                    self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2)
+            return
         # the two weight-gradient kernels are independent: fork them onto two streams (two parallel
         # branches of the captured graph) so they share the chip
         main = torch.cuda.current_stream(self.device)
@@ -323,19 +335,27 @@ class FusedCifarEngine:
         main.wait_stream(self.comm_stream)
 
     # --- graph capture --------------------------------------------------------------------------
-    def capture(self):
+    def capture(self, steps_per_graph: int = 8):
         """Capture the step into HIP graph(s).  N=1: one graph.  N>1 over xGMI: one graph holding
         compute, both all-reduce kernels and the two SGD halves on two streams.  N>1 over RCCL:
-        compute graphs around eager RCCL collectives (or one graph when capture_comm=True)."""
+        compute graphs around eager RCCL collectives (or one graph when capture_comm=True).
+
+        When the whole step is one graph, a second graph chains ``steps_per_graph`` complete steps
+        (every step reads its batch and LR through the device step counter, so consecutive steps
+        need no host work): :meth:`run` replays it inside an epoch and saves the host launch gap
+        between graphs (~5 us per step)."""
         torch.cuda.synchronize(self.device)
-        self.graphs = []
+        self.graphs, self.multi = [], None
         pool = torch.cuda.graph_pool_handle()
-        if self.world_size == 1:
-            segs = [self._eager_step]
-        elif self.capture_comm or self.xgmi is not None:
+        single = self.world_size == 1 or self.capture_comm or self.xgmi is not None
+        if single:
             segs = [self._eager_step]
         else:
             segs = [self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv]
+        if single and steps_per_graph > 1:
+            k = int(steps_per_graph)
+            self.multi = (k, None)
+            segs = segs + [lambda: [self._eager_step() for _ in range(k)]]
         # state (step counter, master weights) must be identical before and after capture: a
         # capture records launches without running them, so nothing changes here.
         for fn in segs:
@@ -347,7 +367,25 @@ class FusedCifarEngine:
                     fn()
             torch.cuda.current_stream(self.device).wait_stream(s)
             self.graphs.append(g)
+        if self.multi is not None:
+            self.multi = (self.multi[0], self.graphs.pop())
         torch.cuda.synchronize(self.device)
+
+    def run(self, n: int):
+        """``n`` complete training steps (asynchronous).  Inside an epoch, whole ``steps_per_graph``
+        chunks replay the multi-step graph; epoch boundaries (host-side permutation refresh) and the
+        remainder go through :meth:`step`."""
+        n = int(n)
+        while n > 0:
+            self._maybe_new_epoch()
+            left_in_epoch = self.period - self.host_step % self.period
+            if self.multi is not None and n >= self.multi[0] and left_in_epoch >= self.multi[0]:
+                self.multi[1].replay()
+                self.host_step += self.multi[0]
+                n -= self.multi[0]
+            else:
+                self.step()
+                n -= 1
 
     def step(self):
         """One training step (asynchronous: returns once launched)."""

@@ -60,6 +60,42 @@ def test_gradients_match_reference(B):
         assert cos > 0.99 and _rel(a, b) < 0.1, (s.name, cos, _rel(a, b))
 
 
+@pytest.mark.parametrize("B,g2", [(64, 10), (256, 42), (48, 5)])
+def test_merged_wgrad_launch_equals_two_kernels(B, g2):
+    """ops.wgrad (both weight gradients in one launch, conv2 as 4-wave halves) is bit-identical to the
+    two separate kernels for the same split-K groups -- including an odd group count (idle half)."""
+    data, labels = _synthetic(4 * B, seed=7)
+    eng = FusedCifarEngine(B, data, labels, seed=6, g2=g2)
+    assert eng.merged_wgrad
+    g_merged = eng.compute_gradients().cpu().clone()
+    p1, pb1, p2, pb2 = (t.clone() for t in (eng.part1, eng.partb1, eng.part2, eng.partb2))
+    eng.merged_wgrad = False
+    g_split = eng.compute_gradients().cpu().clone()
+    assert torch.equal(eng.part2, p2) and torch.equal(eng.partb2, pb2)
+    assert torch.equal(eng.part1, p1) and torch.equal(eng.partb1, pb1)
+    assert torch.equal(g_merged, g_split)
+
+
+def test_multi_step_graph_run_equals_eager_steps():
+    """run(n) replays a graph of 3 chained steps inside each epoch and single steps across epoch
+    boundaries; the result is bit-identical to n eager steps (same batches, same LR schedule)."""
+    B = 32
+    data, labels = _synthetic(5 * B, seed=9)          # period 5: chunks of 3 must stop at boundaries
+    kw = dict(seed=11, lr=1e-4, decay_steps=4, relu_logits=False)     # stays finite: NaN != NaN
+    a = FusedCifarEngine(B, data, labels, **kw)
+    b = FusedCifarEngine(B, data, labels, **kw)
+    a.step()
+    a.capture(steps_per_graph=3)
+    a.run(20)
+    for _ in range(21):
+        b.step()
+    torch.cuda.synchronize()
+    assert a.global_step() == b.global_step() == 21 and a.host_step == 21
+    assert torch.isfinite(a.flat_params()).all()
+    assert torch.equal(a.flat_params(), b.flat_params())
+    assert a.read_stats(21) == b.read_stats(21)
+
+
 def test_sgd_step_matches_reference_update():
     B = 64
     data, labels = _synthetic(4 * B, seed=5)

@@ -63,14 +63,17 @@ def main():
     res["conv1_wgrad"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.perm, eng.step_t, eng.period, eng.cy, eng.cx,
                                                       eng.dp1, eng.am1, eng.part1, eng.partb1), a.iters)
     res["conv2_wgrad"] = timeit(lambda: o.conv2_wgrad(eng.p1, eng.dy2, eng.part2, eng.partb2), a.iters)
-    res["conv_bwd_forked"] = timeit(eng._conv_backward, a.iters)
+    res["wgrad_merged"] = timeit(lambda: o.wgrad(eng.data, eng.perm, eng.step_t, eng.period, eng.cy, eng.cx,
+                                                 eng.dp1, eng.am1, eng.part1, eng.partb1, eng.p1, eng.dy2,
+                                                 eng.part2, eng.partb2), a.iters)
+    res["conv_bwd"] = timeit(eng._conv_backward, a.iters)
     res["sgd_reduce_only"] = timeit(lambda: eng._sgd(mode=1), a.iters)
     res["sgd_full"] = timeit(lambda: eng._sgd(mode=0), a.iters)
     res["step_eager"] = timeit(eng._eager_step, a.iters)
     eng.capture()
     res["step_graph"] = timeit(lambda: eng.graphs[0].replay(), a.iters)
     res["sum_kernels"] = sum(v for k, v in res.items()
-                             if not k.startswith("step") and k not in ("sgd_reduce_only", "conv_bwd_forked"))
+                             if not k.startswith("step") and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad"))
     cfg = dict(batch=a.batch, g1=eng.g1, g2=eng.g2, fc1_split=eng.fc1_split)
     print(json.dumps({"config": cfg, "us": {k: round(v, 2) for k, v in res.items()}}), flush=True)
 
