@@ -136,19 +136,20 @@ void conv2_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const
 
 void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
            int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
-           const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2) {
-  const int64_t B = dp1.size(0), g1 = part1.size(0), g2 = part2.size(0);
+           const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2) {
+  const int64_t B = dp1.size(0), g1 = part1.size(0), g2 = groups2, slabs2 = (groups2 + 1) / 2;
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
   TORCH_CHECK(g1 >= 1 && g1 <= B && g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
+  TORCH_CHECK(part2.size(0) == slabs2, "wgrad: conv2 slabs must be ceil(groups2 / 2)");
   check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
   check(am1, "am1", at::kByte, {B, 12, 12, 64});
   check(part1, "part1", at::kFloat, {g1, 80, 64});
   check(partb1, "partb1", at::kFloat, {g1, 64});
   check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  check(part2, "part2", at::kFloat, {g2, 1600, 64});
-  check(partb2, "partb2", at::kFloat, {g2, 64});
+  check(part2, "part2", at::kFloat, {slabs2, 1600, 64});
+  check(partb2, "partb2", at::kFloat, {slabs2, 64});
   c10::DeviceGuard guard(dp1.device());
   DmlcWgradArgs a;
   a.w1.data = data.data_ptr<uint8_t>(); a.w1.src = index_src(idx, counter, period, B);
@@ -335,7 +336,8 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(a!) part1, Tensor(b!) partb1) -> ()");
   m.def("conv2_wgrad(Tensor p1, Tensor dy2, Tensor(a!) part2, Tensor(b!) partb2) -> ()");
   m.def("wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
-        "Tensor(a!) part1, Tensor(b!) partb1, Tensor p1, Tensor dy2, Tensor(c!) part2, Tensor(d!) partb2) -> ()");
+        "Tensor(a!) part1, Tensor(b!) partb1, Tensor p1, Tensor dy2, Tensor(c!) part2, Tensor(d!) partb2, "
+        "int groups2) -> ()");
   m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params) -> ()");
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "

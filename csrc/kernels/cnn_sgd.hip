@@ -45,15 +45,17 @@ DEV float4 split_sum(const float* __restrict__ p, size_t stride, int n, float4* 
   constexpr int T = 256 / S;
   const int sp = threadIdx.x / T, idx = threadIdx.x % T;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  int q = sp;
-  for (; q + 7 * S < n; q += 8 * S) {
+  // 8 branch-free loads in flight per round (out-of-range slabs read slab 0 and add zero): a
+  // remainder loop here would serialise one memory latency per slab
+  for (int q = sp; q < n; q += 8 * S) {
     float4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(p + (size_t)(q + u * S) * stride);
+    for (int u = 0; u < 8; ++u)
+      v[u] = load_sel(reinterpret_cast<const float4*>(p + (size_t)(q + u * S) * stride),
+                      reinterpret_cast<const float4*>(p), q + u * S < n);
 #pragma unroll
     for (int u = 0; u < 8; ++u) s = add4(s, v[u]);
   }
-  for (; q < n; q += S) s = add4(s, *reinterpret_cast<const float4*>(p + (size_t)q * stride));
   lds[threadIdx.x] = s;
   __syncthreads();
   float4 t = lds[idx];
@@ -103,9 +105,11 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   // w2d[ci][((4-kh)*5 + (4-kw))*64 + co] : contiguous in co
   *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.w2d) + (size_t)ci * 1600 + (24 - khw) * 64 + co) =
       pack4(w.x, w.y, w.z, w.w);
+#ifndef DMLC_SGD_NO_W2F
   bf16* w2f = reinterpret_cast<bf16*>(a.w2f) + krow;  // w2f[co][krow]
   w2f[(co + 0) * 1600] = (bf16)w.x; w2f[(co + 1) * 1600] = (bf16)w.y;
   w2f[(co + 2) * 1600] = (bf16)w.z; w2f[(co + 3) * 1600] = (bf16)w.w;
+#endif
 }
 
 DEV void conv1_rows(const DmlcSgdArgs& a, int row, float lr, float4* lds) {
@@ -169,9 +173,11 @@ DEV void fc_block(const DmlcSgdArgs& a, int blk, float lr) {
     } else if (i >= a.off[6] && i < a.off[7]) {      // fc2 weight [384][192]
       const int j = i - a.off[6], k = j / 192, n = j - k * 192;
       *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.fc2n) + j) = pack4(v.x, v.y, v.z, v.w);
+#ifndef DMLC_SGD_NO_FC2T
       bf16* t = reinterpret_cast<bf16*>(a.fc2t);
       t[(n + 0) * 384 + k] = (bf16)v.x; t[(n + 1) * 384 + k] = (bf16)v.y;
       t[(n + 2) * 384 + k] = (bf16)v.z; t[(n + 3) * 384 + k] = (bf16)v.w;
+#endif
     } else if (i >= a.off[8] && i < a.off[9]) {      // fc3 weight [192][10]
       const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll

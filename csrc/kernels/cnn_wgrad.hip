@@ -277,8 +277,43 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* sme
     }
   }
   DMLC_STAMP(DMLC_TK_W2, 2);
-  if (valid) {
-    float* out = a.part2 + (size_t)grp * 1600 * 64;
+  // HALVES == 2: the two halves' partial sums are added in-block (half 0 + half 1, fixed order), so
+  // one slab per PAIR leaves the kernel -- half the bytes for the SGD kernel to reduce.
+  const int slab = HALVES == 2 ? blk / 5 : grp;
+  const bool writer = HALVES == 2 ? half == 0 : valid;
+  if (kh == 0) {
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);      // this half's region
+    block_chunk_sum(bsum, red, tid);
+    __syncthreads();
+    if (writer && tid < 64) {
+      float sb = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+      if (HALVES == 2) {
+        const float* r1 = reinterpret_cast<const float*>(smem_all + W2_LDS);
+        sb += (r1[tid] + r1[64 + tid]) + (r1[128 + tid] + r1[192 + tid]);
+      }
+      a.partb2[slab * 64 + tid] = sb;
+    }
+  }
+  if (HALVES == 2) {
+    f32x4* xch = reinterpret_cast<f32x4*>(smem_all);  // 20 x 256 f32x4 = 80 KB
+    __syncthreads();                                   // MFMA / bias reads of LDS are done
+    if (half == 1) {
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) xch[(kw * 4 + ct) * 256 + tid] = acc[kw][ct];
+    }
+    __syncthreads();
+    if (half == 0) {
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[kw][ct] += xch[(kw * 4 + ct) * 256 + tid];
+    }
+  }
+  if (writer) {
+    float* out = a.part2 + (size_t)slab * 1600 * 64;
 #pragma unroll
     for (int kw = 0; kw < 5; ++kw)
 #pragma unroll
@@ -289,14 +324,6 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* sme
           out[krow * 64 + 16 * ct + li] = acc[kw][ct][i];
         }
   }
-  if (kh == 0) {
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);
-    block_chunk_sum(bsum, red, tid);
-    __syncthreads();
-    if (valid && tid < 64)
-      a.partb2[grp * 64 + tid] = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
-  }
   DMLC_STAMP(DMLC_TK_W2, 3);
 }
 
@@ -306,8 +333,9 @@ __global__ __launch_bounds__(256, 2) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
 }
 
 // Both weight gradients in ONE launch (no stream fork/join in the step graph): blocks [0, g1) run
-// the conv1 body (8 waves), the rest run the conv2 body as two 4-wave halves.  One block per CU
-// (LDS), so g1 + 5 * ceil(g2 / 2) <= 256 keeps every block resident in a single wave of blocks.
+// the conv1 body (8 waves), the rest run the conv2 body as two 4-wave halves on image groups
+// 2p, 2p+1 whose sums leave as ONE slab p (a.w2.g2 = image groups, slabs = ceil(g2 / 2)).  One block
+// per CU (LDS): g1 + 5 * ceil(g2 / 2) <= 256 keeps every block resident in one wave of blocks.
 constexpr size_t WG_LDS = W1_LDS > 2 * W2_LDS ? W1_LDS : 2 * W2_LDS;
 __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];

@@ -126,11 +126,17 @@ class FusedCifarEngine:
         # DMLC_SPLIT_WGRAD=1 runs them as two kernels on forked streams instead (A/B comparisons)
         import os
         self.merged_wgrad = os.environ.get("DMLC_SPLIT_WGRAD", "0") != "1"
-        self.g2 = g2 or max(1, min(B, B // 6))          # conv2 wgrad: 5 kh blocks x ~6 images per group
-        #   (fewer groups = fewer slab bytes for the SGD kernel to reduce)
-        if self.merged_wgrad:                            # conv1 groups fill the CUs the conv2 halves leave
-            self.g1 = g1 or max(1, min(B, 256 - 5 * ((self.g2 + 1) // 2)))
+        if self.merged_wgrad:
+            # conv2: pairs of ~5-image groups (one 8-wave block per (kh, pair), one slab per pair);
+            # conv1: the CUs the conv2 blocks leave, >= 2 images per block (B=256: 25 pairs, g1=131:
+            # both roles end together, measured in profiles/r1_v7_*)
+            pairs = max(1, min(B // 2, round(B / 10.24))) if g2 is None else (g2 + 1) // 2
+            self.groups2 = g2 or 2 * pairs
+            self.g2 = pairs                              # slabs the SGD kernel reduces
+            self.g1 = g1 or max(1, min(B, max(B // 2, 256 - 5 * pairs)))
         else:
+            self.g2 = g2 or max(1, min(B, B // 6))      # conv2 wgrad: 5 kh blocks x ~6 images per group
+            self.groups2 = self.g2
             self.g1 = g1 or max(1, min(B, B // 2))      # conv1 wgrad: 2 images per block
         self.p1, self.am1 = z(B, 12, 12, 64), z(B, 12, 12, 64, dt=torch.uint8)
         self.p2, self.am2 = z(B, 6, 6, 64), z(B, 6, 6, 64, dt=torch.uint8)
@@ -236,7 +242,7 @@ class FusedCifarEngine:
         o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         if self.merged_wgrad:
             o.wgrad(self.data, self.perm, self.step_t, self.period, self.cy, self.cx, self.dp1, self.am1,
-                    self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2)
+                    self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2)
             return
         # the two weight-gradient kernels are independent: fork them onto two streams (two parallel
         # branches of the captured graph) so they share the chip

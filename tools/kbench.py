@@ -62,10 +62,11 @@ def main():
     res["conv2_dgrad"] = timeit(lambda: o.conv2_dgrad(eng.dp2, eng.am2, eng.w2d, eng.dp1, eng.dy2), a.iters)
     res["conv1_wgrad"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.perm, eng.step_t, eng.period, eng.cy, eng.cx,
                                                       eng.dp1, eng.am1, eng.part1, eng.partb1), a.iters)
-    res["conv2_wgrad"] = timeit(lambda: o.conv2_wgrad(eng.p1, eng.dy2, eng.part2, eng.partb2), a.iters)
+    if not eng.merged_wgrad:
+        res["conv2_wgrad"] = timeit(lambda: o.conv2_wgrad(eng.p1, eng.dy2, eng.part2, eng.partb2), a.iters)
     res["wgrad_merged"] = timeit(lambda: o.wgrad(eng.data, eng.perm, eng.step_t, eng.period, eng.cy, eng.cx,
                                                  eng.dp1, eng.am1, eng.part1, eng.partb1, eng.p1, eng.dy2,
-                                                 eng.part2, eng.partb2), a.iters)
+                                                 eng.part2, eng.partb2, eng.groups2), a.iters)
     res["conv_bwd"] = timeit(eng._conv_backward, a.iters)
     res["sgd_reduce_only"] = timeit(lambda: eng._sgd(mode=1), a.iters)
     res["sgd_full"] = timeit(lambda: eng._sgd(mode=0), a.iters)
