@@ -218,6 +218,9 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
   TORCH_CHECK(h1part.dim() == 3 && h1part.size(2) == 384, "h1part must be [nsplit,B,384]");
   const int64_t nsplit = h1part.size(0), B = h1part.size(1);
   TORCH_CHECK(B % 16 == 0 && B > 0, "head: batch must be a positive multiple of 16");
+  TORCH_CHECK(loss_part.numel() >= 1 && B % loss_part.numel() == 0, "head: loss partials must divide the batch");
+  const int64_t rows = B / loss_part.numel();      // rows per workgroup, picked by the caller
+  TORCH_CHECK(rows == 4 || rows == 8 || rows == 16, "head: B / loss_part.numel() must be 4, 8 or 16");
   check(h1part, "h1part", at::kFloat, {nsplit, B, 384});
   check_numel(b1, "b1", at::kFloat, 384);
   check(w2t, "w2t", at::kBFloat16, {192, 384});
@@ -228,8 +231,8 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
   check(w2d, "w2d", at::kBFloat16, {384, 192});
   dev(labels, "labels");
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.dim() == 1, "labels must be int32 [N]");
-  check(loss_part, "loss_part", at::kFloat, {B / 16});
-  check(correct_part, "correct_part", at::kInt, {B / 16});
+  check(loss_part, "loss_part", at::kFloat, {B / rows});
+  check(correct_part, "correct_part", at::kInt, {B / rows});
   if (train) {
     check(h1, "h1", at::kBFloat16, {B, 384});
     check(h2, "h2", at::kBFloat16, {B, 192});
@@ -243,7 +246,7 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
   a.b1 = b1.data_ptr<float>(); a.w2t = w2t.data_ptr(); a.b2 = b2.data_ptr<float>();
   a.w3t = w3t.data_ptr(); a.b3 = b3.data_ptr<float>(); a.w3d = w3d.data_ptr(); a.w2d = w2d.data_ptr();
   a.labels = labels.data_ptr<int>(); a.src = index_src(idx, counter, period, B);
-  a.B = (int)B; a.inv_batch = (float)inv_batch; a.relu_logits = relu_logits; a.train = train;
+  a.B = (int)B; a.rows = (int)rows; a.inv_batch = (float)inv_batch; a.relu_logits = relu_logits; a.train = train;
   a.h1 = train ? h1.data_ptr() : nullptr; a.h2 = train ? h2.data_ptr() : nullptr; a.dl = train ? dl.data_ptr() : nullptr;
   a.dh1 = train ? dh1.data_ptr() : nullptr; a.dh2 = train ? dh2.data_ptr() : nullptr;
   a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
@@ -261,7 +264,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
          const Tensor& fc3t, const Tensor& fc3d, const Tensor& step, double lr0, double decay, double decay_steps,
          bool staircase, const Tensor& ticket, const Tensor& loss_part, const Tensor& correct_part,
          const Tensor& stats, const c10::optional<Tensor>& w2f8, const c10::optional<Tensor>& amax_w,
-         const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize) {
+         const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize, int64_t batch) {
   TORCH_CHECK(roles >= 0 && roles <= 2, "sgd roles must be 0..2");
   TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
   TORCH_CHECK(off.size() == 10, "off must have 10 entries");
@@ -278,7 +281,8 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   check(part2, "part2", at::kFloat, {g2, 1600, 64});
   check(partb2, "partb2", at::kFloat, {g2, 64});
   TORCH_CHECK(loss_part.numel() >= 1, "loss partials missing");
-  const int64_t B = loss_part.numel() * 16;
+  const int64_t B = batch;
+  TORCH_CHECK(B >= 1 && B % loss_part.numel() == 0, "sgd: batch must be a multiple of the loss partial count");
   check(w1f, "w1f", at::kBFloat16, {64, 160});
   check(w2f, "w2f", at::kBFloat16, {64, 1600});
   check(w2d, "w2d", at::kBFloat16, {64, 1600});
@@ -347,8 +351,8 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
-        "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles=0, "
-        "bool finalize=True) -> ()");
+        "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
+        "bool finalize, int batch) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

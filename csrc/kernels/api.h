@@ -118,7 +118,7 @@ struct DmlcGemmGroup {
   int nblocks;
 };
 
-// MLP head, rows-parallel (16 rows per workgroup): fc1 split-K reduce + bias + ReLU, fc2, fc3,
+// MLP head, rows-parallel (rows = 4, 8 or 16 per workgroup; B / rows workgroups): fc1 split-K reduce + bias + ReLU, fc2, fc3,
 // (ReLU logits), softmax cross-entropy + accuracy, and (train) the backward through fc3/fc2.
 struct DmlcHeadArgs {
   const float* h1part; int nsplit;   // [nsplit][B][384]
@@ -129,9 +129,9 @@ struct DmlcHeadArgs {
   const void* w2d;                   // bf16 [384][192]
   const int* labels;                 // [N] dataset labels
   DmlcIndexSrc src;
-  int B; float inv_batch; int relu_logits; int train;
+  int B; int rows; float inv_batch; int relu_logits; int train;
   void* h1; void* h2; void* dl; void* dh1; void* dh2;   // bf16 [B][384],[B][192],[B][16],[B][384],[B][192]
-  float* loss_part; int* correct_part;                  // [B/16]
+  float* loss_part; int* correct_part;                  // [B/rows]
   float* logits_out;                                    // optional fp32 [B][10]
 };
 

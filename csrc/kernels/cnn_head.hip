@@ -4,7 +4,10 @@
 // Replaces /root/reference/cifar10cnn.py:130-176 (full1..full3, cifar_loss, batch_accuracy) and the
 // corresponding autodiff ops (SURVEY.md §2.B N7/N8/N10-N12, §2.C xent10_fwd_bwd + linear_bwd_dx).
 //
-// Rows-parallel: 16 batch rows per workgroup of 16 waves; everything per row stays in LDS.  Every
+// Rows-parallel: RB (4/8/16) batch rows per workgroup of 16 waves; everything per row stays in LDS.
+// The MFMA tiles keep 16 row columns (columns >= RB compute on zeros and are never stored): the head
+// is bound by how fast each CU pulls the ~300 KB of fc2 weights (both layouts), not by MFMA, so more
+// workgroups with fewer rows -- 8 per XCD sharing one L2 copy of the weights -- finish sooner.  Every
 // product is computed TRANSPOSED (C[feature][row]) so the weight fragment streams from L2 and each
 // lane ends up with 4 consecutive features of one row.  The weight fragments of a wave's output
 // tiles are loaded up front (fc2 at entry, behind the fc1 reduction; fc2^T right after the fc2
@@ -31,6 +34,7 @@ DEV bf16x4 relu_mask4(const f32x4& acc, const bf16x4& h) {
                (float)h[2] > 0.f ? acc[2] : 0.f, (float)h[3] > 0.f ? acc[3] : 0.f);
 }
 
+template <int RB>
 __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 h1s[16 * H1_LD];
   __shared__ __attribute__((aligned(16))) bf16 h2s[16 * H2_LD];
@@ -39,12 +43,13 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
   __shared__ float lg[16][17];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int r0 = blockIdx.x * 16;
+  const int r0 = blockIdx.x * RB;
+  const bool rv = li < RB;                      // this lane's row column is a real batch row
   DMLC_STAMP(DMLC_TK_HEAD, 0);
 
   // the loss wave's labels (counter -> index -> label chain) are fetched at entry
   int label = 0;
-  if (w == 12 && lane < 16) label = a.labels[head_index(a.src, a.B, r0 + lane)];
+  if (w == 12 && lane < RB) label = a.labels[head_index(a.src, a.B, r0 + lane)];
 
   // fc2 weight fragments of this wave's output tile (waves 0..11: features 16w..16w+15), in flight
   // while the fc1 partial sums are reduced
@@ -55,16 +60,16 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     for (int ks = 0; ks < 12; ++ks) w2f[ks] = glb_b128(W + ks * 32);
   }
 
-  // (a) h1 = relu(sum_s part[s] + b1): 16 x 96 float4, at most 2 per thread.  (Issuing all 2 x 8
-  // split loads up front measured slower than 4 at a time: with 16 blocks the head is bound by the
-  // per-CU L2 bandwidth of its ~0.5 MB of weights + partials, not by load latency.)
+  // (a) h1 = relu(sum_s part[s] + b1): RB x 96 float4, at most 2 per thread; rows RB..15 of the LDS
+  // tile are zeroed (their MFMA columns then compute on zeros).
   {
-    float4 acc[2];
-    int e[2];
+    constexpr int U = (RB * 96 + HT - 1) / HT;
+    float4 acc[U];
+    int e[U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < U; ++u) {
       e[u] = tid + u * HT;
-      const int ec = e[u] < 16 * 96 ? e[u] : 0;               // branch-free: clamp, discard later
+      const int ec = e[u] < RB * 96 ? e[u] : 0;               // branch-free: clamp, discard later
       const int r = ec / 96, n = (ec - r * 96) * 4;
       acc[u] = *reinterpret_cast<const float4*>(a.b1 + n);
       const float* hp = a.h1part + (size_t)(r0 + r) * 384 + n;
@@ -82,9 +87,13 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
         acc[u].x += v.x; acc[u].y += v.y; acc[u].z += v.z; acc[u].w += v.w;
       }
     }
+    if (RB < 16) {
+      for (int z = tid; z < (16 - RB) * 96; z += HT)
+        *reinterpret_cast<bf16x4*>(h1s + (RB + z / 96) * H1_LD + (z % 96) * 4) = pack4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (e[u] < 16 * 96) {
+    for (int u = 0; u < U; ++u) {
+      if (e[u] < RB * 96) {
         const int r = e[u] / 96, n = (e[u] - r * 96) * 4;
         const bf16x4 o = pack4(fmaxf(acc[u].x, 0.f), fmaxf(acc[u].y, 0.f), fmaxf(acc[u].z, 0.f), fmaxf(acc[u].w, 0.f));
         *reinterpret_cast<bf16x4*>(h1s + r * H1_LD + n) = o;
@@ -104,7 +113,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     const bf16x4 o = pack4(fmaxf(acc[0] + a.b2[n], 0.f), fmaxf(acc[1] + a.b2[n + 1], 0.f),
                            fmaxf(acc[2] + a.b2[n + 2], 0.f), fmaxf(acc[3] + a.b2[n + 3], 0.f));
     *reinterpret_cast<bf16x4*>(h2s + li * H2_LD + n) = o;
-    if (a.train) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.h2) + (size_t)(r0 + li) * 192 + n) = o;
+    if (a.train && rv) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.h2) + (size_t)(r0 + li) * 192 + n) = o;
   }
   // fc2^T fragments for (f): tiles w and w+16 (w < 8) of the 24 dh1 feature tiles, K = 192
   bf16x8 w2d[2][6];
@@ -144,7 +153,11 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
   // (d) softmax cross-entropy, accuracy, dlogits (wave 12, lanes 0..15 = rows)
   if (w == 12) {
     float loss = 0.f, corr = 0.f;
-    if (lane < 16) {
+    if (lane >= RB && lane < 16 && a.train) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j) dls[lane * DL_LD + j] = (bf16)0.f;
+    }
+    if (lane < RB) {
       const int b = r0 + lane;
       float m = lg[lane][0];
       int am = 0;
@@ -192,7 +205,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     const int n = 16 * w + 4 * g;
     const bf16x4 o = relu_mask4(acc, *reinterpret_cast<const bf16x4*>(h2s + li * H2_LD + n));
     *reinterpret_cast<bf16x4*>(dh2s + li * H2_LD + n) = o;
-    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh2) + (size_t)(r0 + li) * 192 + n) = o;
+    if (rv) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh2) + (size_t)(r0 + li) * 192 + n) = o;
   }
   lds_barrier();
   DMLC_STAMP(DMLC_TK_HEAD, 4);
@@ -206,7 +219,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     for (int ks = 0; ks < 6; ++ks) acc = mfma16(w2d[j][ks], lds_b128(dh2s + li * H2_LD + ks * 32 + 8 * g), acc);
     const int n = 16 * (w + 16 * j) + 4 * g;
     const bf16x4 o = relu_mask4(acc, *reinterpret_cast<const bf16x4*>(h1s + li * H1_LD + n));
-    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh1) + (size_t)(r0 + li) * 384 + n) = o;
+    if (rv) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh1) + (size_t)(r0 + li) * 384 + n) = o;
   }
   DMLC_STAMP(DMLC_TK_HEAD, 5);
 }
@@ -216,6 +229,11 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
 using namespace dmlc;
 
 extern "C" hipError_t dmlc_head(const DmlcHeadArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(k_head, dim3(a->B / 16), dim3(HT), 0, s, *a);
+  switch (a->rows) {
+    case 4: hipLaunchKernelGGL(k_head<4>, dim3(a->B / 4), dim3(HT), 0, s, *a); break;
+    case 8: hipLaunchKernelGGL(k_head<8>, dim3(a->B / 8), dim3(HT), 0, s, *a); break;
+    case 16: hipLaunchKernelGGL(k_head<16>, dim3(a->B / 16), dim3(HT), 0, s, *a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }

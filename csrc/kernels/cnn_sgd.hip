@@ -210,24 +210,31 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
   // Nothing is published THROUGH the ticket (loss/accuracy partials come from an earlier launch and
   // the step/stats are consumed by later launches), so no release/acquire fences: an agent-scope
   // release is an L2 write-back on every XCD, which 700 blocks would pay for nothing.  The only
-  // ordering needed -- every block has read *a.step before the last one bumps it -- is given by the
-  // vmcnt(0) drain before each block's ticket increment.
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // ordering needed -- every block has read *a.step before the last one bumps it -- holds once every
+  // wave of the block is past its update code, which consumed lr (hence *a.step): an LDS-only barrier (its
+  // lgkmcnt(0) also retires the scalar load) instead of __syncthreads(), whose vmcnt(0) would hold
+  // the ticket until every store of the block had been acknowledged.
+  lds_barrier();
+  if (threadIdx.x < 64) {                              // wave 0: ticket, then (last) the stats
+    unsigned t = 0;
+    if (threadIdx.x == 0) t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __shfl(t, 0);
     if (t == (unsigned)gridDim.x - 1) {
-      float loss = 0.f;
-      int corr = 0;
-      for (int q = 0; q < a.nhead; ++q) { loss += a.loss_part[q]; corr += a.correct_part[q]; }
-      float* st = a.stats + (size_t)(step % a.stats_len) * 4;
-      st[0] = (float)(step + 1);
-      st[1] = loss / (float)a.B;
-      st[2] = (float)corr / (float)a.B;
-      st[3] = lr;
-      *a.step = step + 1;
-      if (a.w2f8) a.amax_w[step & 1] = 0.f;           // every block has read it; next step's target
-      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the head's per-workgroup partials, summed by the whole wave (all loads in flight at once)
+      float loss = 0.f, corr = 0.f;
+      for (int q = threadIdx.x; q < a.nhead; q += 64) { loss += a.loss_part[q]; corr += (float)a.correct_part[q]; }
+      loss = wave_sum(loss);
+      corr = wave_sum(corr);
+      if (threadIdx.x == 0) {
+        float* st = a.stats + (size_t)(step % a.stats_len) * 4;
+        st[0] = (float)(step + 1);
+        st[1] = loss / (float)a.B;
+        st[2] = corr / (float)a.B;
+        st[3] = lr;
+        *a.step = step + 1;
+        if (a.w2f8) a.amax_w[step & 1] = 0.f;         // every block has read it; next step's target
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   DMLC_STAMP(DMLC_TK_SGD, 2);

@@ -21,6 +21,7 @@ while launches 6-7 run, then the conv bucket, then the SGD applies (SURVEY.md §
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -41,6 +42,8 @@ def _ops():
 
 
 SEG_OFF = [s.offset for s in M.PARAM_SPECS]
+# batch rows per head workgroup (4, 8 or 16; DMLC_HEAD_ROWS overrides it for A/B runs)
+HEAD_ROWS = int(os.environ.get("DMLC_HEAD_ROWS", "4"))
 SEG = {M.short(s.name): s for s in M.PARAM_SPECS}
 
 
@@ -147,8 +150,9 @@ class FusedCifarEngine:
         self.dp1, self.dy2 = z(B, 12, 12, 64), z(B, 144, 64)
         self.part2, self.partb2 = z(self.g2, 1600, 64, dt=torch.float32), z(self.g2, 64, dt=torch.float32)
         self.part1, self.partb1 = z(self.g1, 80, 64, dt=torch.float32), z(self.g1, 64, dt=torch.float32)
-        self.loss_part = z(B // 16, dt=torch.float32)
-        self.correct_part = z(B // 16, dt=torch.int32)
+        # head: HEAD_ROWS batch rows per workgroup (B / HEAD_ROWS workgroups share the fc2 weight reads)
+        self.loss_part = z(B // HEAD_ROWS, dt=torch.float32)
+        self.correct_part = z(B // HEAD_ROWS, dt=torch.int32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
@@ -260,7 +264,7 @@ class FusedCifarEngine:
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                      self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
                                                                       if self.fp8 else (None, None, None)),
-                     roles, finalize)
+                     roles, finalize, self.B)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist

@@ -83,6 +83,11 @@ def main():
                     d = (sub[:, 1] - sub[:, 0]) / 100.0
                     rec[f"role_{name}_work_us_med_max"] = [round(float(np.median(d)), 2), round(float(d.max()), 2)]
                     rec[f"role_{name}_start_us_max"] = round(float((sub[:, 0].max() - ent.min()) / 100.0), 2)
+                    rec[f"role_{name}_work_q10_50_90"] = [round(float(np.percentile(d, q)), 2) for q in (10, 50, 90)]
+                    ids = np.nonzero(raw[lo:hi, 0] > 0)[0] + lo
+                    rec[f"role_{name}_slowest_blocks"] = [int(i) for i in ids[np.argsort(-d)[:8]]]
+                    rec[f"role_{name}_work_by_xcd"] = [round(float(d[(ids % 8) == x].mean()), 2) if ((ids % 8) == x).any()
+                                                       else None for x in range(8)]
         out[NAMES[k]] = rec
     print(json.dumps(out, indent=1))
 
