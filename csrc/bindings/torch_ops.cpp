@@ -292,7 +292,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   check(fc3t, "fc3t", at::kBFloat16, {16, 192});
   check(fc3d, "fc3d", at::kBFloat16, {192, 32});
   check_numel(step, "step", at::kLong, 1);
-  check_numel(ticket, "ticket", at::kInt, 1);
+  check_numel(ticket, "ticket", at::kInt, DMLC_TICKET_WORDS);
   dev(loss_part, "loss_part"); dev(correct_part, "correct_part");
   TORCH_CHECK(loss_part.scalar_type() == at::kFloat && correct_part.scalar_type() == at::kInt &&
                   loss_part.numel() == correct_part.numel(), "loss/correct partials mismatch");

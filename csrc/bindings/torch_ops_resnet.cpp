@@ -209,7 +209,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
   check_numel(correct_img, "correct_img", at::kInt, B);
   check_numel(loss_img, "loss_img", at::kFloat, B);
   check_numel(step, "step", at::kLong, 1);
-  check_numel(ticket, "ticket", at::kInt, 1);
+  check_numel(ticket, "ticket", at::kInt, DMLC_TICKET_WORDS);
   dev(stats, "stats");
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(1) == 4, "stats must be [R,4] fp32");
   TORCH_CHECK(fcw_off >= 0 && fcw_off % 4 == 0 && fcw_off + 640 <= np && fcb_off >= 0 && fcb_off + 10 <= np,

@@ -7,6 +7,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// uints in the arrival-ticket buffer of the SGD launches (two-level counters, common.h last_arrival)
+#define DMLC_TICKET_WORDS (9 * 32)
+
 extern "C" {
 
 // Batch index source shared by the data-consuming kernels: sample index of row b is

@@ -13,9 +13,10 @@
 //   conv2 rows  : 4 weight rows (k = (kh,kw,ci)) x 64 co per block (400 blocks); the g2 slabs are
 //                 split over 4 thread groups (<= 8 loads in flight each) and combined in fixed order;
 //                 shadows w2f (co-major) and w2d (flipped, ci-major).
-//   conv1 rows  : 1 of the 75 HWIO rows per block, g1 slabs split 16 ways.
+//   conv1 rows  : half (32 co) of one of the 75 HWIO rows per block, g1 slabs split 32 ways.
 //   conv biases : 2 blocks over the per-group partial rows of each conv.
-//   fc          : float4 groups of the contiguous fc region (all segments 64-aligned), 4 per thread.
+//   fc1         : float4 groups of fc1 weight + bias (contiguous, 64-aligned), 4 per thread;
+//   fc2         : 64 weight rows per block, transposed shadow through LDS;  fc tail: fc2 bias + fc3.
 // modes: 0 = reduce + apply (single GPU), 1 = reduce only (conv grads -> flat grad, before the DP
 // all-reduce; fc blocks are not launched), 2 = apply from the flat grad (after the all-reduce),
 // 3 = refresh the shadows only (after init / checkpoint restore).
@@ -27,9 +28,19 @@ namespace dmlc {
 constexpr int SEG_NUMEL[10] = {4800, 64, 102400, 64, 884736, 384, 73728, 192, 1920, 10};
 constexpr int C2_SPLIT = 4, C2_ROWS = 256 / C2_SPLIT / 16;   // 4 rows x 64 co per block
 constexpr int C2_BLOCKS = 1600 / C2_ROWS;                     // 400
-constexpr int C1_SPLIT = 16;                                  // 1 row x 64 co per block
-constexpr int C1_BLOCKS = 75;
+constexpr int C1_SPLIT = 32;                                  // 1 row x 32 co per block
+constexpr int C1_LOADS = 5;                                   // g1 <= 160 slabs: one round of loads
+constexpr int C1_BLOCKS = 150;
 constexpr int FC_F4_PER_THREAD = 4;
+constexpr int FC2_ROWS = 64, FC2_COLS = 48;                  // fc2 weight tile (k x n) per block
+constexpr int FC2_BLOCKS = (384 / FC2_ROWS) * (192 / FC2_COLS);   // 24
+constexpr int FC_TAIL = 192 + 1920 + 10;                      // fc2 bias, fc3 weight + bias
+constexpr int FC_TAIL_BLOCKS = (FC_TAIL + 255) / 256;         // one element per thread
+
+// fc1 weight + bias (contiguous float4 range, same-layout shadow): blocks of 1024 float4
+__host__ __device__ inline int fc1_blocks(const DmlcSgdArgs& a) {
+  return ((a.off[6] - a.off[4]) / 4 + 256 * FC_F4_PER_THREAD - 1) / (256 * FC_F4_PER_THREAD);
+}
 
 DEV float lr_of(const DmlcSgdArgs& a, int64_t step) {
   return a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
@@ -40,21 +51,21 @@ DEV float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a
 // Deterministic split reduction of n fp32 slabs (float4 at p + q*stride).  The block's threads are
 // S splits x (256/S) outputs; split sp sums slabs sp, sp+S, ... with up to 8 loads in flight, then
 // split 0 adds the S partial sums in fixed order.  Returns the total on split-0 threads.
-template <int S>
+template <int S, int U = 8>
 DEV float4 split_sum(const float* __restrict__ p, size_t stride, int n, float4* lds) {
   constexpr int T = 256 / S;
   const int sp = threadIdx.x / T, idx = threadIdx.x % T;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  // 8 branch-free loads in flight per round (out-of-range slabs read slab 0 and add zero): a
+  // U branch-free loads in flight per round (out-of-range slabs read slab 0 and add zero): a
   // remainder loop here would serialise one memory latency per slab
-  for (int q = sp; q < n; q += 8 * S) {
-    float4 v[8];
+  for (int q = sp; q < n; q += U * S) {
+    float4 v[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < U; ++u)
       v[u] = load_sel(reinterpret_cast<const float4*>(p + (size_t)(q + u * S) * stride),
                       reinterpret_cast<const float4*>(p), q + u * S < n);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s = add4(s, v[u]);
+    for (int u = 0; u < U; ++u) s = add4(s, v[u]);
   }
   lds[threadIdx.x] = s;
   __syncthreads();
@@ -112,14 +123,14 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
 #endif
 }
 
-DEV void conv1_rows(const DmlcSgdArgs& a, int row, float lr, float4* lds) {
+DEV void conv1_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   constexpr int T = 256 / C1_SPLIT;
-  const int co = (threadIdx.x % T) * 4;               // HWIO row = (kh*5+kw)*3 + ci
+  const int row = blk >> 1, co = (blk & 1) * 32 + (threadIdx.x % T) * 4;   // HWIO row = (kh*5+kw)*3 + ci
   const int ci = row % 3, khw = row / 3, kh = khw / 5, kw = khw - kh * 5;
   const size_t e = (size_t)row * 64 + co;
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
   if (a.mode == 0 || a.mode == 1)                     // slab row k'' = kh*16 + kw*3 + ci
-    g = split_sum<C1_SPLIT>(a.part1 + (size_t)(kh * 16 + kw * 3 + ci) * 64 + co, 80 * 64, a.g1, lds);
+    g = split_sum<C1_SPLIT, C1_LOADS>(a.part1 + (size_t)(kh * 16 + kw * 3 + ci) * 64 + co, 80 * 64, a.g1, lds);
   if (threadIdx.x >= T) return;
   if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[0] + e);
   if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[0] + e) = g; return; }
@@ -146,8 +157,8 @@ DEV void conv_bias(const DmlcSgdArgs& a, int which, float lr, float4* lds) {
   sgd4(a.master + a.off[seg] + c, g, lr, a.grad_scale, a.mode != 3);
 }
 
-DEV void fc_block(const DmlcSgdArgs& a, int blk, float lr) {
-  const int base4 = a.off[4] >> 2, end4 = (a.off[9] + 10 + 3) >> 2;
+DEV void fc1_block(const DmlcSgdArgs& a, int blk, float lr) {
+  const int base4 = a.off[4] >> 2, end4 = a.off[6] >> 2;
   const bool apply = a.mode != 3;
   const float f = lr * a.grad_scale;
   int i4[FC_F4_PER_THREAD];
@@ -168,40 +179,82 @@ DEV void fc_block(const DmlcSgdArgs& a, int blk, float lr) {
       v.x -= f * g[u].x; v.y -= f * g[u].y; v.z -= f * g[u].z; v.w -= f * g[u].w;
       reinterpret_cast<float4*>(a.master)[i4[u]] = v;
     }
-    if (i < a.off[5]) {                               // fc1 weight [2304][384]: same layout shadow
+    if (i < a.off[5])                                 // fc1 weight [2304][384]: same layout shadow
       *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.fc1n) + (i - a.off[4])) = pack4(v.x, v.y, v.z, v.w);
-    } else if (i >= a.off[6] && i < a.off[7]) {      // fc2 weight [384][192]
-      const int j = i - a.off[6], k = j / 192, n = j - k * 192;
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.fc2n) + j) = pack4(v.x, v.y, v.z, v.w);
-#ifndef DMLC_SGD_NO_FC2T
-      bf16* t = reinterpret_cast<bf16*>(a.fc2t);
-      t[(n + 0) * 384 + k] = (bf16)v.x; t[(n + 1) * 384 + k] = (bf16)v.y;
-      t[(n + 2) * 384 + k] = (bf16)v.z; t[(n + 3) * 384 + k] = (bf16)v.w;
-#endif
-    } else if (i >= a.off[8] && i < a.off[9]) {      // fc3 weight [192][10]
-      const float vv[4] = {v.x, v.y, v.z, v.w};
+  }
+}
+
+// fc2 weight [384 k][192 n], one FC2_ROWS x FC2_COLS tile per block: shadows fc2n[k][n] (same
+// layout) and fc2t[n][k].  The transposed copy goes through LDS so every global store is a 16-B chunk
+// of a whole 128-B fc2t row segment (2-byte stores scattered over 192 rows made these blocks the
+// SGD's tail); tiles keep each block's bytes near the other roles' (the launch is bandwidth-bound:
+// a block that moves 3x the average bytes finishes 2-3x later).
+DEV void fc2_block(const DmlcSgdArgs& a, int blk, float lr, bf16* tl /*[FC2_COLS][FC2_ROWS + 8]*/) {
+  constexpr int LD = FC2_ROWS + 8, C4 = FC2_COLS / 4;
+  constexpr int F4 = FC2_ROWS * C4 / 256;                      // float4 per thread (3)
+  const bool apply = a.mode != 3;
+  const float f = lr * a.grad_scale;
+  const int k0 = (blk / (192 / FC2_COLS)) * FC2_ROWS, n0 = (blk % (192 / FC2_COLS)) * FC2_COLS;
+  float4 w[F4], g[F4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int j = i - a.off[8] + c;
-        if (j >= 1920) break;
-        const int k = j / 10, n = j - k * 10;
-        reinterpret_cast<bf16*>(a.fc3t)[n * 192 + k] = (bf16)vv[c];
-        reinterpret_cast<bf16*>(a.fc3d)[k * 32 + n] = (bf16)vv[c];
-      }
+  for (int u = 0; u < F4; ++u) {
+    const int j4 = u * 256 + threadIdx.x, kk = j4 / C4, n = n0 + 4 * (j4 - kk * C4);
+    const size_t e = (size_t)a.off[6] + (size_t)(k0 + kk) * 192 + n;
+    w[u] = *reinterpret_cast<const float4*>(a.master + e);
+    g[u] = *reinterpret_cast<const float4*>(a.grad + e);
+  }
+#pragma unroll
+  for (int u = 0; u < F4; ++u) {
+    const int j4 = u * 256 + threadIdx.x, kk = j4 / C4, nn = 4 * (j4 - kk * C4);
+    float4 v = w[u];
+    if (apply) {
+      v.x -= f * g[u].x; v.y -= f * g[u].y; v.z -= f * g[u].z; v.w -= f * g[u].w;
+      *reinterpret_cast<float4*>(a.master + a.off[6] + (size_t)(k0 + kk) * 192 + n0 + nn) = v;
     }
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.fc2n) + (size_t)(k0 + kk) * 192 + n0 + nn) =
+        pack4(v.x, v.y, v.z, v.w);
+    tl[(nn + 0) * LD + kk] = (bf16)v.x; tl[(nn + 1) * LD + kk] = (bf16)v.y;
+    tl[(nn + 2) * LD + kk] = (bf16)v.z; tl[(nn + 3) * LD + kk] = (bf16)v.w;
+  }
+  lds_barrier();
+  for (int c = threadIdx.x; c < FC2_COLS * (FC2_ROWS / 8); c += 256) {
+    const int nn = c / (FC2_ROWS / 8), k8 = c - nn * (FC2_ROWS / 8);
+    *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.fc2t) + (size_t)(n0 + nn) * 384 + k0 + 8 * k8) =
+        *reinterpret_cast<const bf16x8*>(tl + nn * LD + 8 * k8);
+  }
+}
+
+// fc2 bias, fc3 weight [192][10] (shadows fc3t[n][k], fc3d[k][n]) and fc3 bias: one scalar per thread
+DEV void fc_tail_block(const DmlcSgdArgs& a, int blk, float lr) {
+  const int j = blk * 256 + threadIdx.x;
+  if (j >= FC_TAIL) return;
+  const int i = a.off[7] + j;
+  float v = a.master[i];
+  if (a.mode != 3) {
+    v -= lr * a.grad_scale * a.grad[i];
+    a.master[i] = v;
+  }
+  if (i >= a.off[8] && i < a.off[8] + 1920) {
+    const int q = i - a.off[8], k = q / 10, n = q - k * 10;
+    reinterpret_cast<bf16*>(a.fc3t)[n * 192 + k] = (bf16)v;
+    reinterpret_cast<bf16*>(a.fc3d)[k * 32 + n] = (bf16)v;
   }
 }
 
 __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
-  __shared__ float4 lds[256];
+  constexpr int LDS4 = FC2_COLS * (FC2_ROWS + 8) * 2 / 16 > 256 ? FC2_COLS * (FC2_ROWS + 8) * 2 / 16 : 256;
+  __shared__ float4 lds[LDS4];                                // split sums (4 KB), fc2 transpose (6.8 KB)
   DMLC_STAMP(DMLC_TK_SGD, 0);
   const int64_t step = *a.step;
   const float lr = lr_of(a, step);
+  const int nfc1 = fc1_blocks(a);
   int blk = blockIdx.x + (a.roles == 2 ? C2_BLOCKS + C1_BLOCKS + 2 : 0);
   if (blk < C2_BLOCKS) conv2_rows(a, blk, lr, lds);
   else if ((blk -= C2_BLOCKS) < C1_BLOCKS) conv1_rows(a, blk, lr, lds);
   else if ((blk -= C1_BLOCKS) < 2) conv_bias(a, blk, lr, lds);
-  else fc_block(a, blk - 2, lr);
+  else if ((blk -= 2) < nfc1) fc1_block(a, blk, lr);
+  else if ((blk -= nfc1) < FC2_BLOCKS) fc2_block(a, blk, lr, reinterpret_cast<bf16*>(lds));
+  else fc_tail_block(a, blk - FC2_BLOCKS, lr);
   DMLC_STAMP(DMLC_TK_SGD, 1);
 
   if (!(a.mode == 0 || a.mode == 2) || !a.finalize) return;
@@ -211,15 +264,14 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
   // the step/stats are consumed by later launches), so no release/acquire fences: an agent-scope
   // release is an L2 write-back on every XCD, which 700 blocks would pay for nothing.  The only
   // ordering needed -- every block has read *a.step before the last one bumps it -- holds once every
-  // wave of the block is past its update code, which consumed lr (hence *a.step): an LDS-only barrier (its
-  // lgkmcnt(0) also retires the scalar load) instead of __syncthreads(), whose vmcnt(0) would hold
-  // the ticket until every store of the block had been acknowledged.
+  // wave of the block is past its update code, which consumed lr (hence *a.step): an LDS-only
+  // barrier (its lgkmcnt(0) also retires the scalar load) instead of __syncthreads(), whose vmcnt(0)
+  // would hold the ticket until every store of the block had been acknowledged.
   lds_barrier();
   if (threadIdx.x < 64) {                              // wave 0: ticket, then (last) the stats
-    unsigned t = 0;
-    if (threadIdx.x == 0) t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t = __shfl(t, 0);
-    if (t == (unsigned)gridDim.x - 1) {
+    int last = 0;
+    if (threadIdx.x == 0) last = last_arrival(a.ticket, blockIdx.x, gridDim.x) ? 1 : 0;
+    if (__shfl(last, 0)) {
       // the head's per-workgroup partials, summed by the whole wave (all loads in flight at once)
       float loss = 0.f, corr = 0.f;
       for (int q = threadIdx.x; q < a.nhead; q += 64) { loss += a.loss_part[q]; corr += (float)a.correct_part[q]; }
@@ -233,7 +285,6 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
         st[3] = lr;
         *a.step = step + 1;
         if (a.w2f8) a.amax_w[step & 1] = 0.f;         // every block has read it; next step's target
-        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -245,8 +296,10 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
 using namespace dmlc;
 
 extern "C" hipError_t dmlc_sgd(DmlcSgdArgs* a, hipStream_t s) {
-  const int fc4 = ((a->off[9] + 10 + 3) >> 2) - (a->off[4] >> 2);
-  const int fc_blocks = (fc4 + 256 * FC_F4_PER_THREAD - 1) / (256 * FC_F4_PER_THREAD);
+  if (a->off[5] - a->off[4] != 884736 || a->off[6] % 4 || a->off[6] - a->off[4] != 884736 + 384 ||
+      a->off[7] - a->off[6] != 73728 || a->off[8] - a->off[7] != 192 || a->off[9] - a->off[8] != 1920)
+    return hipErrorInvalidValue;                      // the fc segments must be contiguous, float4-aligned
+  const int fc_blocks = fc1_blocks(*a) + FC2_BLOCKS + FC_TAIL_BLOCKS;
   const int conv_blocks = C2_BLOCKS + C1_BLOCKS + 2;
   int blocks = conv_blocks + (a->mode == 1 ? 0 : fc_blocks);
   if (a->roles == 1) blocks = conv_blocks;

@@ -78,6 +78,27 @@ DEV float wave_sum(float v) {
   return v;
 }
 
+// Last-arrival detection over a whole grid, two levels: workgroup b adds to the counter of group
+// b % 8 (each counter on its own 128-B line), the last of each group adds to a top counter, and the
+// last of those is the grid's last arriver.  One counter taking ~800 atomics in a row serialised
+// them at the memory side (~4-5 us at the end of the SGD launch); 8 groups + 8 top arrivals cut the
+// queue by ~90x.  Counters re-arm themselves (every member has arrived when its group's last one
+// resets it), so a zeroed buffer of DMLC_TICKET_WORDS (api.h) uints serves every later launch.
+// Relaxed atomics, no fences: nothing is published THROUGH the ticket (callers order their own
+// data).  Call from ONE thread per workgroup; returns true in exactly one workgroup.
+DEV bool last_arrival(unsigned int* tk, int blk, int nblk) {
+  const int g = blk & 7;
+  const unsigned gsize = (unsigned)((nblk - g + 7) >> 3);
+  unsigned int* gc = tk + g * 32;
+  if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gsize - 1) return false;
+  __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned ngroups = (unsigned)(nblk < 8 ? nblk : 8);
+  unsigned int* top = tk + 8 * 32;
+  if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ngroups - 1) return false;
+  __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 // 16-byte chunk swizzle for [pixel][64 x bf16] LDS images (128-B rows): chunk c of pixel p is
 // stored at chunk slot c ^ (p & 7), spreading 16 consecutive pixels over all bank slots.
 DEV int swz128(int pix, int chunk) { return pix * 64 + ((chunk ^ (pix & 7)) << 3); }

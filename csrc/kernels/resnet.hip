@@ -785,13 +785,11 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
   __syncthreads();
   if (tid == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == (unsigned)gridDim.x - 1) {          // last block: publish the step
+    if (last_arrival(a.ticket, blockIdx.x, gridDim.x)) {   // last block: publish the step
       float* st = a.stats + (size_t)(step % a.stats_len) * 4;
       st[0] = (float)(step + 1);
       st[3] = lr;
       *a.step = step + 1;
-      __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

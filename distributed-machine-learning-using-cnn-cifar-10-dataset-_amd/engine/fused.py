@@ -44,6 +44,8 @@ def _ops():
 SEG_OFF = [s.offset for s in M.PARAM_SPECS]
 # batch rows per head workgroup (4, 8 or 16; DMLC_HEAD_ROWS overrides it for A/B runs)
 HEAD_ROWS = int(os.environ.get("DMLC_HEAD_ROWS", "4"))
+# int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
+TICKET_WORDS = 9 * 32
 SEG = {M.short(s.name): s for s in M.PARAM_SPECS}
 
 
@@ -154,7 +156,7 @@ class FusedCifarEngine:
         self.loss_part = z(B // HEAD_ROWS, dt=torch.float32)
         self.correct_part = z(B // HEAD_ROWS, dt=torch.int32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ticket = torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)   # two-level arrival counters
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
         self.logits_buf = z(B, 10, dt=torch.float32)
 

@@ -28,6 +28,7 @@ import torch
 from .. import config as C
 from ..models import resnet as R
 from ..ops import _ext
+from .fused import TICKET_WORDS
 
 OPS = None
 
@@ -157,7 +158,7 @@ class FusedResNetEngine:
         self.correct_img = z(B, dt=torch.int32)
         self.logits_buf = z(B, 10, dt=torch.float32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ticket = torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)   # two-level arrival counters
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
