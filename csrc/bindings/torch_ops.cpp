@@ -220,7 +220,7 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
   TORCH_CHECK(B % 16 == 0 && B > 0, "head: batch must be a positive multiple of 16");
   TORCH_CHECK(loss_part.numel() >= 1 && B % loss_part.numel() == 0, "head: loss partials must divide the batch");
   const int64_t rows = B / loss_part.numel();      // rows per workgroup, picked by the caller
-  TORCH_CHECK(rows == 4 || rows == 8 || rows == 16, "head: B / loss_part.numel() must be 4, 8 or 16");
+  TORCH_CHECK(rows == 2 || rows == 4, "head: B / loss_part.numel() (rows per workgroup) must be 2 or 4");
   check(h1part, "h1part", at::kFloat, {nsplit, B, 384});
   check_numel(b1, "b1", at::kFloat, 384);
   check(w2t, "w2t", at::kBFloat16, {192, 384});

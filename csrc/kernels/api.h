@@ -121,7 +121,7 @@ struct DmlcGemmGroup {
   int nblocks;
 };
 
-// MLP head, rows-parallel (rows = 4, 8 or 16 per workgroup; B / rows workgroups): fc1 split-K reduce + bias + ReLU, fc2, fc3,
+// MLP head, rows-parallel (rows = 2 or 4 per workgroup; B / rows workgroups): fc1 split-K reduce + bias + ReLU, fc2, fc3,
 // (ReLU logits), softmax cross-entropy + accuracy, and (train) the backward through fc3/fc2.
 struct DmlcHeadArgs {
   const float* h1part; int nsplit;   // [nsplit][B][384]

@@ -4,24 +4,39 @@
 // Replaces /root/reference/cifar10cnn.py:130-176 (full1..full3, cifar_loss, batch_accuracy) and the
 // corresponding autodiff ops (SURVEY.md §2.B N7/N8/N10-N12, §2.C xent10_fwd_bwd + linear_bwd_dx).
 //
-// Rows-parallel: RB (4/8/16) batch rows per workgroup of 16 waves; everything per row stays in LDS.
-// The MFMA tiles keep 16 row columns (columns >= RB compute on zeros and are never stored): the head
-// is bound by how fast each CU pulls the ~300 KB of fc2 weights (both layouts), not by MFMA, so more
-// workgroups with fewer rows -- 8 per XCD sharing one L2 copy of the weights -- finish sooner.  Every
-// product is computed TRANSPOSED (C[feature][row]) so the weight fragment streams from L2 and each
-// lane ends up with 4 consecutive features of one row.  The weight fragments of a wave's output
-// tiles are loaded up front (fc2 at entry, behind the fc1 reduction; fc2^T right after the fc2
-// MFMAs, behind the loss phase), so each phase pays at most one exposed L2 latency.  Weight
-// *gradients* of fc1/fc2/fc3 need a reduction over the whole batch: the grouped GEMM kernel does them.
+// Rows-parallel: RB (2 or 4) batch rows per workgroup of 16 waves; everything per row stays in LDS.
+// What bounds this launch is the bytes every CU must pull in -- each workgroup needs ALL of fc2's
+// 384 x 192 weights, at the ~11-15 B/clk a CU gets from the fabric -- not MFMA work.  So the fc2
+// weight matrix is staged ONCE per workgroup into LDS (144 KB of the 160 KB) and read there in both
+// orientations: row fragments (ds_read_b128) for h2 = h1 W2 and hardware-transposed fragments
+// (ds_read_b64_tr_b16) for dh1 = dh2 W2^T -- half the bytes of fetching fc2 and its transpose.
+// Every product is computed TRANSPOSED (C[feature][row]); the MFMA tiles keep 16 row columns and
+// lanes of rows >= RB read a zero LDS row (their columns compute zeros and are never stored).
+// Small operands (biases, fc3 fragments) are fetched at entry: a load issued inside a phase is an
+// exposed memory latency on the serial chain.  Weight *gradients* of fc1/fc2/fc3 need a reduction
+// over the whole batch: the grouped GEMM kernel does them.
 #include "common.h"
 #include "api.h"
 
 namespace dmlc {
 
 constexpr int HT = 1024;     // 16 waves
+constexpr int W2_LD = 392;   // fc2 weights in LDS, [192 n][384 k] rows of 784 B (b128 row reads conflict-free)
 constexpr int H1_LD = 392;   // 784-B rows: 16-B aligned, rows land on distinct bank slots
 constexpr int H2_LD = 200;   // 400-B rows
 constexpr int DL_LD = 40;    // 80-B rows (k padded to 32 with zeros)
+
+template <int RB>
+struct HeadLds {             // byte offsets into the dynamic LDS; RB real rows + one zero row
+  static constexpr int W2 = 0;
+  static constexpr int H1 = W2 + 192 * W2_LD * 2;
+  static constexpr int H2 = H1 + (RB + 1) * H1_LD * 2;
+  static constexpr int DH2 = H2 + (RB + 1) * H2_LD * 2;
+  static constexpr int DL = DH2 + (RB + 1) * H2_LD * 2;
+  static constexpr int LG = DL + (RB + 1) * DL_LD * 2;
+  static constexpr int BYTES = LG + 16 * 17 * 4;
+  static_assert(BYTES <= 160 * 1024, "head LDS exceeds the 160 KB of a CU");
+};
 
 DEV int head_index(const DmlcIndexSrc& s, int B, int b) {
   int row = 0;
@@ -36,113 +51,108 @@ DEV bf16x4 relu_mask4(const f32x4& acc, const bf16x4& h) {
 
 template <int RB>
 __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 h1s[16 * H1_LD];
-  __shared__ __attribute__((aligned(16))) bf16 h2s[16 * H2_LD];
-  __shared__ __attribute__((aligned(16))) bf16 dh2s[16 * H2_LD];
-  __shared__ __attribute__((aligned(16))) bf16 dls[16 * DL_LD];
-  __shared__ float lg[16][17];
+  using L = HeadLds<RB>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* w2s = reinterpret_cast<bf16*>(smem + L::W2);
+  bf16* h1s = reinterpret_cast<bf16*>(smem + L::H1);
+  bf16* h2s = reinterpret_cast<bf16*>(smem + L::H2);
+  bf16* dh2s = reinterpret_cast<bf16*>(smem + L::DH2);
+  bf16* dls = reinterpret_cast<bf16*>(smem + L::DL);
+  float (*lg)[17] = reinterpret_cast<float (*)[17]>(smem + L::LG);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int r0 = blockIdx.x * RB;
   const bool rv = li < RB;                      // this lane's row column is a real batch row
+  const int rr = rv ? li : RB;                  // LDS row it reads (RB = the zero row)
   DMLC_STAMP(DMLC_TK_HEAD, 0);
 
   // the loss wave's labels (counter -> index -> label chain) are fetched at entry
   int label = 0;
   if (w == 12 && lane < RB) label = a.labels[head_index(a.src, a.B, r0 + lane)];
 
-  // fc2 weight fragments of this wave's output tile (waves 0..11: features 16w..16w+15), in flight
-  // while the fc1 partial sums are reduced
-  bf16x8 w2f[12];
-  if (w < 12) {
-    const bf16* W = reinterpret_cast<const bf16*>(a.w2t) + (16 * w + li) * 384 + 8 * g;
+  // fc2 weights (a.w2t = [192 n][384 k]) -> LDS: 9216 chunks of 16 B, 9 per thread, all in flight
+  constexpr int WCH = 192 * 48 / HT;
+  uint4 wv[WCH];
 #pragma unroll
-    for (int ks = 0; ks < 12; ++ks) w2f[ks] = glb_b128(W + ks * 32);
+  for (int i = 0; i < WCH; ++i) {
+    const int c = tid + i * HT;
+    wv[i] = *(reinterpret_cast<const uint4*>(a.w2t) + c);
+  }
+  // small operands of the later phases
+  const float4 b2v = w < 12 ? *reinterpret_cast<const float4*>(a.b2 + 16 * w + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+  bf16x8 w3f[6], w3d;
+  float b3v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (w < 12 && a.train) w3d = glb_b128(reinterpret_cast<const bf16*>(a.w3d) + (16 * w + li) * 32 + 8 * g);
+  if (w == 12) {
+    const bf16* W = reinterpret_cast<const bf16*>(a.w3t) + li * 192 + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) w3f[ks] = glb_b128(W + ks * 32);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b3v[i] = load_sel(a.b3 + 4 * g + i, a.b3, 4 * g + i < 10);
   }
 
-  // (a) h1 = relu(sum_s part[s] + b1): RB x 96 float4, at most 2 per thread; rows RB..15 of the LDS
-  // tile are zeroed (their MFMA columns then compute on zeros).
+  // (a) h1 = relu(sum_s part[s] + b1): RB x 96 float4, one per thread (threads < RB * 96)
   {
-    constexpr int U = (RB * 96 + HT - 1) / HT;
-    float4 acc[U];
-    int e[U];
+    const bool act = tid < RB * 96;
+    const int ec = act ? tid : 0;                             // branch-free: clamp, discard later
+    const int r = ec / 96, n = (ec - r * 96) * 4;
+    float4 acc = *reinterpret_cast<const float4*>(a.b1 + n);
+    const float* hp = a.h1part + (size_t)(r0 + r) * 384 + n;
+    const size_t sstride = (size_t)a.B * 384;
+    int sp = 0;
+    for (; sp + 4 <= a.nsplit; sp += 4) {
+      float4 v[4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      e[u] = tid + u * HT;
-      const int ec = e[u] < RB * 96 ? e[u] : 0;               // branch-free: clamp, discard later
-      const int r = ec / 96, n = (ec - r * 96) * 4;
-      acc[u] = *reinterpret_cast<const float4*>(a.b1 + n);
-      const float* hp = a.h1part + (size_t)(r0 + r) * 384 + n;
-      const size_t sstride = (size_t)a.B * 384;
-      int sp = 0;
-      for (; sp + 4 <= a.nsplit; sp += 4) {
-        float4 v[4];
+      for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(hp + (sp + k) * sstride);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(hp + (sp + k) * sstride);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { acc[u].x += v[k].x; acc[u].y += v[k].y; acc[u].z += v[k].z; acc[u].w += v[k].w; }
-      }
-      for (; sp < a.nsplit; ++sp) {
-        const float4 v = *reinterpret_cast<const float4*>(hp + sp * sstride);
-        acc[u].x += v.x; acc[u].y += v.y; acc[u].z += v.z; acc[u].w += v.w;
-      }
+      for (int k = 0; k < 4; ++k) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
     }
-    if (RB < 16) {
-      for (int z = tid; z < (16 - RB) * 96; z += HT)
-        *reinterpret_cast<bf16x4*>(h1s + (RB + z / 96) * H1_LD + (z % 96) * 4) = pack4(0.f, 0.f, 0.f, 0.f);
+    for (; sp < a.nsplit; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(hp + sp * sstride);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
+    // zero rows (row RB of every activation tile)
+    if (tid < 96) *reinterpret_cast<bf16x4*>(h1s + RB * H1_LD + tid * 4) = pack4(0.f, 0.f, 0.f, 0.f);
+    else if (tid < 144) *reinterpret_cast<bf16x4*>(h2s + RB * H2_LD + (tid - 96) * 4) = pack4(0.f, 0.f, 0.f, 0.f);
+    else if (tid < 192) *reinterpret_cast<bf16x4*>(dh2s + RB * H2_LD + (tid - 144) * 4) = pack4(0.f, 0.f, 0.f, 0.f);
+    else if (tid < 200) *reinterpret_cast<bf16x4*>(dls + RB * DL_LD + (tid - 192) * 4) = pack4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (e[u] < RB * 96) {
-        const int r = e[u] / 96, n = (e[u] - r * 96) * 4;
-        const bf16x4 o = pack4(fmaxf(acc[u].x, 0.f), fmaxf(acc[u].y, 0.f), fmaxf(acc[u].z, 0.f), fmaxf(acc[u].w, 0.f));
-        *reinterpret_cast<bf16x4*>(h1s + r * H1_LD + n) = o;
-        if (a.train) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.h1) + (size_t)(r0 + r) * 384 + n) = o;
-      }
+    for (int i = 0; i < WCH; ++i) {
+      const int c = tid + i * HT, n2 = c / 48, k8 = c - n2 * 48;
+      *reinterpret_cast<uint4*>(w2s + n2 * W2_LD + k8 * 8) = wv[i];
+    }
+    if (act) {
+      const bf16x4 o = pack4(fmaxf(acc.x, 0.f), fmaxf(acc.y, 0.f), fmaxf(acc.z, 0.f), fmaxf(acc.w, 0.f));
+      *reinterpret_cast<bf16x4*>(h1s + r * H1_LD + n) = o;
     }
   }
   lds_barrier();
   DMLC_STAMP(DMLC_TK_HEAD, 1);
 
-  // (b) h2 = relu(h1 W2 + b2): C[n][r] = sum_k W2t[n][k] h1[r][k]
+  // (b) h2 = relu(h1 W2 + b2): C[n][r] = sum_k W2t[n][k] h1[r][k], waves 0..11 = n tiles
   if (w < 12) {
     f32x4 acc = zero4();
+    const bf16* wa = w2s + (16 * w + li) * W2_LD + 8 * g;
 #pragma unroll
-    for (int ks = 0; ks < 12; ++ks) acc = mfma16(w2f[ks], lds_b128(h1s + li * H1_LD + ks * 32 + 8 * g), acc);
+    for (int ks = 0; ks < 12; ++ks) acc = mfma16(lds_b128(wa + ks * 32), lds_b128(h1s + rr * H1_LD + ks * 32 + 8 * g), acc);
     const int n = 16 * w + 4 * g;
-    const bf16x4 o = pack4(fmaxf(acc[0] + a.b2[n], 0.f), fmaxf(acc[1] + a.b2[n + 1], 0.f),
-                           fmaxf(acc[2] + a.b2[n + 2], 0.f), fmaxf(acc[3] + a.b2[n + 3], 0.f));
-    *reinterpret_cast<bf16x4*>(h2s + li * H2_LD + n) = o;
-    if (a.train && rv) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.h2) + (size_t)(r0 + li) * 192 + n) = o;
-  }
-  // fc2^T fragments for (f): tiles w and w+16 (w < 8) of the 24 dh1 feature tiles, K = 192
-  bf16x8 w2d[2][6];
-  if (a.train) {
-    const bf16* W = reinterpret_cast<const bf16*>(a.w2d);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j == 0 || w < 8) {
-        const bf16* Wr = W + (16 * (w + 16 * j) + li) * 192 + 8 * g;
-#pragma unroll
-        for (int ks = 0; ks < 6; ++ks) w2d[j][ks] = glb_b128(Wr + ks * 32);
-      }
-    }
+    const bf16x4 o = pack4(fmaxf(acc[0] + b2v.x, 0.f), fmaxf(acc[1] + b2v.y, 0.f),
+                           fmaxf(acc[2] + b2v.z, 0.f), fmaxf(acc[3] + b2v.w, 0.f));
+    if (rv) *reinterpret_cast<bf16x4*>(h2s + li * H2_LD + n) = o;
   }
   lds_barrier();
   DMLC_STAMP(DMLC_TK_HEAD, 2);
 
   // (c) logits = [relu](h2 W3 + b3): wave 12, one 16x16 tile, K = 192
   if (w == 12) {
-    const bf16* W = reinterpret_cast<const bf16*>(a.w3t);
     f32x4 acc = zero4();
 #pragma unroll
-    for (int ks = 0; ks < 6; ++ks)
-      acc = mfma16(glb_b128(W + li * 192 + ks * 32 + 8 * g), lds_b128(h2s + li * H2_LD + ks * 32 + 8 * g), acc);
+    for (int ks = 0; ks < 6; ++ks) acc = mfma16(w3f[ks], lds_b128(h2s + rr * H2_LD + ks * 32 + 8 * g), acc);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int n = 4 * g + i;
       if (n < 10) {
-        float v = acc[i] + a.b3[n];
+        float v = acc[i] + b3v[i];
         if (a.relu_logits) v = fmaxf(v, 0.f);
         lg[li][n] = v;
       }
@@ -150,13 +160,10 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
   }
   lds_barrier();
 
-  // (d) softmax cross-entropy, accuracy, dlogits (wave 12, lanes 0..15 = rows)
+  // (d) softmax cross-entropy, accuracy, dlogits (wave 12, lanes 0..RB-1 = rows)
+  float loss_w = 0.f, corr_w = 0.f;
   if (w == 12) {
     float loss = 0.f, corr = 0.f;
-    if (lane >= RB && lane < 16 && a.train) {
-#pragma unroll
-      for (int j = 0; j < 32; ++j) dls[lane * DL_LD + j] = (bf16)0.f;
-    }
     if (lane < RB) {
       const int b = r0 + lane;
       float m = lg[lane][0];
@@ -174,7 +181,6 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
         for (int j = 0; j < 10; ++j) a.logits_out[b * 10 + j] = lg[lane][j];
       }
       if (a.train) {
-        bf16* dlg = reinterpret_cast<bf16*>(a.dl) + (size_t)b * 16;
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
           float d = 0.f;
@@ -183,16 +189,17 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
             if (a.relu_logits && !(lg[lane][j] > 0.f)) d = 0.f;
           }
           dls[lane * DL_LD + j] = (bf16)d;
-          if (j < 16) dlg[j] = (bf16)d;
         }
       }
     }
     loss = wave_sum(loss);
     corr = wave_sum(corr);
-    if (lane == 0) {
+    if (lane == 0 && !a.train) {                   // eval: nothing follows
       a.loss_part[blockIdx.x] = loss;
       a.correct_part[blockIdx.x] = (int)(corr + 0.5f);
     }
+    loss_w = loss;
+    corr_w = corr;
   }
   if (!a.train) return;
   lds_barrier();
@@ -200,28 +207,66 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
 
   // (e) dh2 = (dl W3^T) * (h2 > 0): C[n][r] = sum_k W3d[n][k] dl[r][k], K = 32 (one step), waves 0..11
   if (w < 12) {
-    const bf16* W = reinterpret_cast<const bf16*>(a.w3d);
-    const f32x4 acc = mfma16(glb_b128(W + (16 * w + li) * 32 + 8 * g), lds_b128(dls + li * DL_LD + 8 * g), zero4());
+    const f32x4 acc = mfma16(w3d, lds_b128(dls + rr * DL_LD + 8 * g), zero4());
     const int n = 16 * w + 4 * g;
-    const bf16x4 o = relu_mask4(acc, *reinterpret_cast<const bf16x4*>(h2s + li * H2_LD + n));
-    *reinterpret_cast<bf16x4*>(dh2s + li * H2_LD + n) = o;
-    if (rv) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh2) + (size_t)(r0 + li) * 192 + n) = o;
+    const bf16x4 o = relu_mask4(acc, *reinterpret_cast<const bf16x4*>(h2s + rr * H2_LD + n));
+    if (rv) *reinterpret_cast<bf16x4*>(dh2s + li * H2_LD + n) = o;
   }
   lds_barrier();
   DMLC_STAMP(DMLC_TK_HEAD, 4);
 
-  // (f) dh1 = (dh2 W2^T) * (h1 > 0): tiles w and w+16, K = 192
+  // (f) dh1 = (dh2 W2^T) * (h1 > 0): C[k][r] = sum_n W2[k][n] dh2[r][n], k tiles w and w+16 (w < 8),
+  // K = 192.  The A fragment (lane li: k = k0 + li, n = 32 ks + 8 g + j) is a column of the [n][k]
+  // LDS image: two ds_read_b64_tr_b16 per fragment (wave-uniform control flow: EXEC all ones).
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     if (j == 1 && w >= 8) break;
+    const int k0 = 16 * (w + 16 * j);
     f32x4 acc = zero4();
 #pragma unroll
-    for (int ks = 0; ks < 6; ++ks) acc = mfma16(w2d[j][ks], lds_b128(dh2s + li * H2_LD + ks * 32 + 8 * g), acc);
-    const int n = 16 * (w + 16 * j) + 4 * g;
-    const bf16x4 o = relu_mask4(acc, *reinterpret_cast<const bf16x4*>(h1s + li * H1_LD + n));
+    for (int ks = 0; ks < 6; ++ks) {
+      const bf16x8 af = tr_frag(w2s + (32 * ks + 8 * g + q) * W2_LD + k0 + 4 * p,
+                                w2s + (32 * ks + 8 * g + 4 + q) * W2_LD + k0 + 4 * p);
+      acc = mfma16(af, lds_b128(dh2s + rr * H2_LD + ks * 32 + 8 * g), acc);
+    }
+    const int n = k0 + 4 * g;
+    const bf16x4 o = relu_mask4(acc, *reinterpret_cast<const bf16x4*>(h1s + rr * H1_LD + n));
     if (rv) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.dh1) + (size_t)(r0 + li) * 384 + n) = o;
   }
+  // (g) the intermediates the fc weight-gradient GEMMs read (h1, h2, dl, dh2) and the loss partials
+  // leave last, from LDS: vmcnt counts stores too, so a global store issued ahead of a load the wave
+  // later waits for holds that wait until the store is acknowledged.
+  if (w == 12 && lane == 0) {
+    a.loss_part[blockIdx.x] = loss_w;
+    a.correct_part[blockIdx.x] = (int)(corr_w + 0.5f);
+  }
+  for (int c = tid; c < RB * 98; c += HT) {       // per row: 48 + 24 + 24 + 2 chunks of 16 B
+    const int r = c / 98, qq = c - r * 98;
+    const bf16* src;
+    bf16* dst;
+    if (qq < 48) { src = h1s + r * H1_LD + 8 * qq; dst = reinterpret_cast<bf16*>(a.h1) + (size_t)(r0 + r) * 384 + 8 * qq; }
+    else if (qq < 72) {
+      src = h2s + r * H2_LD + 8 * (qq - 48); dst = reinterpret_cast<bf16*>(a.h2) + (size_t)(r0 + r) * 192 + 8 * (qq - 48);
+    } else if (qq < 96) {
+      src = dh2s + r * H2_LD + 8 * (qq - 72); dst = reinterpret_cast<bf16*>(a.dh2) + (size_t)(r0 + r) * 192 + 8 * (qq - 72);
+    } else {
+      src = dls + r * DL_LD + 8 * (qq - 96); dst = reinterpret_cast<bf16*>(a.dl) + (size_t)(r0 + r) * 16 + 8 * (qq - 96);
+    }
+    *reinterpret_cast<bf16x8*>(dst) = lds_b128(src);
+  }
   DMLC_STAMP(DMLC_TK_HEAD, 5);
+}
+
+template <int RB>
+hipError_t launch_head(const DmlcHeadArgs* a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_head<RB>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              HeadLds<RB>::BYTES);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_head<RB>, dim3(a->B / RB), dim3(HT), HeadLds<RB>::BYTES, s, *a);
+  return hipGetLastError();
 }
 
 }  // namespace dmlc
@@ -230,10 +275,8 @@ using namespace dmlc;
 
 extern "C" hipError_t dmlc_head(const DmlcHeadArgs* a, hipStream_t s) {
   switch (a->rows) {
-    case 4: hipLaunchKernelGGL(k_head<4>, dim3(a->B / 4), dim3(HT), 0, s, *a); break;
-    case 8: hipLaunchKernelGGL(k_head<8>, dim3(a->B / 8), dim3(HT), 0, s, *a); break;
-    case 16: hipLaunchKernelGGL(k_head<16>, dim3(a->B / 16), dim3(HT), 0, s, *a); break;
+    case 2: return launch_head<2>(a, s);
+    case 4: return launch_head<4>(a, s);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }

@@ -130,6 +130,17 @@ extern __device__ unsigned long long dmlc_timing_buf[DMLC_TK_N * DMLC_TK_BLOCKS 
 #else
 #define DMLC_STAMP(k, slot) do {} while (0)
 #endif
+// DMLC_STAMP_T(kernel, slot, thread): the same, recorded by thread `thread` (another wave's view)
+#ifdef DMLC_TIMING
+#define DMLC_STAMP_T(k, slot, t)                                                                     \
+  do {                                                                                               \
+    if (threadIdx.x == (t) && blockIdx.x < DMLC_TK_BLOCKS)                                           \
+      dmlc_timing_buf[((k) * DMLC_TK_BLOCKS + blockIdx.x) * DMLC_TK_SLOTS + (slot)] =               \
+          __builtin_amdgcn_s_memrealtime();                                                          \
+  } while (0)
+#else
+#define DMLC_STAMP_T(k, slot, t) do {} while (0)
+#endif
 
 // ---- branch-free guarded loads --------------------------------------------------------------------
 // `if (ok) v = *p;` makes hipcc branch around the load and wait vmcnt(0) inside the branch, which

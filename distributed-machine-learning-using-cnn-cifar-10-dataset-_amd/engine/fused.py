@@ -42,7 +42,7 @@ def _ops():
 
 
 SEG_OFF = [s.offset for s in M.PARAM_SPECS]
-# batch rows per head workgroup (4, 8 or 16; DMLC_HEAD_ROWS overrides it for A/B runs)
+# batch rows per head workgroup (2 or 4; DMLC_HEAD_ROWS overrides it for A/B runs)
 HEAD_ROWS = int(os.environ.get("DMLC_HEAD_ROWS", "4"))
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
