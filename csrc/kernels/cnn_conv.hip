@@ -115,34 +115,33 @@ constexpr int C2_XIN = 256 * 64;
 constexpr int C2_OUT = 144 * 64;
 
 // conv2-shaped implicit GEMM core, weights staged through LDS.
-// The 64 x 1600 weight matrix is consumed one kh slice (64 co x 320 k, 42 KB with padded rows) at a
-// time: all 512 threads load the slice for kh+1 from L2 into registers while the MFMAs of slice kh
-// run, then store it to the other LDS buffer -- every weight byte crosses L2->CU once per block
-// (streaming it per wave into registers re-read each co tile 2-4x and was L2-bandwidth bound).
+// The 64 x 1600 weight matrix is consumed one kh slice (64 co x 320 k, 40 KB) at a time.  Each slice
+// is copied global -> LDS by LDS-DMA (global_load_lds_dwordx4: 40 wave-instructions of 1 KB, 5 per
+// wave, no registers), issued for slice kh+1 into the other buffer before slice kh's MFMAs and
+// waited for at the end of the slice -- the copy is hidden behind the MFMAs.  (Register-staged, the
+// compiler sank the loads down to their LDS stores -- one exposed L2 latency per slice -- and pinning
+// them spilled the staging registers to scratch.)  Every weight byte crosses L2 -> CU once per block.
+// Rows are 640 B with the 16-B chunks XOR-swizzled by (row & 7), which keeps the A-fragment reads
+// (16 co rows x 4 chunks per ds_read_b128) conflict-free.
 // Wave w owns c_out tiles 2cp, 2cp+1 (cp = w & 1) and pixel tiles pg, pg+4, pg+8 (< 9), pg = w >> 1:
 // per k-chunk it reads 2 A and 2-3 B fragments (ds_read_b128, conflict-free) for 4-6 MFMAs.
-constexpr int WS_LD = 328;                    // 656-B rows: 16 co rows of a fragment hit distinct banks
-constexpr int WS_ELEMS = 64 * WS_LD;
+constexpr int WS_ELEMS = 64 * 320;            // one slice, bf16
 constexpr size_t WS_BYTES = 2 * WS_ELEMS * 2;
 
-DEV void ws_load(uint4 (&v)[5], const bf16* __restrict__ Wg, int kh, int tid) {
+// slice kh of W[64 co][1600] -> LDS slice buffer (physical chunk P = row*40 + (lc ^ (row & 7)))
+DEV void ws_dma(const bf16* Wg, int kh, bf16* buf, int w, int lane) {
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    const int c = tid + i * NT, row = c / 40, k8 = c - row * 40;
-    v[i] = *reinterpret_cast<const uint4*>(Wg + row * 1600 + kh * 320 + k8 * 8);
-  }
-}
-DEV void ws_store(const uint4 (&v)[5], bf16* ws, int tid) {
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const int c = tid + i * NT, row = c / 40, k8 = c - row * 40;
-    *reinterpret_cast<uint4*>(ws + row * WS_LD + k8 * 8) = v[i];
+    const int j = w * 5 + i;                            // wave-uniform: 1 KB of LDS per instruction
+    const int P = j * 64 + lane, row = P / 40, pc = P - row * 40, lc = pc ^ (row & 7);
+    __builtin_amdgcn_global_load_lds(Wg + row * 1600 + kh * 320 + lc * 8, (LDS_AS void*)(buf + j * 512), 16, 0, 0);
   }
 }
 
 template <int NPX>
-DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][NPX], int pg, int cp,
+DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][NPX], int pg, int cp,
                     int g, int li, int tid) {
+  const int w = tid >> 6, lane = tid & 63, sw = li & 7;
   int pb[NPX];
 #pragma unroll
   for (int t = 0; t < NPX; ++t) {
@@ -152,20 +151,20 @@ DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, bf16* ws, f32x
   }
 #pragma unroll
   for (int t = 0; t < NPX; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
-  uint4 pf[5];
-  ws_load(pf, Wg, 0, tid);
-  ws_store(pf, ws, tid);
-  __syncthreads();
+  ws_dma(Wg, 0, ws, w, lane);
+  __syncthreads();                                       // (waits vmcnt(0): the DMA has landed)
 #pragma unroll
   for (int kh = 0; kh < 5; ++kh) {
-    ws_load(pf, Wg, kh < 4 ? kh + 1 : 4, tid);        // next slice in flight during this one
-    const bf16* wsb = ws + (kh & 1) * WS_ELEMS + (32 * cp + li) * WS_LD + 8 * g;
+    if (kh < 4) ws_dma(Wg, kh + 1, ws + ((kh + 1) & 1) * WS_ELEMS, w, lane);   // buffer freed by the last barrier
+    const bf16* wr0 = ws + (kh & 1) * WS_ELEMS + (32 * cp + li) * 320;
+    const bf16* wr1 = wr0 + 16 * 320;
 #pragma unroll
     for (int kw = 0; kw < 5; ++kw) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const bf16x8 a0 = lds_b128(wsb + kw * 64 + s * 32);
-        const bf16x8 a1 = lds_b128(wsb + 16 * WS_LD + kw * 64 + s * 32);
+        const int c = ((kw * 8 + s * 4 + g) ^ sw) * 8;
+        const bf16x8 a0 = lds_b128(wr0 + c);
+        const bf16x8 a1 = lds_b128(wr1 + c);
 #pragma unroll
         for (int t = 0; t < NPX; ++t) {
           const bf16x8 bx = lds_b128(xin + swz128(pb[t] + kh * 16 + kw, 4 * s + g));
@@ -174,8 +173,7 @@ DEV void conv2_core(const bf16* __restrict__ Wg, const bf16* xin, bf16* ws, f32x
         }
       }
     }
-    ws_store(pf, ws + ((kh + 1) & 1) * WS_ELEMS, tid);   // (kh == 4: harmless rewrite of slice 4)
-    __syncthreads();
+    if (kh < 4) __syncthreads();                         // next slice landed; this one fully read
   }
 }
 
