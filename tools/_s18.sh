@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 200 python tools/rn_kbench.py > gpurun_out/rnk.json 2> gpurun_out/rnk.err || { tail gpurun_out/rnk.err; exit 1; }
+timeout -k 10 200 python bench.py --model resnet20 --steps 100 --warmup 10 > gpurun_out/bench_rn.log 2>&1 || { tail -20 gpurun_out/bench_rn.log; exit 1; }
+echo done
