@@ -130,29 +130,47 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
   }
   DMLC_STAMP(DMLC_TK_GEMM, 1);
 
-  // epilogue: acc[i][j] holds C[m0+32wm+16i+4g+r][n0+32wn+16j+li]
+  // epilogue: acc[i][j] holds C[m0+32wm+16i+4g+r][n0+32wn+16j+li] -- 4 rows of ONE column per lane,
+  // i.e. 4-byte stores scattered over rows.  The tile goes through LDS instead ([64][68] fp32 over
+  // the A buffers, free once every wave is past the last chunk) and leaves as 16-B row vectors.
+  float* ct = reinterpret_cast<float*>(smem);
+  constexpr int CT_LD = 68;
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + 32 * wn + 16 * j + li;
-      if (n >= P.nvalid) continue;
-      const float bn = P.bias ? P.bias[n] : 0.f;
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 32 * wm + 16 * i + 4 * g + r;
-        if (m >= P.M) continue;
-        float v = acc[i][j][r];
-        if (P.c_mode == 2) {
-          reinterpret_cast<float*>(P.C)[(size_t)split * P.M * P.ldc + (size_t)m * P.ldc + n] = v;
-          continue;
-        }
-        v += bn;
-        if (P.relu) v = fmaxf(v, 0.f);
-        if (P.c_mode == 0) reinterpret_cast<float*>(P.C)[(size_t)m * P.ldc + n] = v;
-        else reinterpret_cast<bf16*>(P.C)[(size_t)m * P.ldc + n] = (bf16)v;
+      for (int r = 0; r < 4; ++r) ct[(32 * wm + 16 * i + 4 * g + r) * CT_LD + 32 * wn + 16 * j + li] = acc[i][j][r];
+  __syncthreads();
+  const bool vec = (P.ldc & 3) == 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = tid + u * 256, rr = e >> 4, cc = (e & 15) * 4;
+    const int m = m0 + rr, n = n0 + cc;
+    if (m >= P.M || n >= P.nvalid) continue;
+    float4 v = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
+    float vv[4] = {v.x, v.y, v.z, v.w};
+    if (P.c_mode != 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        vv[k] += (P.bias && n + k < P.nvalid) ? P.bias[n + k] : 0.f;
+        if (P.relu) vv[k] = fmaxf(vv[k], 0.f);
       }
     }
+    const size_t base = (P.c_mode == 2 ? (size_t)split * P.M * P.ldc : 0) + (size_t)m * P.ldc + n;
+    if (vec && n + 4 <= P.nvalid) {
+      if (P.c_mode == 1) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(P.C) + base) = pack4(vv[0], vv[1], vv[2], vv[3]);
+      else *reinterpret_cast<float4*>(reinterpret_cast<float*>(P.C) + base) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (n + k >= P.nvalid) break;
+        if (P.c_mode == 1) reinterpret_cast<bf16*>(P.C)[base + k] = (bf16)vv[k];
+        else reinterpret_cast<float*>(P.C)[base + k] = vv[k];
+      }
+    }
+  }
   DMLC_STAMP(DMLC_TK_GEMM, 2);
 }
 
