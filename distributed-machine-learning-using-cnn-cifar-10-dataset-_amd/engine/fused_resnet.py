@@ -165,8 +165,11 @@ class FusedResNetEngine:
         self.side_stream = torch.cuda.Stream(device=dev)
         if wgrad_branch is None:
             import os
-            wgrad_branch = os.environ.get("DMLC_RN_WGRAD_BRANCH", "1") == "1"
-        self.wgrad_branch = wgrad_branch     # wgrads on a second stream / graph branch
+            wgrad_branch = os.environ.get("DMLC_RN_WGRAD_BRANCH", "0") == "1"
+        # wgrads on a second stream / graph branch: faster launched eagerly (658 vs 692 us/step), but
+        # the 19 fork/join edges cost more than the overlap inside a HIP graph (751 vs 698 us/step,
+        # 336 k vs 364 k img/s at B=256) -- off by default
+        self.wgrad_branch = wgrad_branch
         self.host_step = 0
         self.refresh_shadows()
 
