@@ -77,11 +77,11 @@ void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::o
   CHECK_HIP(dmlc_rn_fwd(&gc, &a, stream_of(z)));
 }
 
-void rn_dgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
-              const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
-              const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
-              const Tensor& gy_prev, const Tensor& red_prev) {
-  const Geom g = geom(cin, cout, hin, stride);
+DmlcRnDgradArgs dgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin, const Tensor& gy, const Tensor& z,
+                           const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd,
+                           const Tensor& a_prev, const Tensor& z_prev, const Tensor& stat_prev,
+                           const c10::optional<Tensor>& gy_sc, int64_t sc_mode, const Tensor& gy_prev,
+                           const Tensor& red_prev) {
   TORCH_CHECK(cin >= 16, "rn_dgrad: the stem has no input gradient");
   const int64_t B = gy.size(0), ho = g.hout();
   check(gy, "gy", at::kBFloat16, {B, ho, ho, cout});
@@ -108,16 +108,26 @@ void rn_dgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tens
   a.inv_n_prev = 1.f / (float)(B * hin * hin);
   a.gy_sc = sc_mode ? gy_sc->data_ptr() : nullptr; a.sc_mode = (int)sc_mode;
   a.gy_prev = gy_prev.data_ptr(); a.red_prev = red_prev.data_ptr<double>(); a.B = (int)B;
+  return a;
+}
+
+void rn_dgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
+              const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
+              const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
+              const Tensor& gy_prev, const Tensor& red_prev) {
+  const Geom g = geom(cin, cout, hin, stride);
+  const DmlcRnDgradArgs a = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
+                                       gy_sc, sc_mode, gy_prev, red_prev);
   c10::DeviceGuard guard(gy.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_dgrad(&gc, &a, stream_of(gy)));
 }
 
-void rn_wgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::optional<Tensor>& data,
-              const c10::optional<Tensor>& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
-              int64_t cx, const c10::optional<Tensor>& x, const Tensor& gy, const Tensor& z, const Tensor& stat,
-              const Tensor& red, const Tensor& gamma, const Tensor& part) {
-  const Geom g = geom(cin, cout, hin, stride);
+DmlcRnWgradArgs wgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin,
+                           const c10::optional<Tensor>& data, const c10::optional<Tensor>& idx,
+                           const c10::optional<Tensor>& counter, int64_t period, int64_t cy, int64_t cx,
+                           const c10::optional<Tensor>& x, const Tensor& gy, const Tensor& z, const Tensor& stat,
+                           const Tensor& red, const Tensor& gamma, const Tensor& part) {
   const int64_t B = gy.size(0), ho = g.hout(), G = part.size(0);
   check(gy, "gy", at::kBFloat16, {B, ho, ho, cout});
   check(z, "z", at::kBFloat16, {B, ho, ho, cout});
@@ -140,9 +150,34 @@ void rn_wgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10:
   a.gy = gy.data_ptr(); a.z = z.data_ptr(); a.stat = stat.data_ptr<double>(); a.red = red.data_ptr<double>();
   a.gamma = gamma.data_ptr<float>(); a.inv_n = 1.f / (float)(B * ho * ho);
   a.part = part.data_ptr<float>(); a.G = (int)G; a.B = (int)B;
+  return a;
+}
+
+void rn_wgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::optional<Tensor>& data,
+              const c10::optional<Tensor>& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
+              int64_t cx, const c10::optional<Tensor>& x, const Tensor& gy, const Tensor& z, const Tensor& stat,
+              const Tensor& red, const Tensor& gamma, const Tensor& part) {
+  const Geom g = geom(cin, cout, hin, stride);
+  const DmlcRnWgradArgs a = wgrad_args(g, cin, cout, hin, data, idx, counter, period, cy, cx, x, gy, z, stat, red,
+                                       gamma, part);
   c10::DeviceGuard guard(gy.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_wgrad(&gc, &a, stream_of(gy)));
+}
+
+// dgrad + wgrad of one (non-stem) layer in one launch; the wgrad's input is the dgrad's a_prev
+void rn_bwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
+            const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
+            const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
+            const Tensor& gy_prev, const Tensor& red_prev, const Tensor& part) {
+  const Geom g = geom(cin, cout, hin, stride);
+  const DmlcRnDgradArgs d = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
+                                       gy_sc, sc_mode, gy_prev, red_prev);
+  const DmlcRnWgradArgs w = wgrad_args(g, cin, cout, hin, c10::nullopt, c10::nullopt, c10::nullopt, 1, 0, 0, a_prev, gy,
+                                       z, stat, red, gamma, part);
+  c10::DeviceGuard guard(gy.device());
+  const DmlcRnLayerGeom gc = g.c();
+  CHECK_HIP(dmlc_rn_bwd(&gc, &d, &w, stream_of(gy)));
 }
 
 void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Tensor& beta, const Tensor& sc,
@@ -268,6 +303,9 @@ TORCH_LIBRARY_FRAGMENT(dmlc, m) {
   m.def("rn_wgrad(int cin, int cout, int hin, int stride, Tensor? data, Tensor? idx, Tensor? counter, int period, "
         "int cy, int cx, Tensor? x, Tensor gy, Tensor z, Tensor stat, Tensor red, Tensor gamma, "
         "Tensor(a!) part) -> ()");
+  m.def("rn_bwd(int cin, int cout, int hin, int stride, Tensor gy, Tensor z, Tensor stat, Tensor red, "
+        "Tensor gamma, Tensor wd, Tensor a_prev, Tensor z_prev, Tensor stat_prev, Tensor? gy_sc, int sc_mode, "
+        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part) -> ()");
   m.def("rn_head(Tensor z, Tensor stat, Tensor gamma, Tensor beta, Tensor sc, Tensor fcw, Tensor fcb, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, Tensor(a!) gy, Tensor(b!) red, "
         "Tensor(c!) fc_part, Tensor(d!) loss_img, Tensor(e!) correct_img, Tensor(f!)? logits) -> ()");
@@ -282,6 +320,7 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("rn_fwd", &rn_fwd);
   m.impl("rn_dgrad", &rn_dgrad);
   m.impl("rn_wgrad", &rn_wgrad);
+  m.impl("rn_bwd", &rn_bwd);
   m.impl("rn_head", &rn_head);
   m.impl("rn_sgd", &rn_sgd);
 }

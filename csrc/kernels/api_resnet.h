@@ -90,6 +90,8 @@ struct DmlcRnSgdArgs {
 hipError_t dmlc_rn_fwd(const DmlcRnLayerGeom* g, const DmlcRnFwdArgs* a, hipStream_t s);
 hipError_t dmlc_rn_dgrad(const DmlcRnLayerGeom* g, const DmlcRnDgradArgs* a, hipStream_t s);
 hipError_t dmlc_rn_wgrad(const DmlcRnLayerGeom* g, const DmlcRnWgradArgs* a, hipStream_t s);
+// dgrad (workgroups [0, B)) + wgrad (the rest) of one layer in one launch
+hipError_t dmlc_rn_bwd(const DmlcRnLayerGeom* g, const DmlcRnDgradArgs* d, const DmlcRnWgradArgs* w, hipStream_t s);
 hipError_t dmlc_rn_head(const DmlcRnHeadArgs* a, hipStream_t s);
 hipError_t dmlc_rn_sgd(DmlcRnSgdArgs* a, hipStream_t s);
 

@@ -263,7 +263,7 @@ struct Dg {
 };
 
 template <int CIN, int COUT, int HIN, int S>
-__global__ __launch_bounds__(RT) void k_rn_dgrad(DmlcRnDgradArgs a) {
+DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = image (grid starts with these)
   using D = Dg<CIN, COUT, HIN, S>;
   constexpr int HOUT = D::HOUT, HPD = D::HPD, KPD = D::KPD, C8 = COUT / 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -417,7 +417,7 @@ struct Wg {
 };
 
 template <int CIN, int COUT, int HIN, int S>
-__global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
+DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
   using G = Wg<CIN, COUT, HIN, S>;
   constexpr int CINP = G::CINP, HP = G::HP, HOUT = G::HOUT, KP = G::KP, NT = G::NT, GLD = G::GLD, NB = G::NB;
   constexpr int C8 = COUT / 8;
@@ -426,7 +426,6 @@ __global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
   bf16* gz = xs + NB * G::XE;                                     // [NB][GE]
   float* cf = reinterpret_cast<float*>(gz + NB * G::GE);          // [3][64]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int grp = blockIdx.x, mc = blockIdx.y;
   const int b0 = grp * a.B / a.G, b1 = (grp + 1) * a.B / a.G;
 
   if (tid < COUT) {
@@ -548,6 +547,28 @@ __global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) out[(16 * m + 4 * g + i) * COUT + 16 * n + li] = acc[j][n][i];
     }
+  }
+}
+
+template <int CIN, int COUT, int HIN, int S>
+__global__ __launch_bounds__(RT) void k_rn_dgrad(DmlcRnDgradArgs a) { rn_dgrad_body<CIN, COUT, HIN, S>(a); }
+
+template <int CIN, int COUT, int HIN, int S>
+__global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
+  rn_wgrad_body<CIN, COUT, HIN, S>(a, blockIdx.x, blockIdx.y);
+}
+
+// Layer l's input gradient AND weight gradient in ONE launch (both only read what layer l+1's dgrad
+// produced): workgroups [0, B) run the dgrad body (one image each, the same blockIdx as its own
+// launch, so the BN-reduction slots are unchanged), the rest the wgrad body (group, m-chunk).  One
+// launch per layer instead of two, with no stream fork/join in the step graph.
+template <int CIN, int COUT, int HIN, int S>
+__global__ __launch_bounds__(RT) void k_rn_bwd(DmlcRnDgradArgs d, DmlcRnWgradArgs w) {
+  if ((int)blockIdx.x < d.B) {
+    rn_dgrad_body<CIN, COUT, HIN, S>(d);
+  } else {
+    const int t = (int)blockIdx.x - d.B;
+    rn_wgrad_body<CIN, COUT, HIN, S>(w, t % w.G, t / w.G);
   }
 }
 
@@ -839,6 +860,21 @@ hipError_t launch_dgrad(const DmlcRnDgradArgs& a, hipStream_t s) {
 }
 
 template <int CI, int CO, int H, int ST>
+hipError_t launch_bwd(const DmlcRnDgradArgs& d, const DmlcRnWgradArgs& w, hipStream_t s) {
+  if constexpr (CI < 16) {
+    return hipErrorInvalidValue;             // the stem has no input gradient
+  } else {
+    using D = Dg<CI, CO, H, ST>;
+    using G = Wg<CI, CO, H, ST>;
+    constexpr size_t lds = D::LDS > G::LDS ? D::LDS : G::LDS;
+    static bool once = false;
+    if (!once) { set_lds(&k_rn_bwd<CI, CO, H, ST>, lds); once = true; }
+    hipLaunchKernelGGL((k_rn_bwd<CI, CO, H, ST>), dim3(d.B + w.G * G::MC), dim3(RT), lds, s, d, w);
+    return hipGetLastError();
+  }
+}
+
+template <int CI, int CO, int H, int ST>
 hipError_t launch_wgrad(const DmlcRnWgradArgs& a, hipStream_t s) {
   using G = Wg<CI, CO, H, ST>;
   static bool once = false;
@@ -870,6 +906,15 @@ hipError_t dmlc_rn_dgrad(const DmlcRnLayerGeom* g, const DmlcRnDgradArgs* a, hip
 hipError_t dmlc_rn_wgrad(const DmlcRnLayerGeom* g, const DmlcRnWgradArgs* a, hipStream_t s) {
 #define X(CI, CO, H, ST) \
   if (g->cin == CI && g->cout == CO && g->hin == H && g->stride == ST) return launch_wgrad<CI, CO, H, ST>(*a, s);
+  DMLC_RN_SHAPES(X)
+#undef X
+  return hipErrorInvalidValue;
+}
+
+hipError_t dmlc_rn_bwd(const DmlcRnLayerGeom* g, const DmlcRnDgradArgs* d, const DmlcRnWgradArgs* w, hipStream_t s) {
+  if (d->B != w->B) return hipErrorInvalidValue;
+#define X(CI, CO, H, ST) \
+  if (CI >= 16 && g->cin == CI && g->cout == CO && g->hin == H && g->stride == ST) return launch_bwd<CI, CO, H, ST>(*d, *w, s);
   DMLC_RN_SHAPES(X)
 #undef X
   return hipErrorInvalidValue;

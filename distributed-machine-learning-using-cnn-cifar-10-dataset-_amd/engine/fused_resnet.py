@@ -11,7 +11,8 @@ all HIP kernels of csrc/kernels/resnet.hip, captured as one HIP graph:
   head           BN_18 + residual + ReLU + global average pool + fc + softmax-xent + its backward
   bwd  l=18..1   dgrad_l: g_z_l (BN backward, prologue) -> g_a_{l-1} (+ shortcut grad) -> ReLU mask
                  -> g_y_{l-1} and the BN_{l-1} reductions (epilogue)
-       l=18..0   wgrad_l on a side stream (a second graph branch), split-K fp32 slabs
+       l=18..0   wgrad_l, split-K fp32 slabs: in the same launch as dgrad_l (block roles), or on a
+                 side stream (a second graph branch, DMLC_RN_WGRAD_BRANCH=1)
   sgd            slab reduction + SGD (conv, BN gamma/beta, fc) + BN running statistics (momentum 0.1)
                  + bf16 weight shadows + global_step++ + stats ring
 
@@ -21,6 +22,7 @@ in two halves around ONE all-reduce of the 1.1 MB flat gradient (mode 1 -> RCCL 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -163,13 +165,18 @@ class FusedResNetEngine:
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.side_stream = torch.cuda.Stream(device=dev)
+        # Backward schedule, measured per batch size (graph replay, img/s on 1 MI355X):
+        #                          B=256   B=1024
+        #   merged dgrad+wgrad     376 k   508 k   one launch per layer, no fork/join edges
+        #   two launches, 1 stream 363 k   590 k
+        #   wgrads on a branch     336 k   620 k   19 fork/join edges in the graph
+        # The merged kernel runs at the occupancy of the larger (wgrad) body, which costs more than the
+        # saved launches once each layer has >= ~4 dgrad workgroups per CU; DMLC_RN_WGRAD_BRANCH /
+        # DMLC_RN_MERGED_BWD override the choice.
         if wgrad_branch is None:
-            import os
-            wgrad_branch = os.environ.get("DMLC_RN_WGRAD_BRANCH", "0") == "1"
-        # wgrads on a second stream / graph branch: faster launched eagerly (658 vs 692 us/step), but
-        # the 19 fork/join edges cost more than the overlap inside a HIP graph (751 vs 698 us/step,
-        # 336 k vs 364 k img/s at B=256) -- off by default
+            wgrad_branch = os.environ.get("DMLC_RN_WGRAD_BRANCH", "1" if B > 256 else "0") == "1"
         self.wgrad_branch = wgrad_branch
+        self.merged_bwd = os.environ.get("DMLC_RN_MERGED_BWD", "1" if B <= 256 else "0") == "1"
         self.host_step = 0
         self.refresh_shadows()
 
@@ -239,6 +246,19 @@ class FusedResNetEngine:
         o = self.ops
         main = torch.cuda.current_stream(self.device)
         side = self.side_stream if self.wgrad_branch else main
+        if side is main and self.merged_bwd:
+            # one launch per layer: dgrad_l and wgrad_l both only read what dgrad_{l+1} produced
+            for l in range(NL - 1, 0, -1):
+                _, ci, co, h, s = LAYERS[l]
+                sc_mode, gy_sc = 0, None
+                if l % 2 == 1:
+                    sc_mode = _block_sc_mode(l + 1)
+                    gy_sc = self.gy[l + 1]
+                o.rn_bwd(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
+                         self.a[l - 1], self.z[l - 1], self.stat[l - 1], gy_sc, sc_mode, self.gy[l - 1],
+                         self.red[l - 1], self.part[l])
+            self._wgrad(0)
+            return
         for l in range(NL - 1, -1, -1):
             # gy_l and red_l are complete here (head or dgrad_{l+1}): fork wgrad_l onto the side branch
             if side is not main:

@@ -208,3 +208,20 @@ def test_cli_fused_resnet20_checkpoint_resume(tmp_path):
                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r2.returncode == 0 and "Restored" in r2.stdout, r2.stdout[-3000:]
     assert int(CK.read_bundle(CK.latest_checkpoint(str(tmp_path)))["global_step"]) == 9
+
+
+def test_merged_backward_launch_matches_separate_launches(monkeypatch):
+    """rn_bwd (dgrad_l + wgrad_l as one launch, block roles) computes the same gradients as the two
+    separate launches (up to the order of the fp64 BN-statistics atomics)."""
+    B = 32
+    data, labels = _data(4 * B, seed=13)
+    merged = FusedResNetEngine(B, data, labels, seed=12)
+    assert merged.merged_bwd and not merged.wgrad_branch
+    g_m = merged.compute_gradients().cpu().clone()
+    monkeypatch.setenv("DMLC_RN_MERGED_BWD", "0")
+    split = FusedResNetEngine(B, data, labels, seed=12)
+    assert not split.merged_bwd
+    g_s = split.compute_gradients().cpu().clone()
+    assert _rel(g_m, g_s) < 1e-4, _rel(g_m, g_s)
+    for lm, ls in zip(merged.part, split.part):
+        assert _rel(lm, ls) < 1e-3
