@@ -72,6 +72,32 @@ void fp8_roundtrip(const Tensor& x, const Tensor& y, double scale) {
   CHECK_HIP(dmlc_fp8_roundtrip(x.data_ptr<float>(), y.data_ptr<float>(), (int)x.numel(), (float)scale, stream_of(x)));
 }
 
+void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
+                int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& p1, const Tensor& am1,
+                const Tensor& w2f, const Tensor& b2, const Tensor& p2, const Tensor& am2) {
+  const int64_t B = p1.size(0);
+  check_data(data);
+  TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
+  check(w1f, "w1f", at::kBFloat16, {64, 160});
+  check_numel(b1, "b1", at::kFloat, 64);
+  check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
+  check(am1, "am1", at::kByte, {B, 12, 12, 64});
+  check(w2f, "w2f", at::kBFloat16, {64, 1600});
+  check_numel(b2, "b2", at::kFloat, 64);
+  check(p2, "p2", at::kBFloat16, {B, 6, 6, 64});
+  check(am2, "am2", at::kByte, {B, 6, 6, 64});
+  c10::DeviceGuard guard(p1.device());
+  DmlcConv1FwdArgs a1;
+  a1.data = data.data_ptr<uint8_t>(); a1.src = index_src(idx, counter, period, B);
+  a1.B = (int)B; a1.cy = (int)cy; a1.cx = (int)cx;
+  a1.w = w1f.data_ptr(); a1.bias = b1.data_ptr<float>(); a1.out = p1.data_ptr(); a1.am = am1.data_ptr<uint8_t>();
+  a1.amax = nullptr;
+  DmlcConv2FwdArgs a2;
+  a2.in = p1.data_ptr(); a2.w = w2f.data_ptr(); a2.bias = b2.data_ptr<float>();
+  a2.out = p2.data_ptr(); a2.am = am2.data_ptr<uint8_t>(); a2.B = (int)B;
+  CHECK_HIP(dmlc_conv12_fwd(&a1, &a2, stream_of(p1)));
+}
+
 void conv2_fwd(const Tensor& in, const Tensor& w2f, const Tensor& b2, const Tensor& out, const Tensor& am) {
   const int64_t B = in.size(0);
   check(in, "in", at::kBFloat16, {B, 12, 12, 64});
@@ -335,6 +361,8 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("fp8_roundtrip(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("conv2_fwd(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
+  m.def("conv12_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
+        "Tensor(a!) p1, Tensor(b!) am1, Tensor w2f, Tensor b2, Tensor(c!) p2, Tensor(d!) am2) -> ()");
   m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv1_wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor(a!) part1, Tensor(b!) partb1) -> ()");
@@ -358,6 +386,7 @@ TORCH_LIBRARY(dmlc, m) {
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("conv1_fwd", &conv1_fwd);
   m.impl("conv2_fwd", &conv2_fwd);
+  m.impl("conv12_fwd", &conv12_fwd);
   m.impl("conv2_fwd_fp8", &conv2_fwd_fp8);
   m.impl("fp8_roundtrip", &fp8_roundtrip);
   m.impl("conv2_dgrad", &conv2_dgrad);

@@ -286,6 +286,90 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
   DMLC_STAMP(DMLC_TK_DGRAD, 4);
 }
 
+// ---------------------------------------------------------------------------------------------
+// conv1 -> pool1 -> conv2 -> pool2 of one image in ONE launch (bf16 path): the images are
+// independent, so the pool1 output goes straight into conv2's zero-padded LDS input instead of
+// round-tripping through global memory and a second launch (p1 / am1 are still written for the
+// backward).  LDS: [0, 80 KB) conv1 input + output, then conv2's two weight-slice buffers;
+// [80, 112 KB) conv2's padded input; [112, 130 KB) conv2's output.
+constexpr size_t C12_WS = 0, C12_XIN2 = 81920, C12_OUT2 = C12_XIN2 + C2_XIN * 2;
+constexpr size_t C12_LDS = C12_OUT2 + C2_OUT * 2;
+static_assert((C1_XIN + C1_OUT) * 2 <= C12_XIN2 && WS_BYTES <= C12_XIN2, "conv12 LDS map");
+
+__global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcConv2FwdArgs a2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* xin = reinterpret_cast<bf16*>(smem);
+  bf16* cout = xin + C1_XIN;
+  bf16* xin2 = reinterpret_cast<bf16*>(smem + C12_XIN2);
+  bf16* cout2 = reinterpret_cast<bf16*>(smem + C12_OUT2);
+  bf16* ws = reinterpret_cast<bf16*>(smem + C12_WS);
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, li = lane & 15, cp = w & 1, pq = w >> 1;
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
+
+  const int img = batch_index(a1.src, a1.B, b);
+  stage_conv1_input(xin, a1.data + (size_t)img * 3072, a1.cy, a1.cx, tid);
+  // conv2's padded input: zero halo (rows/cols 0,1,14,15); the interior comes from pool1
+  for (int s = tid; s < 2048; s += NT) {
+    const int pix = s >> 3, c = s & 7, r = pix >> 4, col = pix & 15;
+    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(xin2 + swz128(pix, c)) = bf16x8{};
+  }
+  const bf16* W = reinterpret_cast<const bf16*>(a1.w) + (32 * cp + li) * 160 + 8 * g;
+  bf16x8 wa[2][5];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh) wa[h][kh] = glb_b128(W + h * 16 * 160 + 32 * kh);
+  float b4[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b4[h][i] = a1.bias[32 * cp + 16 * h + 4 * g + i];
+  __syncthreads();
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 1);
+
+  {
+    f32x4 acc[2][9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int px = (pq * 9 + t) * 16 + li;
+      const int y = px / 24, x = px - (px / 24) * 24;
+      const bf16* base = xin + (y * 32 + x + 2 * g) * 4;
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh) {
+        const bf16* p = base + kh * 128;
+        const bf16x8 bx = cat44(*reinterpret_cast<const bf16x4*>(p), *reinterpret_cast<const bf16x4*>(p + 4));
+        acc[0][t] = mfma16(wa[0][kh], bx, acc[0][t]);
+        acc[1][t] = mfma16(wa[1][kh], bx, acc[1][t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        store_relu_tile(cout, (pq * 9 + t) * 16 + li, 32 * cp + 16 * h + 4 * g, acc[h][t], b4[h]);
+  }
+  __syncthreads();
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 2);
+  pool_emit<24>(cout, reinterpret_cast<bf16*>(a1.out) + (size_t)b * 9216, a1.am + (size_t)b * 9216, tid, nullptr, xin2);
+  float c2b[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c2b[h][i] = a2.bias[32 * (w & 1) + 16 * h + 4 * g + i];
+  __syncthreads();                                     // conv2 input complete; conv1 region free
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 3);
+
+  conv2_tiles(reinterpret_cast<const bf16*>(a2.w), xin2, ws, w, g, li, tid, [&](int ct, int t, const f32x4& acc) {
+    store_relu_tile(cout2, 16 * t + li, 16 * ct + 4 * g, acc, c2b[ct & 1]);
+  });
+  __syncthreads();
+  pool_emit<12>(cout2, reinterpret_cast<bf16*>(a2.out) + (size_t)b * 2304, a2.am + (size_t)b * 2304, tid);
+  DMLC_STAMP(DMLC_TK_CONV1_FWD, 4);
+}
+
 }  // namespace dmlc
 
 using namespace dmlc;
@@ -314,6 +398,18 @@ hipError_t dmlc_conv2_fwd(const DmlcConv2FwdArgs* a, hipStream_t s) {
   const size_t lds = (C2_XIN + C2_OUT) * 2 + WS_BYTES;
   allow_lds(reinterpret_cast<const void*>(&k_conv2_fwd), lds, g_c2);
   hipLaunchKernelGGL(k_conv2_fwd, dim3(a->B), dim3(NT), lds, s, *a);
+  return hipGetLastError();
+}
+
+hipError_t dmlc_conv12_fwd(const DmlcConv1FwdArgs* a1, const DmlcConv2FwdArgs* a2, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv12_fwd), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)C12_LDS);
+    attr = true;
+  }
+  if (a1->B != a2->B || a1->amax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_conv12_fwd, dim3(a1->B), dim3(NT), C12_LDS, s, *a1, *a2);
   return hipGetLastError();
 }
 

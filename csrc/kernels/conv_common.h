@@ -138,8 +138,11 @@ DEV void store_relu_tile(bf16* cout, int px, int co_base, const f32x4& acc, cons
 // The inputs are post-ReLU (>= 0), so bf16 bit patterns order like their values: each candidate is a
 // 32-bit key (bits << 16 | 15 - d) and one integer max per element keeps value AND first argmax
 // (ties -> smallest d, like a strict '>' scan).  Sign bits are masked so a -0.0 ranks as 0.
+// pad_lds (optional): also writes the pooled image into an LDS [(HO+4) x (HO+4)][64] swizzled image
+// at offset (2, 2) -- the zero-padded input of the next 5x5 conv (fused conv1 -> conv2 forward).
 template <int H>
-DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid, uint32_t* vmax = nullptr) {
+DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid, uint32_t* vmax = nullptr,
+                   bf16* pad_lds = nullptr) {
   constexpr int HO = H / 2;
   uint32_t bmax = 0;                           // max pooled bf16 bits of this thread (fp8 scaling)
   for (int task = tid; task < HO * HO * 8; task += NT) {
@@ -176,6 +179,7 @@ DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid, uint32_t* 
     }
     *reinterpret_cast<uint4*>(out + q * 64 + c * 8) = o;
     *reinterpret_cast<uint2*>(am + q * 64 + c * 8) = make_uint2(alo, ahi);
+    if (pad_lds) *reinterpret_cast<uint4*>(pad_lds + swz128((py + 2) * (HO + 4) + px + 2, c)) = o;
   }
   if (vmax) *vmax = bmax;
 }

@@ -131,6 +131,8 @@ class FusedCifarEngine:
         # DMLC_SPLIT_WGRAD=1 runs them as two kernels on forked streams instead (A/B comparisons)
         import os
         self.merged_wgrad = os.environ.get("DMLC_SPLIT_WGRAD", "0") != "1"
+        # conv1 and conv2 forward in one launch (bf16 path; DMLC_SPLIT_FWD=1: two launches)
+        self.fused_fwd = os.environ.get("DMLC_SPLIT_FWD", "0") != "1"
         if self.merged_wgrad:
             # conv2: pairs of ~5-image groups (one 8-wave block per (kh, pair), one slab per pair);
             # conv1: the CUs the conv2 blocks leave, >= 2 images per block (B=256: 25 pairs, g1=131:
@@ -227,11 +229,15 @@ class FusedCifarEngine:
     # --- kernels ------------------------------------------------------------------------------
     def _forward(self, idx, counter, period, train=True, logits_out=None):
         o, p, B = self.ops, self.pv, self.B
-        o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1, self.am1,
-                    self.amax_x if self.fp8 else None)
+        if self.fused_fwd and not self.fp8:        # conv1 + pool1 + conv2 + pool2 in one launch
+            o.conv12_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
+                         self.am1, self.w2f, p["conv2_bias"], self.p2, self.am2)
+        else:
+            o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
+                        self.am1, self.amax_x if self.fp8 else None)
         if self.fp8:
             o.conv2_fwd_fp8(self.p1, self.w2f8, p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
-        else:
+        elif not self.fused_fwd:
             o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
         f = self._fc1_fwd
         o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])

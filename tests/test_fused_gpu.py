@@ -163,3 +163,21 @@ def test_lr_staircase_schedule_on_device():
     torch.cuda.synchronize()
     lrs = [eng.read_stats(s)["lr"] for s in range(1, 6)]
     assert lrs == pytest.approx([0.1, 0.1, 0.05, 0.05, 0.025])
+
+
+def test_fused_conv12_forward_equals_two_launches(monkeypatch):
+    """ops.conv12_fwd (conv1 -> pool1 -> conv2 -> pool2 of an image in one workgroup, pool1 handed to
+    conv2 through LDS) produces bit-identical p1 / argmax / p2 / logits to the two separate launches."""
+    B = 64
+    data, labels = _synthetic(4 * B, seed=21)
+    fused = FusedCifarEngine(B, data, labels, seed=20)
+    assert fused.fused_fwd
+    idx = torch.randperm(data.shape[0])[:B].to(torch.int32)
+    lf = fused.forward_logits(idx).clone()
+    monkeypatch.setenv("DMLC_SPLIT_FWD", "1")
+    split = FusedCifarEngine(B, data, labels, seed=20)
+    assert not split.fused_fwd
+    ls = split.forward_logits(idx).clone()
+    for n in ("p1", "am1", "p2", "am2"):
+        assert torch.equal(getattr(fused, n), getattr(split, n)), n
+    assert torch.equal(lf, ls)

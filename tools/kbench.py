@@ -51,6 +51,9 @@ def main():
     res["conv1_fwd"] = timeit(lambda: o.conv1_fwd(eng.data, eng.perm, eng.step_t, eng.period, eng.cy, eng.cx, eng.w1f,
                                                   p["conv1_bias"], eng.p1, eng.am1), a.iters)
     res["conv2_fwd"] = timeit(lambda: o.conv2_fwd(eng.p1, eng.w2f, p["conv2_bias"], eng.p2, eng.am2), a.iters)
+    res["conv12_fwd"] = timeit(lambda: o.conv12_fwd(eng.data, eng.perm, eng.step_t, eng.period, eng.cy, eng.cx,
+                                                    eng.w1f, p["conv1_bias"], eng.p1, eng.am1, eng.w2f,
+                                                    p["conv2_bias"], eng.p2, eng.am2), a.iters)
     f = eng._fc1_fwd
     res["fc1_fwd_gemm"] = timeit(lambda: o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"]), a.iters)
     B = eng.B
@@ -74,7 +77,8 @@ def main():
     eng.capture()
     res["step_graph"] = timeit(lambda: eng.graphs[0].replay(), a.iters)
     res["sum_kernels"] = sum(v for k, v in res.items()
-                             if not k.startswith("step") and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad"))
+                             if not k.startswith("step") and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad")
+                             and k not in (("conv1_fwd", "conv2_fwd") if eng.fused_fwd else ("conv12_fwd",)))
     cfg = dict(batch=a.batch, g1=eng.g1, g2=eng.g2, fc1_split=eng.fc1_split)
     print(json.dumps({"config": cfg, "us": {k: round(v, 2) for k, v in res.items()}}), flush=True)
 
