@@ -75,7 +75,8 @@ def init(info: Optional[DistInfo] = None, device: str = "auto", timeout_s: float
     """Initialise the default process group (if world_size > 1) and bind this rank's device."""
     info = info or env_info()
     info.device = pick_device(info.local_rank, device)
-    info.backend = backend or ("nccl" if info.device.type == "cuda" else "gloo")
+    # DMLC_DIST_BACKEND=gloo: rehearse a multi-rank GPU job on one GPU (RCCL refuses two ranks per GPU)
+    info.backend = backend or os.environ.get("DMLC_DIST_BACKEND") or ("nccl" if info.device.type == "cuda" else "gloo")
     if info.world_size > 1 and not dist.is_initialized():
         timeout = datetime.timedelta(seconds=timeout_s)
         kw = {}
