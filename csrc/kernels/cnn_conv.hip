@@ -167,7 +167,7 @@ DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][N
         const bf16x8 a1 = lds_b128(wr1 + c);
 #pragma unroll
         for (int t = 0; t < NPX; ++t) {
-          const bf16x8 bx = lds_b128(xin + swz128(pb[t] + kh * 16 + kw, 4 * s + g));
+          const bf16x8 bx = lds_b128(xin + swzpad(pb[t] + kh * 16 + kw, 4 * s + g));
           acc[0][t] = mfma16(a0, bx, acc[0][t]);
           acc[1][t] = mfma16(a1, bx, acc[1][t]);
         }
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd(DmlcConv2FwdArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int s = tid + i * NT;
-    *reinterpret_cast<uint4*>(xin + swz128(s >> 3, s & 7)) = v[i];
+    *reinterpret_cast<uint4*>(xin + swzpad(s >> 3, s & 7)) = v[i];
   }
   float b4[2][4];
 #pragma unroll
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
   for (int s = tid; s < 2048; s += NT) {
     const int pix = s >> 3, c = s & 7;
     const int r = pix >> 4, col = pix & 15;
-    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(dyp + swz128(pix, c)) = bf16x8{};
+    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(dyp + swzpad(pix, c)) = bf16x8{};
   }
   __syncthreads();
   DMLC_STAMP(DMLC_TK_DGRAD, 1);
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
     for (int k = 0; k < 4; ++k) {
       const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
       const bf16x8 v = to_bf16x8(o[k]);
-      *reinterpret_cast<bf16x8*>(dyp + swz128((y + 2) * 16 + x + 2, c)) = v;
+      *reinterpret_cast<bf16x8*>(dyp + swzpad((y + 2) * 16 + x + 2, c)) = v;
       *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8) = v;
     }
   }
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
   // conv2's padded input: zero halo (rows/cols 0,1,14,15); the interior comes from pool1
   for (int s = tid; s < 2048; s += NT) {
     const int pix = s >> 3, c = s & 7, r = pix >> 4, col = pix & 15;
-    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(xin2 + swz128(pix, c)) = bf16x8{};
+    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(xin2 + swzpad(pix, c)) = bf16x8{};
   }
   const bf16* W = reinterpret_cast<const bf16*>(a1.w) + (32 * cp + li) * 160 + 8 * g;
   bf16x8 wa[2][5];

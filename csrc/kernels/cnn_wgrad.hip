@@ -27,41 +27,16 @@ constexpr int W1_DY_LD = 72;                  // dY1 LDS row stride (bf16): 144 
 constexpr int W1_PL = 28 * 24 + 8;            // shifted-plane stride (bf16): 1360 B, b128 reads conflict-free
 constexpr int W1_DYT = 576 * W1_DY_LD;        // bf16 elements
 constexpr int W1_XS = 16 * W1_PL;
-constexpr int W1_RAW = 28 * 32 * 4;           // bf16 [28][32][4] padded crop (col c <-> ix = c-2)
 constexpr int W1T = 512;                      // 8 waves (2 per SIMD) for the VALU-heavy gather phases
-constexpr size_t W1_LDS = (size_t)(W1_DYT + W1_XS + 9216 + W1_RAW) * 2 + 9216 + (W1T / 64) * 64 * 4;
-
-struct Conv1Input {                            // prefetch of the 28x32 zero-padded crop, 3 bytes/pixel
-  static constexpr int IT = (896 + W1T - 1) / W1T;
-  uint32_t v[IT];
-  MDEV void load(const uint8_t* img, int cy, int cx, int tid) {
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int p = tid + i * W1T;
-      const int r = p >> 5, c = p & 31, iy = r - 2, ix = c - 2;
-      const bool ok = p < 896 && iy >= 0 && iy < 24 && ix >= 0 && ix < 24;
-      const uint8_t* s = img + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);   // branch-free loads
-      const uint32_t x = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16);
-      v[i] = ok ? x : 0u;
-    }
-  }
-  MDEV void store(bf16* raw, int tid) const {
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int p = tid + i * W1T;
-      if (p < 896)
-        *reinterpret_cast<bf16x4*>(raw + p * 4) =
-            pack4((float)(v[i] & 0xff), (float)((v[i] >> 8) & 0xff), (float)((v[i] >> 16) & 0xff), 0.f);
-    }
-  }
-};
+// dY1 | shifted planes | pool1 grad (bf16) | raw uint8 image [32][32][3] | argmax bytes | reduction
+constexpr size_t W1_LDS = (size_t)(W1_DYT + W1_XS + 9216) * 2 + 3072 + 9216 + (W1T / 64) * 64 * 4;
 
 DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* smem) {
   bf16* dyt = reinterpret_cast<bf16*>(smem);
   bf16* xs = dyt + W1_DYT;
   bf16* dps = xs + W1_XS;
-  bf16* raw = dps + 9216;
-  uint8_t* ams = reinterpret_cast<uint8_t*>(raw + W1_RAW);
+  uint8_t* img = reinterpret_cast<uint8_t*>(dps + 9216);
+  uint8_t* ams = img + 3072;
   float* red = reinterpret_cast<float*>(ams + 9216);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
@@ -78,35 +53,52 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
     for (int t = 0; t < 5; ++t) acc[h][t] = zero4();
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-  Conv1Input pin;
-  Prefetch16<1152, W1T> pdp;
-  Prefetch16<576, W1T> pam;
-  if (b0 < b1) {
-    pin.load(a.data + (size_t)batch_index(a.src, a.B, b0) * 3072, a.cy, a.cx, tid);
-    pdp.load(reinterpret_cast<const bf16*>(a.dp1) + (size_t)b0 * 9216, tid);
-    pam.load(a.am1 + (size_t)b0 * 9216, tid);
-  }
+  // Every load below is unconditional (image indices clamped to the block's last image, surplus
+  // threads duplicating chunks): see PrefetchAll.  The dataset row of image b+1 is read one image
+  // ahead of its pixels, so no index -> pixels dependency is exposed inside the loop.
+  const int last = b1 > b0 ? b1 - 1 : b0;
+  const int* ib = a.src.idx_base + (a.src.counter ? (int)(*a.src.counter % (int64_t)a.src.period) : 0) * a.B;
+  // Per thread: 1 chunk of the whole uint8 image (3072 B = 192 chunks, 16-B aligned dataset rows),
+  // 3 of the pool1 gradient (1152), 2 of the argmax bytes (576).  Named registers, not member
+  // arrays: with the arrays in a struct hipcc kept them in scratch.
+  const int cI = tid % 192, cD2 = 1024 + (tid & 127), cA1 = 512 + (tid & 63);
+  uint4 vI, vD0, vD1, vD2, vA0, vA1;
+  auto load = [&](int idx, int bb) {
+    const uint4* si = reinterpret_cast<const uint4*>(a.data + (size_t)idx * 3072);
+    const uint4* sd = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.dp1) + (size_t)bb * 9216);
+    const uint4* sa = reinterpret_cast<const uint4*>(a.am1 + (size_t)bb * 9216);
+    vI = si[cI];
+    vD0 = sd[tid]; vD1 = sd[tid + 512]; vD2 = sd[cD2];
+    vA0 = sa[tid]; vA1 = sa[cA1];
+  };
+  load(ib[b0 < last ? b0 : last], b0);
+  int nidx = ib[b0 + 1 < last ? b0 + 1 : last];
   for (int b = b0; b < b1; ++b) {
     __syncthreads();                           // previous image's MFMA reads are done
-    pin.store(raw, tid);
-    pdp.store(dps, tid);
-    pam.store(ams, tid);
-    if (b + 1 < b1) {                          // prefetch the next image while this one computes
-      pin.load(a.data + (size_t)batch_index(a.src, a.B, b + 1) * 3072, a.cy, a.cx, tid);
-      pdp.load(reinterpret_cast<const bf16*>(a.dp1) + (size_t)(b + 1) * 9216, tid);
-      pam.load(a.am1 + (size_t)(b + 1) * 9216, tid);
-    }
+    reinterpret_cast<uint4*>(img)[cI] = vI;
+    reinterpret_cast<uint4*>(dps)[tid] = vD0;
+    reinterpret_cast<uint4*>(dps)[tid + 512] = vD1;
+    reinterpret_cast<uint4*>(dps)[cD2] = vD2;
+    reinterpret_cast<uint4*>(ams)[tid] = vA0;
+    reinterpret_cast<uint4*>(ams)[cA1] = vA1;
+    load(nidx, b + 1 < last ? b + 1 : last);   // prefetch the next image while this one computes
+    nidx = ib[b + 2 < last ? b + 2 : last];
     __syncthreads();
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 1);
-    // (a) shifted channel planes: task (yy, x8, kw) -> planes kw*3+{0,1,2}, 8 pixels
+    // (a) shifted channel planes straight from the uint8 image: task (yy, x8, kw) -> planes
+    //     kw*3+{0,1,2}, 8 pixels: plane[kw*3+ci][yy][x] = crop[ci][yy-2][x+kw-2] (0 outside the crop)
     for (int task = tid; task < 28 * 3 * 5; task += W1T) {
-      const int kw = task % 5, r = task / 5, x8 = r % 3, yy = r / 3;
-      const bf16* src = raw + (yy * 32 + x8 * 8 + kw) * 4;
+      const int kw = task % 5, r = task / 5, x8 = r % 3, yy = r / 3, iy = yy - 2;
+      const bool rok = iy >= 0 && iy < 24;
+      const uint8_t* srow = img + ((a.cy + (rok ? iy : 0)) * 32 + a.cx) * 3;
       bf16x8 o0, o1, o2;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const bf16x4 v = *reinterpret_cast<const bf16x4*>(src + j * 4);
-        o0[j] = v[0]; o1[j] = v[1]; o2[j] = v[2];
+        const int ix = x8 * 8 + kw + j - 2;
+        const bool ok = rok && ix >= 0 && ix < 24;
+        const uint8_t* px = srow + (ok ? ix : 0) * 3;
+        const float f0 = px[0], f1 = px[1], f2 = px[2];
+        o0[j] = (bf16)(ok ? f0 : 0.f); o1[j] = (bf16)(ok ? f1 : 0.f); o2[j] = (bf16)(ok ? f2 : 0.f);
       }
       bf16* dst = xs + (kw * 3) * W1_PL + yy * 24 + x8 * 8;
       *reinterpret_cast<bf16x8*>(dst) = o0;
@@ -221,40 +213,42 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* sme
     for (int ct = 0; ct < 4; ++ct) acc[kw][ct] = zero4();
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // conv2 bias grad (kh == 0 blocks)
 
-  // prefetch: x rows iy = kh-2 .. kh+9 (1152 chunks, invalid rows -> 0) and dY (1152 chunks)
+  // prefetch: x rows iy = kh-2 .. kh+9 (1152 chunks, invalid rows -> 0) and dY (1152 chunks).  No
+  // predicate on any load or store (PrefetchAll's reasoning): the image index is clamped to the
+  // group's last image, and in the 5th round threads 128..255 duplicate the chunks of threads 0..127.
   constexpr int IT = 5;
   uint4 vx[IT], vd[IT];
+  auto chunk = [&](int i) { return i < IT - 1 ? tid + i * 256 : 1024 + (tid & 127); };
+  const int last = b1 > b0 ? b1 - 1 : b0;
   auto load = [&](int b) {
     const uint4* x = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.p1) + (size_t)b * 9216);
     const uint4* d = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.dy2) + (size_t)b * 9216);
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int k = tid + i * 256;
+      const int k = chunk(i);
       const int yy = k / 96, iy = kh + yy - 2;
-      vx[i] = load_sel(x + iy * 96 + (k - yy * 96), x, k < 1152 && iy >= 0 && iy < 12);
-      vd[i] = load_sel(d + k, d, k < 1152);
+      vx[i] = load_sel(x + iy * 96 + (k - yy * 96), x, iy >= 0 && iy < 12);
+      vd[i] = d[k];
     }
   };
-  if (b0 < b1) load(b0);
+  load(b0 < last ? b0 : last);
   for (int it = 0; it < nmax; ++it) {
     const int b = b0 + it;
     const bool act = b < b1;                   // uniform per half (waves of one half agree)
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int k = tid + i * 256;
-      if (act && k < 1152) {
-        const int yy = k / 96, rem = k - yy * 96, px = rem >> 3, c = rem & 7;
-        *reinterpret_cast<uint4*>(xt + (yy * 16 + px + 2) * W2_LD + c * 8) = vx[i];
-        *reinterpret_cast<uint4*>(dyt + (k >> 3) * W2_LD + (k & 7) * 8) = vd[i];
-        if (kh == 0) {                         // chunk k & 7 == tid & 7: channels 8c..8c+7
-          const uint32_t d4[4] = {vd[i].x, vd[i].y, vd[i].z, vd[i].w};
+      const int k = chunk(i);
+      const int yy = k / 96, rem = k - yy * 96, px = rem >> 3, c = rem & 7;
+      *reinterpret_cast<uint4*>(xt + (yy * 16 + px + 2) * W2_LD + c * 8) = vx[i];
+      *reinterpret_cast<uint4*>(dyt + (k >> 3) * W2_LD + (k & 7) * 8) = vd[i];
+      if (kh == 0 && act && (i < IT - 1 || tid < 128)) {   // chunk k & 7 == tid & 7: channels 8c..8c+7
+        const uint32_t d4[4] = {vd[i].x, vd[i].y, vd[i].z, vd[i].w};
 #pragma unroll
-          for (int j = 0; j < 4; ++j) { bsum[2 * j] += bf16_lo(d4[j]); bsum[2 * j + 1] += bf16_hi(d4[j]); }
-        }
+        for (int j = 0; j < 4; ++j) { bsum[2 * j] += bf16_lo(d4[j]); bsum[2 * j + 1] += bf16_hi(d4[j]); }
       }
     }
-    if (b + 1 < b1) load(b + 1);
+    load(b + 1 < last ? b + 1 : last);
     __syncthreads();
     if (it == 0) DMLC_STAMP(DMLC_TK_W2, 1);
     if (!act) continue;

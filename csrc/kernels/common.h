@@ -102,6 +102,11 @@ DEV bool last_arrival(unsigned int* tk, int blk, int nblk) {
 // 16-byte chunk swizzle for [pixel][64 x bf16] LDS images (128-B rows): chunk c of pixel p is
 // stored at chunk slot c ^ (p & 7), spreading 16 consecutive pixels over all bank slots.
 DEV int swz128(int pix, int chunk) { return pix * 64 + ((chunk ^ (pix & 7)) << 3); }
+// Swizzle of the zero-padded 16x16-pixel conv2 input images (pixel = 16*y + x): the XOR key also
+// folds in the row (4*y), so the 16 pixels of an MFMA B tile -- which wrap from x = 11 back to
+// x = 0 of the next row -- hit distinct bank groups: 4 LDS cycles per ds_read_b128 instead of 8
+// with the plain (pix & 7) key (modelled per lane group, tools/lds_banks.py).
+DEV int swzpad(int pix, int chunk) { return pix * 64 + ((chunk ^ ((pix + 4 * (pix >> 4)) & 7)) << 3); }
 
 }  // namespace dmlc
 

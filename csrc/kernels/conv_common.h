@@ -53,6 +53,33 @@ struct Prefetch16 {
   }
 };
 
+// Register prefetch of N 16-byte chunks with NO predicate on any load or store: in the last round
+// the surplus threads re-load (and later re-store) a chunk another thread owns -- identical bytes to
+// the same LDS address.  Every load is then consumed by an unconditional store on every path.  With
+// a predicated store (Prefetch16), hipcc's waitcnt pass sees a path on which the previous prefetch is
+// still in flight when its registers are reloaded, and waits for it in the MIDDLE of issuing the
+// next prefetch -- one exposed memory latency per item again (seen in the wgrad loop's .s).
+template <int N, int T>
+struct PrefetchAll {
+  static constexpr int IT = (N + T - 1) / T;
+  static constexpr int TAIL = N - (IT - 1) * T;
+  uint4 v[IT];
+  MDEV void load(const void* src, int tid) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int c = i < IT - 1 ? tid + i * T : (IT - 1) * T + (TAIL == T ? tid : tid % TAIL);
+      v[i] = reinterpret_cast<const uint4*>(src)[c];
+    }
+  }
+  MDEV void store(void* dst, int tid) const {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int c = i < IT - 1 ? tid + i * T : (IT - 1) * T + (TAIL == T ? tid : tid % TAIL);
+      reinterpret_cast<uint4*>(dst)[c] = v[i];
+    }
+  }
+};
+
 DEV float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 DEV float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
@@ -179,7 +206,7 @@ DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid, uint32_t* 
     }
     *reinterpret_cast<uint4*>(out + q * 64 + c * 8) = o;
     *reinterpret_cast<uint2*>(am + q * 64 + c * 8) = make_uint2(alo, ahi);
-    if (pad_lds) *reinterpret_cast<uint4*>(pad_lds + swz128((py + 2) * (HO + 4) + px + 2, c)) = o;
+    if (pad_lds) *reinterpret_cast<uint4*>(pad_lds + swzpad((py + 2) * (HO + 4) + px + 2, c)) = o;
   }
   if (vmax) *vmax = bmax;
 }

@@ -134,13 +134,18 @@ class FusedCifarEngine:
         # conv1 and conv2 forward in one launch (bf16 path; DMLC_SPLIT_FWD=1: two launches)
         self.fused_fwd = os.environ.get("DMLC_SPLIT_FWD", "0") != "1"
         if self.merged_wgrad:
-            # conv2: pairs of ~5-image groups (one 8-wave block per (kh, pair), one slab per pair);
-            # conv1: the CUs the conv2 blocks leave, >= 2 images per block (B=256: 25 pairs, g1=131:
-            # both roles end together, measured in profiles/r1_v7_*)
-            pairs = max(1, min(B // 2, round(B / 10.24))) if g2 is None else (g2 + 1) // 2
+            # conv2: pairs of ~4.6-image groups (one 8-wave block per (kh, pair), one slab per pair);
+            # conv1: exactly the CUs the conv2 blocks leave while that is >= B/4 blocks (one wave of
+            # workgroups; 5*pairs + g1 > 256 costs ~10 us).  B=256: 28 pairs + g1=116 -> 24.0 us vs
+            # 24.9 (25 + 131) and 34-35 (28 + 128), profiles/r1_v15_kbench_wgrad_sweep.txt
+            if g2 is None:
+                pairs = max(1, min(B // 2, round(B * 7 / 64) if B <= 256 else round(B / 10.24)))
+            else:
+                pairs = (g2 + 1) // 2
             self.groups2 = g2 or 2 * pairs
             self.g2 = pairs                              # slabs the SGD kernel reduces
-            self.g1 = g1 or max(1, min(B, max(B // 2, 256 - 5 * pairs)))
+            left = 256 - 5 * pairs
+            self.g1 = g1 or max(1, min(B, left if left >= B // 4 else B // 2))
         else:
             self.g2 = g2 or max(1, min(B, B // 6))      # conv2 wgrad: 5 kh blocks x ~6 images per group
             self.groups2 = self.g2
