@@ -2,7 +2,7 @@
 # One gpurun session: smoke -> GPU tests -> bench -> rocprofv3 kernel stats.
 # Each GPU step has its own time limit; a crash / abort / timeout (rc >= 124 or signal) ends the
 # session immediately (plain test failures, rc 1, do not).
-# usage: tools/gpu_session.sh [steps...]   (default: smoke tests bench prof; also: xgmi rn eager)
+# usage: tools/gpu_session.sh [steps...]   (default: smoke tests bench prof; also: fused kbench ktiming xgmi rn eager)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -14,6 +14,9 @@ for s in $STEPS; do
     xgmi) timeout -k 10 300 python -u -m pytest tests/test_xgmi_gpu.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_xgmi.log 2>&1; ok $? xgmi ;;
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; ok $? tests ;;
     bench) timeout -k 10 300 python bench.py --steps 200 --warmup 20 > gpurun_out/bench.log 2>&1; ok $? bench ;;
+    fused) timeout -k 10 400 python -u -m pytest tests/test_fused_gpu.py tests/test_fused_dp_gpu.py tests/test_fp8_gpu.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_fused.log 2>&1; ok $? fused ;;
+    kbench) timeout -k 10 200 python tools/kbench.py > gpurun_out/kbench.json 2> gpurun_out/kbench.err; ok $? kbench ;;
+    ktiming) DMLC_TIMING=1 timeout -k 10 200 python tools/ktiming.py > gpurun_out/ktiming.json 2> gpurun_out/ktiming.err; ok $? ktiming ;;
     rn) timeout -k 10 300 python bench.py --model resnet20 --steps 100 --warmup 10 > gpurun_out/bench_rn.log 2>&1; ok $? rn ;;
     eager) timeout -k 10 300 python bench.py --impl eager --steps 50 --warmup 5 > gpurun_out/bench_eager.log 2>&1; ok $? eager ;;
     prof) rm -rf gpurun_out/prof; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 10 > gpurun_out/prof.log 2>&1; ok $? prof ;;
