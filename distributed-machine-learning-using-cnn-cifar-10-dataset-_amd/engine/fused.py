@@ -63,7 +63,8 @@ class FusedCifarEngine:
                  relu_logits: bool = True, crop_offset=(4, 4), world_size: int = 1, rank: int = 0,
                  process_group=None, seed: int = 0, fc1_split: Optional[int] = None, g1: Optional[int] = None,
                  g2: Optional[int] = None, stats_len: int = 4096, comm_dtype: str = "fp32",
-                 capture_comm: bool = False, dtype: str = "bf16", allreduce: str = "auto"):
+                 capture_comm: bool = False, dtype: str = "bf16", allreduce: str = "auto",
+                 dp_schedule: str = "overlap"):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -192,6 +193,12 @@ class FusedCifarEngine:
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.multi = None                  # (k, graph of k chained steps), see capture()
         self.comm_stream = torch.cuda.Stream(device=dev) if world_size > 1 else None
+        # N>1 step schedule: "overlap" = two buckets, fc all-reduce + fc SGD on the comm stream under
+        # the conv backward; "serial" = one stream, one all-reduce of the whole flat gradient, one SGD
+        # launch (no fork/join, no co-resident comm/SGD blocks slowing the conv kernels).
+        # tune_schedule() measures both and keeps the faster.
+        assert dp_schedule in ("overlap", "serial"), dp_schedule
+        self.dp_schedule = dp_schedule
         self.side_stream = torch.cuda.Stream(device=dev)
         self.host_step = 0
         self.refresh_shadows()
@@ -333,7 +340,25 @@ class FusedCifarEngine:
             self._seg_compute_a()
             self._seg_compute_b()
             return
+        if self.dp_schedule == "serial":
+            self._serial_dp_step([self._seg_compute_ab, self._seg_apply])
+            return
         self._dp_step([self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv])
+
+    def _seg_compute_ab(self):
+        self._seg_compute_a()
+        self._seg_compute_b()
+
+    def _serial_dp_step(self, seg):
+        """Single-stream data-parallel step: fwd + bwd + conv-grad reduction | ONE all-reduce of the
+        whole flat gradient (4.27 MB fp32; the two buckets are contiguous) | one SGD launch."""
+        seg[0]()
+        n = self.master.numel()
+        if self.xgmi is not None:
+            self.xgmi.all_reduce(0, n)
+        else:
+            self._allreduce(self.grad[:n])
+        seg[1]()
 
     def _dp_step(self, seg):
         """Data-parallel step around two all-reduce buckets:
@@ -373,8 +398,11 @@ class FusedCifarEngine:
         single = self.world_size == 1 or self.capture_comm or self.xgmi is not None
         if single:
             segs = [self._eager_step]
+        elif self.dp_schedule == "serial":
+            segs = [self._seg_compute_ab, self._seg_apply]
         else:
             segs = [self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv]
+        self._captured_schedule = self.dp_schedule
         if single and steps_per_graph > 1:
             k = int(steps_per_graph)
             self.multi = (k, None)
@@ -417,9 +445,43 @@ class FusedCifarEngine:
             self._eager_step()
         elif len(self.graphs) == 1:
             self.graphs[0].replay()
+        elif self._captured_schedule == "serial":
+            self._serial_dp_step([g.replay for g in self.graphs])
         else:
             self._dp_step([g.replay for g in self.graphs])
         self.host_step += 1
+
+    def tune_schedule(self, iters: int = 30, steps_per_graph: int = 8, log=None) -> str:
+        """N>1: capture each DP step schedule, time ``iters`` real training steps of each (max over
+        ranks, so every rank takes the same decision), keep the faster one captured.  The timed steps
+        are ordinary training steps (the step counter advances).  Returns the chosen schedule."""
+        if self.world_size == 1:
+            return self.dp_schedule
+        import time
+        import torch.distributed as dist
+        nccl = dist.get_backend(self.pg) == "nccl"
+        bdev = self.device if nccl else torch.device("cpu")
+        times = {}
+        for sched in ("overlap", "serial"):
+            self.dp_schedule = sched
+            self.capture(steps_per_graph)
+            self.run(2)
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.pg)
+            t0 = time.perf_counter()
+            self.run(iters)
+            torch.cuda.synchronize(self.device)
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=bdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
+            times[sched] = float(t.item()) / iters
+        best = min(times, key=times.get)
+        self.comm_info.update(schedule=best, schedule_us={k: round(v * 1e6, 1) for k, v in times.items()})
+        if log:
+            log(f"dp schedule: {best} ({self.comm_info['schedule_us']})")
+        if best != self.dp_schedule:
+            self.dp_schedule = best
+            self.capture(steps_per_graph)
+        return best
 
     # --- evaluation -----------------------------------------------------------------------------
     @torch.no_grad()

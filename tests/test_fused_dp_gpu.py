@@ -20,7 +20,7 @@ def _data():
     return x, y
 
 
-def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce):
+def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedule="overlap"):
     sys.path.insert(0, REPO)
     import torch.distributed as dist
     import dmlc  # noqa: F401
@@ -30,7 +30,8 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce):
                             timeout=datetime.timedelta(seconds=60))   # a failing peer must not hang the suite
     x, y = _data()
     eng = FusedCifarEngine(B, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
-                           relu_logits=False, comm_dtype=comm_dtype, allreduce=allreduce)
+                           relu_logits=False, comm_dtype=comm_dtype, allreduce=allreduce,
+                           dp_schedule=schedule)
     assert eng.comm_info["allreduce"] == ("xgmi" if allreduce == "xgmi" else "rccl"), eng.comm_info
     eng.step()
     if graph:
@@ -44,15 +45,18 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce):
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("graph,comm_dtype,allreduce", [(False, "fp32", "rccl"), (True, "fp32", "rccl"),
-                                                        (True, "bf16", "rccl"), (False, "fp32", "xgmi"),
-                                                        (True, "fp32", "xgmi")])
-def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype, allreduce):
+@pytest.mark.parametrize("graph,comm_dtype,allreduce,schedule",
+                         [(False, "fp32", "rccl", "overlap"), (True, "fp32", "rccl", "overlap"),
+                          (True, "bf16", "rccl", "overlap"), (False, "fp32", "xgmi", "overlap"),
+                          (True, "fp32", "xgmi", "overlap"), (True, "fp32", "rccl", "serial"),
+                          (False, "fp32", "xgmi", "serial"), (True, "fp32", "xgmi", "serial")])
+def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype, allreduce, schedule):
     import torch.multiprocessing as mp
     from dmlc.cli import free_port
     from dmlc.engine.fused import FusedCifarEngine
     B, steps = 32, 3
-    mp.spawn(_rank, args=(2, free_port(), str(tmp_path), B, steps, graph, comm_dtype, allreduce), nprocs=2, join=True)
+    mp.spawn(_rank, args=(2, free_port(), str(tmp_path), B, steps, graph, comm_dtype, allreduce, schedule),
+             nprocs=2, join=True)
     r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
     r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
     assert r0["step"] == r1["step"] == steps
@@ -70,3 +74,41 @@ def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype, all
     d_dp, d_ref = r0["flat"] - init, ref.flat_params() - init
     rel = float((d_dp - d_ref).norm() / d_ref.norm())
     assert rel < (2e-2 if comm_dtype == "bf16" else 1e-2), rel
+
+
+def _tune_rank(rank, world, port, out, allreduce):
+    sys.path.insert(0, REPO)
+    import torch.distributed as dist
+    import dmlc  # noqa: F401
+    from dmlc.engine.fused import FusedCifarEngine
+    import datetime
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    x, y = _data()
+    eng = FusedCifarEngine(32, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
+                           relu_logits=False, allreduce=allreduce)
+    eng.step()
+    eng.capture(steps_per_graph=2)
+    best = eng.tune_schedule(iters=3, steps_per_graph=2)
+    eng.run(3)
+    torch.cuda.synchronize()
+    torch.save({"flat": eng.flat_params(), "step": eng.global_step(), "best": best,
+                "info": dict(eng.comm_info)}, os.path.join(out, f"t{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("allreduce", ["rccl", "xgmi"])
+def test_dp2_tune_schedule_agrees_across_ranks(tmp_path, allreduce):
+    """tune_schedule(): both schedules timed (max over ranks), one decision on every rank, the
+    replicas stay identical and every timed step counts (1 + 2x(2 + 3) tuning + 3 = 14 steps)."""
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    mp.spawn(_tune_rank, args=(2, free_port(), str(tmp_path), allreduce), nprocs=2, join=True)
+    t0 = torch.load(tmp_path / "t0.pt", weights_only=True)
+    t1 = torch.load(tmp_path / "t1.pt", weights_only=True)
+    assert t0["best"] == t1["best"] in ("overlap", "serial")
+    assert t0["info"]["schedule"] == t0["best"] and set(t0["info"]["schedule_us"]) == {"overlap", "serial"}
+    assert t0["step"] == t1["step"] == 14
+    assert torch.equal(t0["flat"], t1["flat"])
+    assert torch.isfinite(t0["flat"]).all()

@@ -181,3 +181,4 @@ def test_fused_conv12_forward_equals_two_launches(monkeypatch):
     for n in ("p1", "am1", "p2", "am2"):
         assert torch.equal(getattr(fused, n), getattr(split, n)), n
     assert torch.equal(lf, ls)
+
