@@ -45,7 +45,7 @@ class _FusedAdapter:
                                     lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                     staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
                                     crop_offset=((32 - cfg.crop) // 2,) * 2, comm_dtype=cfg.comm_dtype,
-                                    dtype=cfg.dtype, allreduce=cfg.allreduce)
+                                    dtype=cfg.dtype, allreduce=cfg.allreduce, dp_schedule=cfg.dp_schedule)
         self.graph = cfg.graph
         from ..models import cifar_cnn as M
         self.specs = M.PARAM_SPECS

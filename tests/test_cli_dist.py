@@ -38,6 +38,13 @@ def test_bool_flags():
         cli.parse(["--relu_logits=maybe"])
 
 
+def test_dp_schedule_flag():
+    assert cli.parse([])[0].dp_schedule == "serial"
+    assert cli.parse(["--dp_schedule=overlap"])[0].dp_schedule == "overlap"
+    with pytest.raises(SystemExit):
+        cli.parse(["--dp_schedule=ring"])
+
+
 def test_allreduce_flag():
     assert cli.parse([])[0].allreduce == "auto"
     assert cli.parse(["--allreduce=xgmi"])[0].allreduce == "xgmi"
