@@ -185,10 +185,11 @@ class FusedResNetEngine:
     def _pick_groups(B: int, cin: int, cout: int) -> int:
         """Split-K image groups of one wgrad (grid = groups x m-chunks): enough blocks to fill the chip
         (``DMLC_RN_WG_BLOCKS``, default 256) while the fp32 slabs the SGD kernel reads back stay under
-        ``DMLC_RN_SLAB_MB`` (default 8 MB) per layer.  A power of two in [8, B]."""
+        ``DMLC_RN_SLAB_MB`` (default 16 MB: 64 groups for the 64-channel layers, 677 -> 667 us/step at
+        B=256, profiles/r1_v17_rn_slab_cap_ab.txt) per layer.  A power of two in [8, B]."""
         import os
         blocks = int(os.environ.get("DMLC_RN_WG_BLOCKS", "256"))
-        cap = float(os.environ.get("DMLC_RN_SLAB_MB", "8")) * 2 ** 20
+        cap = float(os.environ.get("DMLC_RN_SLAB_MB", "16")) * 2 ** 20
         mt = _kp(cin) // 16
         mc = 1 if mt <= 12 else (2 if mt <= 24 else 3)      # Wg<>::MC in resnet.hip
         lim = min(blocks / mc, cap / (_kp(cin) * cout * 4))
