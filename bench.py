@@ -12,22 +12,82 @@ all-reduce (N>1, RCCL), SGD update with the on-device LR schedule.
   python bench.py --gpus N --steps K --warmup W
   torchrun --nproc-per-node N bench.py --gpus N ...     (the driver's launch for N > 1)
   python bench.py --impl eager                          (framework-default PyTorch eager line)
+
+``python bench.py --gpus N`` started WITHOUT a torchrun environment becomes a launcher: before any
+GPU call it starts N rank processes of itself (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, rendezvous
+on 127.0.0.1) and exits with their status, so --gpus N always measures N ranks.  Every rank checks
+that the process group it joined really has --gpus ranks and exits non-zero otherwise.
 """
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+BASELINE_VALUE = None   # BASELINE.md: the reference publishes no number
+
+
+def _launch_ranks(n: int) -> int:
+    """Launcher parent (never touches the GPU): N children of this script, one per GPU."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in live:                   # a failed rank: stop the others, report its code
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+def _want_gpus(argv) -> int:
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ and _want_gpus(sys.argv[1:]) > 1:
+    sys.exit(_launch_ranks(_want_gpus(sys.argv[1:])))
+
 import torch  # noqa: E402
 
 import dmlc  # noqa: E402,F401
 from dmlc.parallel import dist as D  # noqa: E402
-
-BASELINE_VALUE = None   # BASELINE.md: the reference publishes no number
 
 
 def parse():
@@ -52,6 +112,9 @@ def parse():
                     help="N>1 fused CNN step: overlap = fc all-reduce + fc SGD on a comm stream under the "
                          "conv backward; serial = one stream, one all-reduce; auto = measure both (before "
                          "the timed region) and keep the faster")
+    ap.add_argument("--capture-comm", choices=["auto", "on", "off"], default="auto",
+                    help="RCCL all-reduce inside the step HIP graph (auto: on over nccl)")
+    ap.add_argument("--steps-per-graph", type=int, default=8, help="longest chain of steps per graph replay")
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
     ap.add_argument("--dataset-size", type=int, default=50000)
@@ -70,15 +133,19 @@ def build_fused(args, info, data, labels):
         from dmlc.engine.fused_resnet import FusedResNetEngine
         eng = FusedResNetEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
                                 rank=info.rank, seed=0, lr=0.01, comm_dtype=args.comm_dtype,
-                                allreduce=args.allreduce)
-        return eng, eng.step, (None if args.no_graph else eng.capture)
+                                allreduce=args.allreduce, capture_comm=_capture_comm(args))
+        return eng, eng.step, (None if args.no_graph else lambda: eng.capture(args.steps_per_graph))
     from dmlc.engine.fused import FusedCifarEngine
     eng = FusedCifarEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
                            rank=info.rank, seed=0, comm_dtype=args.comm_dtype, dtype=args.dtype,
-                           allreduce=args.allreduce,
-                           dp_schedule="overlap" if args.dp_schedule == "auto" else args.dp_schedule)
+                           allreduce=args.allreduce, capture_comm=_capture_comm(args),
+                           dp_schedule="serial" if args.dp_schedule == "auto" else args.dp_schedule)
     step = eng.step
-    return eng, step, (None if args.no_graph else eng.capture)
+    return eng, step, (None if args.no_graph else lambda: eng.capture(args.steps_per_graph))
+
+
+def _capture_comm(args):
+    return None if args.capture_comm == "auto" else args.capture_comm == "on"
 
 
 def build_eager(args, info, data, labels):
@@ -92,8 +159,13 @@ def build_eager(args, info, data, labels):
 def main():
     args = parse()
     info = D.init(D.env_info(), device="auto")
-    if info.world_size != args.gpus and info.rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
+    import torch.distributed as dist
+    seen = dist.get_world_size() if dist.is_initialized() else 1
+    if seen != args.gpus or info.world_size != args.gpus:
+        print(f"bench: --gpus {args.gpus} but this rank joined a world of {seen} (WORLD_SIZE={info.world_size})",
+              file=sys.stderr, flush=True)
+        D.shutdown(info)
+        sys.exit(3)
     if args.impl == "auto":
         args.impl = "fused" if args.model == "cifar_cnn" or args.dtype == "bf16" else "eager"
     if args.crop is None:
@@ -106,33 +178,51 @@ def main():
     builder = build_fused if args.impl == "fused" else build_eager
     eng, step, capture = builder(args, info, data, labels)
 
-    for _ in range(max(1, min(3, args.warmup))):     # eager warm-up before capture
+    def sync():
+        if info.device.type == "cuda":
+            torch.cuda.synchronize(info.device)
+
+    n_eager = max(1, min(3, args.warmup))
+    for _ in range(n_eager):                          # eager warm-up before capture
         step()
+    graph_warm = 0
     if capture is not None:
         capture()
         if args.dp_schedule == "auto" and hasattr(eng, "tune_schedule") and info.world_size > 1:
-            eng.tune_schedule(iters=max(10, args.warmup))   # untimed training steps, both schedules
-    # run(n): n complete steps, chained K per graph replay inside an epoch (fused CNN engine)
+            eng.tune_schedule(iters=max(10, args.warmup), steps_per_graph=args.steps_per_graph)
+        # replay every captured chain once (first launches of a graph pay its upload): untimed
+        # training steps on top of the W warm-up steps, reported as graph_warmup_steps
+        for k in sorted(getattr(eng, "chains", {}) or {}):
+            eng.run(k)
+            graph_warm += k
+    # run(n): n complete steps, as chained graph replays (fused engines) or n step() calls
     run = getattr(eng, "run", None) if capture is not None else None
     if run is None:
         def run(n):
             for _ in range(n):
                 step()
-    run(max(0, args.warmup - 3))
-    torch.cuda.synchronize()
-    gs0 = eng.global_step() if hasattr(eng, "global_step") else None
+    run(max(0, args.warmup - n_eager))
+    sync()
+    def device_step():
+        gs = getattr(eng, "global_step", None)
+        return gs() if callable(gs) else gs
+
+    gs0 = device_step()
     D.barrier(info)
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     run(args.steps)
-    torch.cuda.synchronize()
+    sync()
     D.barrier(info)
-    torch.cuda.synchronize()
+    sync()
     elapsed = D.all_max(time.perf_counter() - t0, info)
     if gs0 is not None:     # every timed step really ran: the device step counter agrees
-        assert eng.global_step() == gs0 + args.steps, (eng.global_step(), gs0, args.steps)
+        assert device_step() == gs0 + args.steps, (device_step(), gs0, args.steps)
     if hasattr(eng, "check_comm"):
         eng.check_comm()
+    comm = dict(getattr(eng, "comm_info", None) or {})
+    comm.update(backend=info.backend if seen > 1 else "none", world_size_seen=seen,
+                device_count=torch.cuda.device_count() if info.device.type == "cuda" else 0, device=str(info.device))
 
     n = info.world_size
     ms = elapsed * 1000.0 / args.steps
@@ -162,7 +252,9 @@ def main():
                 "impl": args.impl + ("+hipgraph" if (args.impl == "fused" and not args.no_graph)
                                      or (args.impl == "eager" and args.eager_graph) else ""),
                 "comm_dtype": args.comm_dtype,
-                "comm": getattr(eng, "comm_info", None),
+                "comm": comm,
+                "graph_warmup_steps": graph_warm,
+                "steps_per_graph": args.steps_per_graph if capture is not None else None,
             },
         }
         print(json.dumps(line), flush=True)

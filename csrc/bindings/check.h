@@ -37,18 +37,46 @@ inline void check_min(const Tensor& t, const char* n, at::ScalarType st, int64_t
   TORCH_CHECK(t.numel() >= numel, n, " has ", t.numel(), " elements, need at least ", numel);
 }
 
+// `idx` is either a device int32 index list [period * B] or, for the generated training order, a
+// HOST int64 descriptor [n, half_bits, world, rank, bvalid, seed] (dmlc/data/order.py
+// OrderSpec.descriptor(); read here at launch/capture time, so no device sync) -- see api.h.
 inline DmlcIndexSrc index_src(const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t B) {
   TORCH_CHECK(period >= 1, "period must be >= 1");
-  check_numel(idx, "idx", at::kInt, period * B);
   DmlcIndexSrc s;
-  s.idx_base = idx.data_ptr<int>();
+  memset(&s, 0, sizeof(s));
   s.counter = nullptr;
   if (counter.has_value()) {
     check_numel(*counter, "counter", at::kLong, 1);
     s.counter = counter->data_ptr<int64_t>();
   }
   s.period = (int)period;
+  if (!idx.is_cuda()) {
+    TORCH_CHECK(idx.scalar_type() == at::kLong && idx.numel() == 6 && idx.is_contiguous(),
+                "a host idx must be the int64 [6] order descriptor");
+    TORCH_CHECK(s.counter != nullptr, "the generated order needs the device step counter");
+    const int64_t* d = idx.data_ptr<int64_t>();
+    const int64_t n = d[0], hb = d[1], world = d[2], rank = d[3], bvalid = d[4], seed = d[5];
+    TORCH_CHECK(n >= 1 && n < (1ll << 30), "order: dataset size out of range");
+    TORCH_CHECK(hb >= 1 && hb <= 15 && (1ll << (2 * hb)) >= n && (1ll << (2 * (hb - 1))) < std::max<int64_t>(n, 2),
+                "order: half_bits must be the smallest h with 4^h >= n");
+    TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "order: bad rank/world");
+    TORCH_CHECK(bvalid >= 1 && bvalid <= B, "order: bvalid must be in [1, B]");
+    TORCH_CHECK(period * world * bvalid <= n, "order: an epoch of period steps must fit in the dataset");
+    TORCH_CHECK(seed >= 0 && seed <= 0xffffffffll, "order: seed must be a uint32");
+    s.idx_base = nullptr;
+    s.n = (int)n; s.half_bits = (int)hb; s.world = (int)world; s.rank = (int)rank; s.bvalid = (int)bvalid;
+    s.seed = (uint32_t)seed;
+    return s;
+  }
+  check_numel(idx, "idx", at::kInt, period * B);
+  s.idx_base = idx.data_ptr<int>();
+  s.bvalid = (int)B;
   return s;
+}
+
+// generated order: every index it yields is < n, which must address rows of the dataset
+inline void check_order_fits(const DmlcIndexSrc& s, int64_t rows) {
+  TORCH_CHECK(s.idx_base != nullptr || s.n <= rows, "order: dataset size ", s.n, " exceeds the ", rows, " rows given");
 }
 
 inline hipStream_t stream_of(const Tensor& t) {

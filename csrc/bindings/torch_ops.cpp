@@ -31,6 +31,7 @@ void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   DmlcConv1FwdArgs a;
   a.data = data.data_ptr<uint8_t>();
   a.src = index_src(idx, counter, period, B);
+  check_order_fits(a.src, data.size(0));
   a.B = (int)B; a.cy = (int)cy; a.cx = (int)cx;
   a.w = w1f.data_ptr(); a.bias = b1.data_ptr<float>();
   a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>();
@@ -89,6 +90,7 @@ void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tenso
   c10::DeviceGuard guard(p1.device());
   DmlcConv1FwdArgs a1;
   a1.data = data.data_ptr<uint8_t>(); a1.src = index_src(idx, counter, period, B);
+  check_order_fits(a1.src, data.size(0));
   a1.B = (int)B; a1.cy = (int)cy; a1.cx = (int)cx;
   a1.w = w1f.data_ptr(); a1.bias = b1.data_ptr<float>(); a1.out = p1.data_ptr(); a1.am = am1.data_ptr<uint8_t>();
   a1.amax = nullptr;
@@ -140,6 +142,7 @@ void conv1_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tens
   c10::DeviceGuard guard(dp1.device());
   DmlcConv1WgradArgs a;
   a.data = data.data_ptr<uint8_t>(); a.src = index_src(idx, counter, period, B);
+  check_order_fits(a.src, data.size(0));
   a.cy = (int)cy; a.cx = (int)cx;
   a.dp1 = dp1.data_ptr(); a.am1 = am1.data_ptr<uint8_t>();
   a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1; a.B = (int)B;
@@ -179,6 +182,7 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
   c10::DeviceGuard guard(dp1.device());
   DmlcWgradArgs a;
   a.w1.data = data.data_ptr<uint8_t>(); a.w1.src = index_src(idx, counter, period, B);
+  check_order_fits(a.w1.src, data.size(0));
   a.w1.cy = (int)cy; a.w1.cx = (int)cx;
   a.w1.dp1 = dp1.data_ptr(); a.w1.am1 = am1.data_ptr<uint8_t>();
   a.w1.part1 = part1.data_ptr<float>(); a.w1.partb1 = partb1.data_ptr<float>(); a.w1.g1 = (int)g1; a.w1.B = (int)B;
@@ -240,7 +244,8 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
           const Tensor& b3, const Tensor& w3d, const Tensor& w2d, const Tensor& labels, const Tensor& idx,
           const c10::optional<Tensor>& counter, int64_t period, double inv_batch, bool relu_logits, bool train,
           const Tensor& h1, const Tensor& h2, const Tensor& dl, const Tensor& dh1, const Tensor& dh2,
-          const Tensor& loss_part, const Tensor& correct_part, const c10::optional<Tensor>& logits_out) {
+          const Tensor& loss_part, const Tensor& correct_part, const c10::optional<Tensor>& logits_out,
+          int64_t nvalid) {
   TORCH_CHECK(h1part.dim() == 3 && h1part.size(2) == 384, "h1part must be [nsplit,B,384]");
   const int64_t nsplit = h1part.size(0), B = h1part.size(1);
   TORCH_CHECK(B % 16 == 0 && B > 0, "head: batch must be a positive multiple of 16");
@@ -272,6 +277,10 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
   a.b1 = b1.data_ptr<float>(); a.w2t = w2t.data_ptr(); a.b2 = b2.data_ptr<float>();
   a.w3t = w3t.data_ptr(); a.b3 = b3.data_ptr<float>(); a.w3d = w3d.data_ptr(); a.w2d = w2d.data_ptr();
   a.labels = labels.data_ptr<int>(); a.src = index_src(idx, counter, period, B);
+  check_order_fits(a.src, labels.size(0));
+  if (nvalid < 0) nvalid = B;
+  TORCH_CHECK(nvalid >= 1 && nvalid <= B, "head: nvalid must be in [1, B]");
+  a.nvalid = (int)nvalid;
   a.B = (int)B; a.rows = (int)rows; a.inv_batch = (float)inv_batch; a.relu_logits = relu_logits; a.train = train;
   a.h1 = train ? h1.data_ptr() : nullptr; a.h2 = train ? h2.data_ptr() : nullptr; a.dl = train ? dl.data_ptr() : nullptr;
   a.dh1 = train ? dh1.data_ptr() : nullptr; a.dh2 = train ? dh2.data_ptr() : nullptr;
@@ -308,7 +317,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   check(partb2, "partb2", at::kFloat, {g2, 64});
   TORCH_CHECK(loss_part.numel() >= 1, "loss partials missing");
   const int64_t B = batch;
-  TORCH_CHECK(B >= 1 && B % loss_part.numel() == 0, "sgd: batch must be a multiple of the loss partial count");
+  TORCH_CHECK(B >= 1 && B <= 4 * loss_part.numel(), "sgd: batch (valid rows) exceeds the head's rows");
   check(w1f, "w1f", at::kBFloat16, {64, 160});
   check(w2f, "w2f", at::kBFloat16, {64, 1600});
   check(w2d, "w2d", at::kBFloat16, {64, 1600});
@@ -374,7 +383,7 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
         "Tensor(a!) h1, Tensor(b!) h2, Tensor(c!) dl, Tensor(d!) dh1, Tensor(e!) dh2, Tensor(f!) loss_part, "
-        "Tensor(g!) correct_part, Tensor(h!)? logits_out) -> ()");
+        "Tensor(g!) correct_part, Tensor(h!)? logits_out, int nvalid=-1) -> ()");
   m.def("sgd(Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor part1, Tensor partb1, "
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "

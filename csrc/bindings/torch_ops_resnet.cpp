@@ -51,6 +51,7 @@ void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::o
     TORCH_CHECK(cy == 0 && cx == 0, "the ResNet stem consumes full 32x32 images (crop offsets 0)");
     a.data = data->data_ptr<uint8_t>();
     a.src = index_src(*idx, counter, period, B);
+    check_order_fits(a.src, data->size(0));
   } else {
     TORCH_CHECK(z_prev && stat_prev && gamma_prev && beta_prev && a_out, "rn_fwd needs the previous layer's tensors");
     check(*z_prev, "z_prev", at::kBFloat16, {B, hin, hin, cin});
@@ -142,6 +143,7 @@ DmlcRnWgradArgs wgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
     TORCH_CHECK(cy == 0 && cx == 0, "the ResNet stem consumes full 32x32 images (crop offsets 0)");
     a.data = data->data_ptr<uint8_t>();
     a.src = index_src(*idx, counter, period, B);
+    check_order_fits(a.src, data->size(0));
   } else {
     TORCH_CHECK(x.has_value(), "rn_wgrad needs x");
     check(*x, "x", at::kBFloat16, {B, hin, hin, cin});
@@ -203,7 +205,9 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
   a.z = z.data_ptr(); a.stat = stat.data_ptr<double>(); a.gamma = gamma.data_ptr<float>();
   a.beta = beta.data_ptr<float>(); a.inv_n = 1.f / (float)(B * 64);
   a.sc = sc.data_ptr(); a.fcw = fcw.data_ptr<float>(); a.fcb = fcb.data_ptr<float>();
-  a.labels = labels.data_ptr<int>(); a.src = index_src(idx, counter, period, B); a.inv_batch = (float)inv_batch;
+  a.labels = labels.data_ptr<int>(); a.src = index_src(idx, counter, period, B);
+  check_order_fits(a.src, labels.size(0));
+  a.inv_batch = (float)inv_batch;
   a.gy = gy.data_ptr(); a.red = red.data_ptr<double>(); a.fc_part = fc_part.data_ptr<float>();
   a.loss_img = loss_img.data_ptr<float>(); a.correct_img = correct_img.data_ptr<int>();
   a.logits_out = nullptr;

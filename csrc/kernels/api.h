@@ -12,13 +12,22 @@
 
 extern "C" {
 
-// Batch index source shared by the data-consuming kernels: sample index of row b is
-//   idx_base[(counter ? (*counter % period) : 0) * B + b]
-// so a captured graph walks an epoch permutation through the device step counter.
+// Batch index source shared by the data-consuming kernels.  Two forms:
+//  * explicit list (idx_base != null): sample of row b is
+//      idx_base[(counter ? (*counter % period) : 0) * B + b]
+//  * generated order (idx_base == null, counter required): the training order is a keyed Feistel
+//    bijection of [0, n) per epoch (common.h order_index; dmlc/data/order.py is the host twin).
+//    With s = *counter, epoch = s / period, j = s % period, row b < bvalid of rank r reads
+//      perm_epoch((j * world + r) * bvalid + b)
+//    so a captured graph crosses epoch boundaries with no host work, and the W ranks of a step
+//    read exactly the rows a single rank with batch W*bvalid would.  Rows b >= bvalid (padding up
+//    to the kernel tile) read row bvalid - 1; their loss gradient is zeroed by the head.
 struct DmlcIndexSrc {
-  const int* idx_base;
-  const int64_t* counter;   // nullable
-  int period;               // number of B-sized batches in idx_base
+  const int* idx_base;      // nullable: generated order
+  const int64_t* counter;   // nullable (explicit list only)
+  int period;               // explicit: B-sized batches in idx_base; generated: steps per epoch
+  int n, half_bits, world, rank, bvalid;
+  uint32_t seed;
 };
 
 // conv1 5x5 (3->64) + bias + ReLU + maxpool 3x3/2 TF-SAME, fused with the uint8 gather + center
@@ -133,6 +142,7 @@ struct DmlcHeadArgs {
   const int* labels;                 // [N] dataset labels
   DmlcIndexSrc src;
   int B; int rows; float inv_batch; int relu_logits; int train;
+  int nvalid;                        // rows b >= nvalid are padding: no loss, accuracy or gradient
   void* h1; void* h2; void* dl; void* dh1; void* dh2;   // bf16 [B][384],[B][192],[B][16],[B][384],[B][192]
   float* loss_part; int* correct_part;                  // [B/rows]
   float* logits_out;                                    // optional fp32 [B][10]

@@ -38,12 +38,6 @@ struct HeadLds {             // byte offsets into the dynamic LDS; RB real rows 
   static_assert(BYTES <= 160 * 1024, "head LDS exceeds the 160 KB of a CU");
 };
 
-DEV int head_index(const DmlcIndexSrc& s, int B, int b) {
-  int row = 0;
-  if (s.counter) row = (int)(*s.counter % (int64_t)s.period);
-  return s.idx_base[row * B + b];
-}
-
 DEV bf16x4 relu_mask4(const f32x4& acc, const bf16x4& h) {
   return pack4((float)h[0] > 0.f ? acc[0] : 0.f, (float)h[1] > 0.f ? acc[1] : 0.f,
                (float)h[2] > 0.f ? acc[2] : 0.f, (float)h[3] > 0.f ? acc[3] : 0.f);
@@ -68,7 +62,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
 
   // the loss wave's labels (counter -> index -> label chain) are fetched at entry
   int label = 0;
-  if (w == 12 && lane < RB) label = a.labels[head_index(a.src, a.B, r0 + lane)];
+  if (w == 12 && lane < RB) label = a.labels[batch_index(a.src, a.B, r0 + lane)];
 
   // fc2 weights (a.w2t = [192 n][384 k]) -> LDS: 9216 chunks of 16 B, 9 per thread, all in flight
   constexpr int WCH = 192 * 48 / HT;
@@ -166,6 +160,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     float loss = 0.f, corr = 0.f;
     if (lane < RB) {
       const int b = r0 + lane;
+      const float vr = b < a.nvalid ? 1.f : 0.f;     // padding rows (any-B tail): weight 0
       float m = lg[lane][0];
       int am = 0;
 #pragma unroll
@@ -174,8 +169,8 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
 #pragma unroll
       for (int j = 0; j < 10; ++j) se += __expf(lg[lane][j] - m);
       const float lse = m + __logf(se);
-      loss = lse - lg[lane][label];
-      corr = am == label ? 1.f : 0.f;
+      loss = vr * (lse - lg[lane][label]);
+      corr = vr * (am == label ? 1.f : 0.f);
       if (a.logits_out) {
 #pragma unroll
         for (int j = 0; j < 10; ++j) a.logits_out[b * 10 + j] = lg[lane][j];
@@ -185,7 +180,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
         for (int j = 0; j < 32; ++j) {
           float d = 0.f;
           if (j < 10) {
-            d = (__expf(lg[lane][j] - lse) - (j == label ? 1.f : 0.f)) * a.inv_batch;
+            d = (__expf(lg[lane][j] - lse) - (j == label ? 1.f : 0.f)) * a.inv_batch * vr;
             if (a.relu_logits && !(lg[lane][j] > 0.f)) d = 0.f;
           }
           dls[lane * DL_LD + j] = (bf16)d;

@@ -57,7 +57,6 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
   // threads duplicating chunks): see PrefetchAll.  The dataset row of image b+1 is read one image
   // ahead of its pixels, so no index -> pixels dependency is exposed inside the loop.
   const int last = b1 > b0 ? b1 - 1 : b0;
-  const int* ib = a.src.idx_base + (a.src.counter ? (int)(*a.src.counter % (int64_t)a.src.period) : 0) * a.B;
   // Per thread: 1 chunk of the whole uint8 image (3072 B = 192 chunks, 16-B aligned dataset rows),
   // 3 of the pool1 gradient (1152), 2 of the argmax bytes (576).  Named registers, not member
   // arrays: with the arrays in a struct hipcc kept them in scratch.
@@ -71,8 +70,8 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
     vD0 = sd[tid]; vD1 = sd[tid + 512]; vD2 = sd[cD2];
     vA0 = sa[tid]; vA1 = sa[cA1];
   };
-  load(ib[b0 < last ? b0 : last], b0);
-  int nidx = ib[b0 + 1 < last ? b0 + 1 : last];
+  load(batch_index(a.src, a.B, b0 < last ? b0 : last), b0);
+  int nidx = batch_index(a.src, a.B, b0 + 1 < last ? b0 + 1 : last);
   for (int b = b0; b < b1; ++b) {
     __syncthreads();                           // previous image's MFMA reads are done
     reinterpret_cast<uint4*>(img)[cI] = vI;
@@ -82,7 +81,7 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
     reinterpret_cast<uint4*>(ams)[tid] = vA0;
     reinterpret_cast<uint4*>(ams)[cA1] = vA1;
     load(nidx, b + 1 < last ? b + 1 : last);   // prefetch the next image while this one computes
-    nidx = ib[b + 2 < last ? b + 2 : last];
+    nidx = batch_index(a.src, a.B, b + 2 < last ? b + 2 : last);
     __syncthreads();
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 1);
     // (a) shifted channel planes straight from the uint8 image: task (yy, x8, kw) -> planes

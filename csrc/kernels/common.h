@@ -99,6 +99,51 @@ DEV bool last_arrival(unsigned int* tk, int blk, int nblk) {
   return true;
 }
 
+// 32-bit integer mixer (a bijective avalanche hash): the round function of the data-order Feistel
+// network below.  Host twin: dmlc/data/order.py (_mix32).
+DEV uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du;
+  x ^= x >> 15; x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// Dataset row of position `pos` in the epoch's permutation of [0, n): a 4-round balanced Feistel
+// network on 2*half_bits bits keyed by (seed, epoch), cycle-walked back into [0, n) (the walk ends:
+// pos < n lies on its own cycle).  Expected walks: 2^(2*half_bits) / n < 4.
+DEV uint32_t order_perm(uint32_t pos, uint32_t n, int half_bits, uint32_t seed, uint32_t epoch) {
+  const uint32_t ek = mix32(mix32(seed ^ 0x5bd1e995u) ^ mix32(epoch * 0x85ebca77u + 0x632be5abu));
+  const uint32_t mask = (1u << half_bits) - 1u;
+  uint32_t x = pos;
+  do {
+    uint32_t l = x >> half_bits, r = x & mask;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t t = l ^ (mix32(r ^ (ek + (uint32_t)k * 0x9e3779b9u)) & mask);
+      l = r;
+      r = t;
+    }
+    x = (l << half_bits) | r;
+  } while (x >= n);
+  return x;
+}
+
+// Sample index of batch row b (api.h DmlcIndexSrc: explicit list or generated epoch order).
+template <class Src>
+DEV int batch_index(const Src& s, int B, int b) {
+  if (s.idx_base) {
+    int row = 0;
+    if (s.counter) row = (int)(*s.counter % (int64_t)s.period);
+    return s.idx_base[row * B + b];
+  }
+  const int64_t step = *s.counter;
+  const uint32_t epoch = (uint32_t)(step / s.period);
+  const int64_t j = step - (int64_t)epoch * s.period;
+  const int bb = b < s.bvalid ? b : s.bvalid - 1;
+  const uint32_t pos = (uint32_t)((j * s.world + s.rank) * s.bvalid + bb);
+  return (int)order_perm(pos, (uint32_t)s.n, s.half_bits, s.seed, epoch);
+}
+
 // 16-byte chunk swizzle for [pixel][64 x bf16] LDS images (128-B rows): chunk c of pixel p is
 // stored at chunk slot c ^ (p & 7), spreading 16 consecutive pixels over all bank slots.
 DEV int swz128(int pix, int chunk) { return pix * 64 + ((chunk ^ (pix & 7)) << 3); }

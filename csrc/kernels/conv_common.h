@@ -7,12 +7,6 @@ namespace dmlc {
 
 constexpr int NT = 512;   // per-image conv kernels: 8 waves, 2 per SIMD hide each other's latency
 
-DEV int batch_index(const DmlcIndexSrc& s, int B, int b) {
-  int row = 0;
-  if (s.counter) row = (int)(*s.counter % (int64_t)s.period);
-  return s.idx_base[row * B + b];
-}
-
 // Copy N 16-byte chunks global -> LDS with every load of the thread issued before any store, so
 // the block pays one memory latency instead of one per iteration.
 template <int N>

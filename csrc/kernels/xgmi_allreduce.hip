@@ -14,7 +14,9 @@
 //     (workgroup, peer) in uncached device memory; epochs are per-workgroup counters in device
 //     memory, so the launch is graph-capturable and replays need no host involvement;
 //   * every spin is bounded (s_memrealtime deadline): a missing peer sets a sticky error word and
-//     the kernel drains instead of hanging the GPU; the host raises on it.
+//     the kernel drains instead of hanging the GPU.  The word is mirrored into mapped pinned host
+//     memory, so the training loop polls it with a plain load (no HIP call, no sync) and exits for
+//     a restart; once it is set, later launches skip their barriers (drain at once).
 // Memory model: writer side = system-scope release fence before a flag store (writes back the L2
 // of this XCD), reader side = system-scope acquire after the flag wait (invalidates non-local L2
 // lines), per the AMDGPU memory model for multi-L2 agents.
@@ -40,6 +42,7 @@ struct XgmiSignal {
 struct XgmiArgs {
   float4* bufs[DMLC_XGMI_MAX_RANKS];
   XgmiSignal* sigs[DMLC_XGMI_MAX_RANKS];
+  uint32_t* host_err; // mapped pinned host word (device pointer), or null
   int rank;
   int64_t off4, n4;   // bucket, in float4 units
 };
@@ -67,9 +70,11 @@ __device__ __forceinline__ void peer_barrier(const XgmiArgs& a, int which, uint3
     XgmiSignal* self = a.sigs[a.rank];
     const uint32_t* mine = &self->flag[which][b][t];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int32_t)(ld_sys(mine) - e) < 0) {
+    // a sticky error (an earlier launch lost a peer) drains this launch without waiting
+    while (ld_sys(&self->err) == 0u && (int32_t)(ld_sys(mine) - e) < 0) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > TIMEOUT_TICKS) {
         __hip_atomic_fetch_or(&self->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a.host_err) __hip_atomic_fetch_or(a.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -113,6 +118,8 @@ struct XgmiCtx {
   int64_t numel = 0;
   float* buf = nullptr;
   XgmiSignal* sig = nullptr;
+  uint32_t* host_err = nullptr;      // pinned, mapped (host view)
+  uint32_t* host_err_dev = nullptr;  // the same word as the kernels address it
   float* peer_buf[DMLC_XGMI_MAX_RANKS] = {};
   XgmiSignal* peer_sig[DMLC_XGMI_MAX_RANKS] = {};
   bool opened = false;
@@ -156,6 +163,22 @@ int dmlc_xgmi_create(int rank, int world, int64_t numel) {
     }
   }
   if (e == hipSuccess) e = hipMemset(c->sig, 0, sizeof(XgmiSignal));
+  if (e == hipSuccess) {
+    // host mirror of the error word: optional (without it dmlc_xgmi_error copies from the device)
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->host_err), sizeof(uint32_t),
+                      hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+      *c->host_err = 0u;
+      if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->host_err_dev), c->host_err, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(c->host_err);
+        c->host_err = nullptr;
+        c->host_err_dev = nullptr;
+      }
+    } else {
+      (void)hipGetLastError();
+      c->host_err = nullptr;
+    }
+  }
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     fail("xgmi_create", e);
@@ -227,6 +250,7 @@ hipError_t dmlc_xgmi_allreduce(int id, int64_t offset, int64_t numel, int blocks
     a.sigs[p] = c->peer_sig[p];
   }
   a.rank = c->rank;
+  a.host_err = c->host_err_dev;
   a.off4 = offset / 4;
   a.n4 = numel / 4;
   const int64_t shard4 = (a.n4 + c->world - 1) / c->world;
@@ -246,6 +270,7 @@ hipError_t dmlc_xgmi_allreduce(int id, int64_t offset, int64_t numel, int blocks
 int dmlc_xgmi_error(int id) {
   XgmiCtx* c = get(id);
   if (!c) return -1;
+  if (c->host_err) return (int)__atomic_load_n(c->host_err, __ATOMIC_ACQUIRE);   // no HIP call, no sync
   uint32_t v = 0;
   if (hipMemcpy(&v, &c->sig->err, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return (int)v;
@@ -262,6 +287,7 @@ void dmlc_xgmi_destroy(int id) {
   }
   (void)hipFree(c->buf);
   (void)hipFree(c->sig);
+  if (c->host_err) (void)hipHostFree(c->host_err);
   std::lock_guard<std::mutex> l(g_mu);
   g_ctx[id] = nullptr;
   delete c;

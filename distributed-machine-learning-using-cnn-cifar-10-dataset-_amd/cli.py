@@ -82,9 +82,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default=d.allreduce,
                    help="gradient all-reduce: xGMI peer-to-peer kernel (auto: when it self-tests and "
                         "measures faster than RCCL) or RCCL")
-    p.add_argument("--dp_schedule", choices=["serial", "overlap"], default=d.dp_schedule,
+    p.add_argument("--dp_schedule", choices=["auto", "serial", "overlap"], default=d.dp_schedule,
                    help="N>1 fused CNN step: one stream + one all-reduce (serial), or the fc bucket's "
-                        "all-reduce + SGD on a comm stream under the conv backward (overlap)")
+                        "all-reduce + SGD on a comm stream under the conv backward (overlap); auto times "
+                        "both at start-up (max over ranks) and keeps the faster")
+    p.add_argument("--steps_per_graph", type=int, default=d.steps_per_graph,
+                   help="longest chain of training steps captured into one HIP graph")
     p.add_argument("--pg_timeout_s", type=float, default=d.pg_timeout_s)
     p.add_argument("--graph", type="bool", default=d.graph)
     p.add_argument("--trace", choices=["", "roctx", "torch"], default=d.trace)

@@ -75,7 +75,8 @@ class TrainConfig:
     metrics_file: Optional[str] = None    # JSONL metrics (default: <log_dir>/metrics.jsonl on the chief)
     comm_dtype: str = "fp32"              # gradient all-reduce dtype: fp32 | bf16
     allreduce: str = "auto"               # gradient all-reduce: auto | rccl | xgmi (parallel/xgmi.py)
-    dp_schedule: str = "serial"           # N>1 fused step: serial | overlap (engine/fused.py; bench tunes)
+    dp_schedule: str = "auto"             # N>1 fused step: auto (measured at start) | serial | overlap
+    steps_per_graph: int = 8              # longest chain of training steps per HIP graph replay
     pg_timeout_s: float = 300.0           # process-group timeout (fail-fast on a dead rank)
     graph: bool = True                    # capture the fused step into a HIP graph
     trace: str = ""                       # '' | 'roctx' (phase ranges for rocprofv3 --marker-trace)

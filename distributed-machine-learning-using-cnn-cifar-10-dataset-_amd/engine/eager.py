@@ -16,6 +16,7 @@ import torch
 import torch.distributed as dist
 
 from .. import config as C
+from ..data.order import OrderSpec
 from ..models import build_model
 
 
@@ -39,8 +40,9 @@ class EagerTrainer:
         self.seed = seed
         self.augment = augment
         self.n_data = self.data.shape[0]
-        self.shard = self.n_data // world_size
-        self.period = max(1, self.shard // self.B)
+        # the same generated order as the fused kernels (data/order.py), so engines agree step by step
+        self.order = OrderSpec(self.n_data, self.B, world_size, rank, seed)
+        self.period = self.order.period
         self.cur_epoch = -1
         self.perm = None
         self.global_step = 0
@@ -60,9 +62,7 @@ class EagerTrainer:
         return self.lr0 * self.decay ** math.floor(step / self.decay_steps)
 
     def epoch_permutation(self, epoch: int) -> torch.Tensor:
-        g = torch.Generator().manual_seed(self.seed * 1000003 + epoch)
-        perm = torch.randperm(self.n_data, generator=g)
-        return perm[self.rank::self.world_size][: self.period * self.B]
+        return self.order.epoch_shard(epoch)
 
     def batch(self, step: int):
         epoch = step // self.period

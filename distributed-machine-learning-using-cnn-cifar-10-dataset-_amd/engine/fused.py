@@ -13,8 +13,11 @@ SURVEY.md §3.3) is nine kernel launches, all reading their inputs from device m
                  and conv2 weight/bias gradients (8-wave blocks as two 4-wave halves); split-K slabs
   8 sgd          partial reduction + SGD + LR schedule + bf16 shadow refresh + global_step++ + stats
 
-The batch index list is read through the device-resident global_step (``perm[step % period]``),
-so the whole step is a static HIP graph replayed once per step.  With data parallelism the fc
+Every data-consuming kernel computes its batch rows from the device-resident global_step and the
+generated epoch order (data/order.py: a keyed Feistel permutation per epoch, no index buffer), so
+the whole step is a static HIP graph and ``k`` consecutive steps -- across epoch boundaries -- are
+one graph replay.  Any batch size works: the kernels run on the batch padded to the 16-row tile and
+the head gives padding rows zero loss weight (their gradients are exactly zero).  With data parallelism the fc
 gradients (90 % of the bytes, complete after launch 5) are all-reduced over RCCL on a side stream
 while launches 6-7 run, then the conv bucket, then the SGD applies.
 """
@@ -27,6 +30,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import config as C
+from ..data.order import OrderSpec
 from ..models import cifar_cnn as M
 from ..ops import _ext
 
@@ -63,22 +67,29 @@ class FusedCifarEngine:
                  relu_logits: bool = True, crop_offset=(4, 4), world_size: int = 1, rank: int = 0,
                  process_group=None, seed: int = 0, fc1_split: Optional[int] = None, g1: Optional[int] = None,
                  g2: Optional[int] = None, stats_len: int = 4096, comm_dtype: str = "fp32",
-                 capture_comm: bool = False, dtype: str = "bf16", allreduce: str = "auto",
-                 dp_schedule: str = "overlap"):
+                 capture_comm: Optional[bool] = None, dtype: str = "bf16", allreduce: str = "auto",
+                 dp_schedule: str = "serial", dp_force: bool = False):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
         dev = self.device
-        B = int(batch_size)
-        if B % 16 != 0 or B < 16:
-            raise ValueError("fused engine needs a batch size that is a positive multiple of 16")
-        self.B = B
+        Bv = int(batch_size)
+        if Bv < 1:
+            raise ValueError("batch size must be >= 1")
+        B = -(-Bv // 16) * 16              # kernel batch: padded to the 16-row MFMA tile
+        self.B, self.Bv = B, Bv
         self.world_size, self.rank, self.pg = world_size, rank, process_group
+        # dp_force: run the data-parallel step (all-reduce + apply) even at world_size 1 -- exercises
+        # the collective path (e.g. a captured RCCL all-reduce) on a single GPU
+        self.dp = world_size > 1 or dp_force
         self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
         self.relu_logits = relu_logits
         self.cy, self.cx = crop_offset
         self.comm_dtype = comm_dtype
-        self.capture_comm = capture_comm
+        if capture_comm is None:     # RCCL collectives go into the step graph unless told otherwise
+            capture_comm = (self.dp and self._pg_backend() == "nccl"
+                            and os.environ.get("DMLC_CAPTURE_COMM", "1") != "0")
+        self.capture_comm = bool(capture_comm)
         self.seed = seed
         if dtype not in ("bf16", "fp8"):
             raise ValueError("fused engine dtype must be bf16 or fp8")
@@ -89,10 +100,9 @@ class FusedCifarEngine:
         self.data = data.to(dev).contiguous()
         self.labels = labels.to(dev, torch.int32).contiguous()
         self.n_data = self.data.shape[0]
-        self.shard = self.n_data // world_size
-        self.period = max(1, self.shard // B)
-        self.perm = torch.zeros(self.period * B, dtype=torch.int32, device=dev)
-        self.cur_epoch = -1
+        self.order = OrderSpec(self.n_data, Bv, world_size, rank, seed)
+        self.period = self.order.period          # steps per epoch
+        self.order_desc = self.order.descriptor()   # host int64 [6]: the kernels' index source
 
         # --- parameters + shadows -------------------------------------------------------------
         if flat_params is None:
@@ -100,14 +110,17 @@ class FusedCifarEngine:
         self.master = flat_params.to(dev, torch.float32).contiguous().clone()
         # gradient all-reduce: xGMI peer-to-peer kernel over an IPC-shared grad buffer when every
         # rank can map every peer and it measures faster than RCCL (parallel/xgmi.py), else RCCL
-        self.xgmi, self.comm_info = None, {"allreduce": "rccl" if world_size > 1 else "none"}
+        self.xgmi, self.comm_info = None, {"allreduce": "rccl" if self.dp else "none"}
         self._buckets = {True: (M.FC_BUCKET_OFFSET, self.master.numel() - M.FC_BUCKET_OFFSET),
                          False: (0, M.FC_BUCKET_OFFSET)}
         if world_size > 1 and dev.type == "cuda" and comm_dtype == "fp32" and allreduce != "rccl":
             from ..parallel import xgmi as X
-            self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev,
-                                                 [self._buckets[True], self._buckets[False]], mode=allreduce,
-                                                 group=process_group)
+            # timed on the call pattern the step will issue: one whole-buffer all-reduce (serial) or
+            # the fc bucket then the conv bucket (overlap)
+            pattern = ([(0, self.master.numel())] if dp_schedule == "serial"
+                       else [self._buckets[True], self._buckets[False]])
+            self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev, pattern,
+                                                 mode=allreduce, group=process_group)
         if self.xgmi is not None:
             self.grad = self.xgmi.buf[:self.master.numel()]
             self.grad.zero_()
@@ -191,14 +204,18 @@ class FusedCifarEngine:
                     + _gemm_params(16, 8, B, 16, 0, 8, 0, 1, 3, nvalid=10)))       # db3
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
-        self.multi = None                  # (k, graph of k chained steps), see capture()
-        self.comm_stream = torch.cuda.Stream(device=dev) if world_size > 1 else None
+        self.chains: Dict[int, Optional[torch.cuda.CUDAGraph]] = {}   # k -> graph of k chained steps
+        self.comm_stream = torch.cuda.Stream(device=dev) if self.dp else None
         # N>1 step schedule: "overlap" = two buckets, fc all-reduce + fc SGD on the comm stream under
         # the conv backward; "serial" = one stream, one all-reduce of the whole flat gradient, one SGD
         # launch (no fork/join, no co-resident comm/SGD blocks slowing the conv kernels).
         # tune_schedule() measures both and keeps the faster.
         assert dp_schedule in ("overlap", "serial"), dp_schedule
         self.dp_schedule = dp_schedule
+        self._captured_schedule = None
+        if self.dp:
+            self.comm_info.update(schedule=dp_schedule, backend=self._backend(),
+                                  captured_comm=bool(self.capture_comm or self.xgmi is not None))
         self.side_stream = torch.cuda.Stream(device=dev)
         self.host_step = 0
         self.refresh_shadows()
@@ -224,23 +241,25 @@ class FusedCifarEngine:
 
     # --- data order ---------------------------------------------------------------------------
     def epoch_permutation(self, epoch: int) -> torch.Tensor:
-        """Rank-sharded permutation of the dataset for ``epoch`` (D6: every rank sees a disjoint
-        shard; the same global order on every rank because the seed is shared).  Generated on the
-        device (no host round trip at epoch boundaries)."""
-        g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + epoch)
-        perm = torch.randperm(self.n_data, generator=g, device=self.device)
-        shard = perm[self.rank::self.world_size][: self.period * self.B]
-        return shard.to(torch.int32)
+        """This rank's dataset rows for ``epoch`` (int32 [period * Bv], batch after batch): the
+        generated order the kernels evaluate in place (data/order.py; D6: disjoint rank shards)."""
+        return self.order.epoch_shard(epoch).to(torch.int32)
 
-    def _maybe_new_epoch(self):
-        epoch = self.host_step // self.period
-        if epoch != self.cur_epoch:
-            self.perm.copy_(self.epoch_permutation(epoch))     # stream-ordered, before the step's graph
-            self.cur_epoch = epoch
+    def batch_indices(self, step: int) -> torch.Tensor:
+        """Dataset rows (int32 [Bv]) this rank trains on at global step ``step``."""
+        return self.order.batch(step).to(torch.int32)
+
+    def _padded(self, idx: torch.Tensor) -> torch.Tensor:
+        """An explicit index list of Bv rows padded to the kernel batch (last row repeated)."""
+        idx = idx.to(self.device, torch.int32).reshape(-1)
+        if idx.numel() == self.B:
+            return idx.contiguous()
+        assert 1 <= idx.numel() <= self.B, idx.numel()
+        return torch.cat([idx, idx[-1:].expand(self.B - idx.numel())]).contiguous()
 
     # --- kernels ------------------------------------------------------------------------------
     def _forward(self, idx, counter, period, train=True, logits_out=None):
-        o, p, B = self.ops, self.pv, self.B
+        o, p = self.ops, self.pv
         if self.fused_fwd and not self.fp8:        # conv1 + pool1 + conv2 + pool2 in one launch
             o.conv12_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
                          self.am1, self.w2f, p["conv2_bias"], self.p2, self.am2)
@@ -254,18 +273,20 @@ class FusedCifarEngine:
         f = self._fc1_fwd
         o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
         o.head(self.h1part, p["full_bias_1"], self.fc2t, p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d,
-               self.fc2n, self.labels, idx, counter, period, 1.0 / (B * self.world_size), self.relu_logits, train,
-               self.h1, self.h2, self.dl, self.dh1, self.dh2, self.loss_part, self.correct_part, logits_out)
+               self.fc2n, self.labels, idx, counter, period, 1.0 / (self.Bv * self.world_size), self.relu_logits,
+               train, self.h1, self.h2, self.dl, self.dh1, self.dh2, self.loss_part, self.correct_part, logits_out,
+               self.Bv)
 
     def _fc_backward(self):
         f = self._fc_bwd
         self.ops.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
 
-    def _conv_backward(self):
+    def _conv_backward(self, src=None):
         o = self.ops
+        idx, counter, period = src or (self.order_desc, self.step_t, self.period)
         o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         if self.merged_wgrad:
-            o.wgrad(self.data, self.perm, self.step_t, self.period, self.cy, self.cx, self.dp1, self.am1,
+            o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
                     self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2)
             return
         # the two weight-gradient kernels are independent: fork them onto two streams (two parallel
@@ -274,7 +295,7 @@ class FusedCifarEngine:
         self.side_stream.wait_stream(main)
         with torch.cuda.stream(self.side_stream):
             o.conv2_wgrad(self.p1, self.dy2, self.part2, self.partb2)
-        o.conv1_wgrad(self.data, self.perm, self.step_t, self.period, self.cy, self.cx, self.dp1, self.am1,
+        o.conv1_wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
                       self.part1, self.partb1)
         main.wait_stream(self.side_stream)
 
@@ -284,7 +305,7 @@ class FusedCifarEngine:
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                      self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
                                                                       if self.fp8 else (None, None, None)),
-                     roles, finalize, self.B)
+                     roles, finalize, self.Bv)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -307,14 +328,25 @@ class FusedCifarEngine:
         if self.xgmi is not None:
             self.xgmi.check()
 
+    def _pg_backend(self) -> str:
+        import torch.distributed as dist
+        return dist.get_backend(self.pg) if dist.is_available() and dist.is_initialized() else "none"
+
+    def _backend(self) -> str:
+        if self.xgmi is not None:
+            return "xgmi"
+        if not self.dp:
+            return "none"
+        return self._pg_backend()
+
     # segments of one step: each is a capturable list of launches on the current stream
     def _seg_compute_a(self):
-        self._forward(self.perm, self.step_t, self.period, train=True)
+        self._forward(self.order_desc, self.step_t, self.period, train=True)
         self._fc_backward()
 
     def _seg_compute_b(self):
         self._conv_backward()
-        self._sgd(mode=0 if self.world_size == 1 else 1)
+        self._sgd(mode=1 if self.dp else 0)
 
     def _seg_apply(self):
         self._sgd(mode=2, scale=1.0)
@@ -327,16 +359,22 @@ class FusedCifarEngine:
     def _seg_apply_conv(self):
         self._sgd(mode=2, scale=1.0, roles=1, finalize=True)
 
-    def compute_gradients(self):
-        """Forward + backward only (no update); the full gradient lands in ``self.grad``."""
-        self._maybe_new_epoch()
-        self._seg_compute_a()
-        self._conv_backward()
+    def compute_gradients(self, idx: Optional[torch.Tensor] = None):
+        """Forward + backward only (no update); the full gradient lands in ``self.grad``.
+        ``idx``: explicit dataset rows (int32 [Bv]) instead of this step's generated batch."""
+        if idx is None:
+            self._seg_compute_a()
+            self._conv_backward()
+        else:
+            ids = self._padded(idx)
+            self._forward(ids, None, 1, train=True)
+            self._fc_backward()
+            self._conv_backward(src=(ids, None, 1))
         self._sgd(mode=1)
         return self.grad
 
     def _eager_step(self):
-        if self.world_size == 1:
+        if not self.dp:
             self._seg_compute_a()
             self._seg_compute_b()
             return
@@ -383,64 +421,74 @@ class FusedCifarEngine:
         main.wait_stream(self.comm_stream)
 
     # --- graph capture --------------------------------------------------------------------------
-    def capture(self, steps_per_graph: int = 8):
-        """Capture the step into HIP graph(s).  N=1: one graph.  N>1 over xGMI: one graph holding
-        compute, both all-reduce kernels and the two SGD halves on two streams.  N>1 over RCCL:
-        compute graphs around eager RCCL collectives (or one graph when capture_comm=True).
+    @property
+    def single_graph(self) -> bool:
+        """The whole step (collectives included) is one capturable launch sequence."""
+        return not self.dp or self.capture_comm or self.xgmi is not None
 
-        When the whole step is one graph, a second graph chains ``steps_per_graph`` complete steps
-        (every step reads its batch and LR through the device step counter, so consecutive steps
-        need no host work): :meth:`run` replays it inside an epoch and saves the host launch gap
-        between graphs (~5 us per step)."""
+    def capture(self, steps_per_graph: int = 8):
+        """Capture the step into HIP graph(s).  N=1, N>1 over xGMI and N>1 over RCCL with
+        ``capture_comm`` (the default): the whole step -- compute, all-reduce, SGD, on one or two
+        streams -- is one graph, and further graphs chain 2, 4, ... ``steps_per_graph`` complete
+        steps (every step reads its batch and LR through the device step counter, so consecutive
+        steps need no host work, across epoch boundaries too).  :meth:`run` replays any step count
+        as a sum of chains -- no single-step tails, no host gap between the chained steps.
+        RCCL without ``capture_comm``: compute graphs around eager collectives (no chains)."""
         torch.cuda.synchronize(self.device)
-        self.graphs, self.multi = [], None
+        self.graphs, self.chains = [], {}
         pool = torch.cuda.graph_pool_handle()
-        single = self.world_size == 1 or self.capture_comm or self.xgmi is not None
-        if single:
+        if self.single_graph:
             segs = [self._eager_step]
         elif self.dp_schedule == "serial":
             segs = [self._seg_compute_ab, self._seg_apply]
         else:
             segs = [self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv]
         self._captured_schedule = self.dp_schedule
-        if single and steps_per_graph > 1:
-            k = int(steps_per_graph)
-            self.multi = (k, None)
-            segs = segs + [lambda: [self._eager_step() for _ in range(k)]]
-        # state (step counter, master weights) must be identical before and after capture: a
-        # capture records launches without running them, so nothing changes here.
+        # a capture records launches without running them: the step counter and weights are
+        # identical before and after
         for fn in segs:
-            g = torch.cuda.CUDAGraph()
-            s = torch.cuda.Stream(device=self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, pool=pool, stream=s):
-                    fn()
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            self.graphs.append(g)
-        if self.multi is not None:
-            self.multi = (self.multi[0], self.graphs.pop())
+            self.graphs.append(self._capture_one(fn, pool))
+        if self.single_graph:
+            k = 2
+            while k <= int(steps_per_graph):
+                self.chains[k] = self._capture_one(lambda k=k: [self._eager_step() for _ in range(k)], pool)
+                k *= 2
+        self.chains[1] = self.graphs[0] if self.single_graph else None
         torch.cuda.synchronize(self.device)
 
+    def _capture_one(self, fn, pool):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, pool=pool, stream=s):
+                fn()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        return g
+
+    @property
+    def multi(self):
+        """(k, graph) of the longest captured chain, or None."""
+        ks = [k for k, g in getattr(self, "chains", {}).items() if g is not None and k > 1]
+        return (max(ks), self.chains[max(ks)]) if ks else None
+
     def run(self, n: int):
-        """``n`` complete training steps (asynchronous).  Inside an epoch, whole ``steps_per_graph``
-        chunks replay the multi-step graph; epoch boundaries (host-side permutation refresh) and the
-        remainder go through :meth:`step`."""
+        """``n`` complete training steps (asynchronous): the longest captured chains first, then the
+        binary decomposition of the remainder (e.g. 21 = 8 + 8 + 4 + 1 replays)."""
         n = int(n)
-        while n > 0:
-            self._maybe_new_epoch()
-            left_in_epoch = self.period - self.host_step % self.period
-            if self.multi is not None and n >= self.multi[0] and left_in_epoch >= self.multi[0]:
-                self.multi[1].replay()
-                self.host_step += self.multi[0]
-                n -= self.multi[0]
-            else:
+        chains = {k: g for k, g in getattr(self, "chains", {}).items() if g is not None}
+        if not self.graphs or not chains:
+            for _ in range(n):
                 self.step()
-                n -= 1
+            return
+        for k in sorted(chains, reverse=True):
+            while n >= k:
+                chains[k].replay()
+                self.host_step += k
+                n -= k
 
     def step(self):
         """One training step (asynchronous: returns once launched)."""
-        self._maybe_new_epoch()
         if not self.graphs:
             self._eager_step()
         elif len(self.graphs) == 1:
@@ -451,21 +499,27 @@ class FusedCifarEngine:
             self._dp_step([g.replay for g in self.graphs])
         self.host_step += 1
 
-    def tune_schedule(self, iters: int = 30, steps_per_graph: int = 8, log=None) -> str:
-        """N>1: capture each DP step schedule, time ``iters`` real training steps of each (max over
-        ranks, so every rank takes the same decision), keep the faster one captured.  The timed steps
-        are ordinary training steps (the step counter advances).  Returns the chosen schedule."""
-        if self.world_size == 1:
+    def tune_schedule(self, iters: int = 30, steps_per_graph: int = 8, rounds: int = 2, log=None) -> str:
+        """Data-parallel step: capture each schedule (overlap / serial), time ``iters`` real
+        training steps of each (max over ranks, so every rank takes the same decision) over
+        ``rounds`` alternating rounds (overlap, serial, serial, overlap, ...), keep the minimum per
+        schedule and the faster schedule captured.  Both windows replay the same chain
+        decomposition and cross no host work (the data order is generated in-kernel), so neither
+        pays for anything the other does not.  The timed steps are ordinary training steps."""
+        if not self.dp:
             return self.dp_schedule
         import time
         import torch.distributed as dist
-        nccl = dist.get_backend(self.pg) == "nccl"
+        nccl = self._backend() == "nccl" or (self.xgmi is not None and dist.get_backend(self.pg) == "nccl")
         bdev = self.device if nccl else torch.device("cpu")
-        times = {}
-        for sched in ("overlap", "serial"):
+        times = {"overlap": [], "serial": []}
+        order = []
+        for r in range(max(1, rounds)):
+            order += ["overlap", "serial"] if r % 2 == 0 else ["serial", "overlap"]
+        for sched in order:
             self.dp_schedule = sched
             self.capture(steps_per_graph)
-            self.run(2)
+            self.run(steps_per_graph)
             torch.cuda.synchronize(self.device)
             dist.barrier(group=self.pg)
             t0 = time.perf_counter()
@@ -473,9 +527,10 @@ class FusedCifarEngine:
             torch.cuda.synchronize(self.device)
             t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=bdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
-            times[sched] = float(t.item()) / iters
-        best = min(times, key=times.get)
-        self.comm_info.update(schedule=best, schedule_us={k: round(v * 1e6, 1) for k, v in times.items()})
+            times[sched].append(float(t.item()) / iters)
+        best_t = {k: min(v) for k, v in times.items()}
+        best = min(best_t, key=best_t.get)
+        self.comm_info.update(schedule=best, schedule_us={k: round(v * 1e6, 1) for k, v in best_t.items()})
         if log:
             log(f"dp schedule: {best} ({self.comm_info['schedule_us']})")
         if best != self.dp_schedule:
@@ -494,18 +549,18 @@ class FusedCifarEngine:
         if self.fp8:    # eval launches carry no step counter: they read scale slot 0 (see cnn_fp8.hip)
             self.scale_w[0] = self.scale_w[self.host_step & 1]
         n = data.shape[0]
-        nb = math.ceil(n / self.B)
+        nb = math.ceil(n / self.Bv)
         if max_batches:
             nb = min(nb, max_batches)
         correct, total = 0, 0
         try:
             for i in range(nb):
-                ids = torch.arange(i * self.B, (i + 1) * self.B, device=self.device, dtype=torch.int32)
-                valid = int(min(self.B, n - i * self.B))
+                ids = torch.arange(i * self.Bv, i * self.Bv + self.B, device=self.device, dtype=torch.int32)
+                valid = int(min(self.Bv, n - i * self.Bv))
                 ids = torch.clamp(ids, max=n - 1)
                 self._forward(ids, None, 1, train=False, logits_out=self.logits_buf)
                 pred = self.logits_buf[:valid].argmax(dim=1)
-                correct += int((pred == labels[i * self.B:i * self.B + valid].long()).sum())
+                correct += int((pred == labels[i * self.Bv:i * self.Bv + valid].long()).sum())
                 total += valid
         finally:
             self.data, self.labels = saved
@@ -513,11 +568,12 @@ class FusedCifarEngine:
 
     @torch.no_grad()
     def forward_logits(self, idx: torch.Tensor) -> torch.Tensor:
-        """Logits (fp32 [B,10]) of dataset rows ``idx`` (int32 [B]) — for tests."""
+        """Logits (fp32 [n,10]) of dataset rows ``idx`` (int32 [n], n <= B) — for tests."""
         if self.fp8:
             self.scale_w[0] = self.scale_w[self.host_step & 1]
-        self._forward(idx.to(self.device, torch.int32).contiguous(), None, 1, train=False, logits_out=self.logits_buf)
-        return self.logits_buf.clone()
+        n = idx.numel()
+        self._forward(self._padded(idx), None, 1, train=False, logits_out=self.logits_buf)
+        return self.logits_buf[:n].clone()
 
     # --- state ----------------------------------------------------------------------------------
     def read_stats(self, step: int) -> Dict[str, float]:

@@ -28,6 +28,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import config as C
+from ..data.order import OrderSpec
 from ..models import resnet as R
 from ..ops import _ext
 from .fused import TICKET_WORDS
@@ -88,7 +89,7 @@ class FusedResNetEngine:
                  decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, world_size: int = 1,
                  rank: int = 0, process_group=None, seed: int = 0, groups: Optional[List[int]] = None,
                  stats_len: int = 4096, comm_dtype: str = "fp32", wgrad_branch: Optional[bool] = None,
-                 allreduce: str = "auto"):
+                 allreduce: str = "auto", capture_comm: Optional[bool] = None, dp_force: bool = False):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -100,15 +101,20 @@ class FusedResNetEngine:
         self.world_size, self.rank, self.pg = world_size, rank, process_group
         self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
         self.seed, self.comm_dtype = seed, comm_dtype
+        self.dp = world_size > 1 or dp_force     # dp_force: the all-reduce path at world_size 1 (tests)
+        if capture_comm is None:                 # RCCL collectives inside the step graph (nccl only)
+            import torch.distributed as dist
+            nccl = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+            capture_comm = self.dp and nccl and os.environ.get("DMLC_CAPTURE_COMM", "1") != "0"
+        self.capture_comm = bool(capture_comm)
 
         assert data.dtype == torch.uint8 and tuple(data.shape[1:]) == (32, 32, 3)
         self.data = data.to(dev).contiguous()
         self.labels = labels.to(dev, torch.int32).contiguous()
         self.n_data = self.data.shape[0]
-        self.shard = self.n_data // world_size
-        self.period = max(1, self.shard // B)
-        self.perm = torch.zeros(self.period * B, dtype=torch.int32, device=dev)
-        self.cur_epoch = -1
+        self.order = OrderSpec(self.n_data, B, world_size, rank, seed)   # generated order (data/order.py)
+        self.period = self.order.period
+        self.order_desc = self.order.descriptor()
 
         f0, s0 = R.init_flat_params(torch.Generator().manual_seed(seed))
         if flat_params is not None:
@@ -119,7 +125,7 @@ class FusedResNetEngine:
         self.state = s0.to(dev, torch.float32).contiguous().clone()
         # gradient all-reduce (N>1): xGMI peer-to-peer kernel over an IPC-shared buffer when it
         # self-tests and measures faster than RCCL (parallel/xgmi.py), else RCCL
-        self.xgmi, self.comm_info = None, {"allreduce": "rccl" if world_size > 1 else "none"}
+        self.xgmi, self.comm_info = None, {"allreduce": "rccl" if self.dp else "none"}
         if world_size > 1 and dev.type == "cuda" and comm_dtype == "fp32" and allreduce != "rccl":
             from ..parallel import xgmi as X
             self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev,
@@ -128,7 +134,7 @@ class FusedResNetEngine:
             self.grad = self.xgmi.buf[:self.master.numel()]
             self.grad.zero_()
         else:
-            self.grad = torch.zeros_like(self.master) if world_size > 1 else None
+            self.grad = torch.zeros_like(self.master) if self.dp else None
         P = {s.name[len(R.SCOPE) + 1:]: s for s in R.PARAM_SPECS}
         S = {s.name[len(R.SCOPE) + 1:]: s for s in R.STATE_SPECS}
         view = lambda buf, s: buf[s.offset:s.offset + s.numel]
@@ -164,6 +170,9 @@ class FusedResNetEngine:
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.chains: Dict[int, torch.cuda.CUDAGraph] = {}
+        if self.dp:
+            self.comm_info.update(captured_comm=bool(self.capture_comm or self.xgmi is not None))
         self.side_stream = torch.cuda.Stream(device=dev)
         # Backward schedule, measured per batch size (graph replay, img/s on 1 MI355X):
         #                          B=256   B=1024
@@ -178,6 +187,7 @@ class FusedResNetEngine:
         self.wgrad_branch = wgrad_branch
         self.merged_bwd = os.environ.get("DMLC_RN_MERGED_BWD", "1" if B <= 256 else "0") == "1"
         self.host_step = 0
+        self._stem_src = None          # explicit (idx, counter, period) of the stem wgrad, else generated
         self.refresh_shadows()
 
     # ------------------------------------------------------------------------------------------
@@ -204,15 +214,11 @@ class FusedResNetEngine:
         self.host_step = int(step)
 
     def epoch_permutation(self, epoch: int) -> torch.Tensor:
-        g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + epoch)
-        perm = torch.randperm(self.n_data, generator=g, device=self.device)
-        return perm[self.rank::self.world_size][: self.period * self.B].to(torch.int32)
+        """This rank's rows of ``epoch`` (int32 [period * B]), the order the kernels generate."""
+        return self.order.epoch_shard(epoch).to(torch.int32)
 
-    def _maybe_new_epoch(self):
-        epoch = self.host_step // self.period
-        if epoch != self.cur_epoch:
-            self.perm.copy_(self.epoch_permutation(epoch))
-            self.cur_epoch = epoch
+    def batch_indices(self, step: int) -> torch.Tensor:
+        return self.order.batch(step).to(torch.int32)
 
     # --- kernels ------------------------------------------------------------------------------
     def _forward(self, idx, counter, period, logits_out=None):
@@ -237,7 +243,8 @@ class FusedResNetEngine:
     def _wgrad(self, l):
         _, ci, co, h, s = LAYERS[l]
         if l == 0:
-            self.ops.rn_wgrad(ci, co, h, s, self.data, self.perm, self.step_t, self.period, 0, 0, None, self.gy[0],
+            idx, counter, period = self._stem_src or (self.order_desc, self.step_t, self.period)
+            self.ops.rn_wgrad(ci, co, h, s, self.data, idx, counter, period, 0, 0, None, self.gy[0],
                               self.z[0], self.stat[0], self.red[0], self.gamma[0], self.part[0])
         else:
             self.ops.rn_wgrad(ci, co, h, s, None, None, None, 1, 0, 0, self.a[l - 1], self.gy[l], self.z[l],
@@ -305,53 +312,86 @@ class FusedResNetEngine:
             self.xgmi.check()
 
     def _seg_compute(self):
-        self._forward(self.perm, self.step_t, self.period)
+        self._forward(self.order_desc, self.step_t, self.period)
         self._backward()
-        self._sgd(mode=0 if self.world_size == 1 else 1)
+        self._sgd(mode=1 if self.dp else 0)
 
     def _seg_apply(self):
         self._sgd(mode=2, scale=1.0)
 
     def _eager_step(self):
         self._seg_compute()
-        if self.world_size > 1:
+        if self.dp:
             self._allreduce(self.grad)
             self._seg_apply()
 
-    def compute_gradients(self) -> torch.Tensor:
-        """Forward + backward + slab reduction only (no update); the flat gradient lands in ``grad``."""
+    def compute_gradients(self, idx: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Forward + backward + slab reduction only (no update); the flat gradient lands in ``grad``.
+        ``idx``: explicit dataset rows (int32 [B]) instead of this step's generated batch."""
         if self.grad is None:
             self.grad = torch.zeros_like(self.master)
-        self._maybe_new_epoch()
-        self._forward(self.perm, self.step_t, self.period)
+        if idx is not None:
+            ids = idx.to(self.device, torch.int32).contiguous()
+            self._stem_src = (ids, None, 1)
+            try:
+                self._forward(ids, None, 1)
+                self._backward()
+                self._sgd(mode=1)
+            finally:
+                self._stem_src = None
+            return self.grad
+        self._forward(self.order_desc, self.step_t, self.period)
         self._backward()
         self._sgd(mode=1)
         return self.grad
 
     # --- graph capture --------------------------------------------------------------------------
-    def capture(self):
+    @property
+    def single_graph(self) -> bool:
+        return not self.dp or self.capture_comm or self.xgmi is not None
+
+    def _capture_one(self, fn, pool):
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, pool=pool, stream=s):
+                fn()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        return g
+
+    def capture(self, steps_per_graph: int = 8):
+        """The whole step as one graph (N=1, xGMI, or RCCL with ``capture_comm``) plus chains of
+        2, 4, ... ``steps_per_graph`` steps for :meth:`run`; RCCL without ``capture_comm``: compute
+        and apply graphs around an eager all-reduce."""
         torch.cuda.synchronize(self.device)
-        self.graphs = []
+        self.graphs, self.chains = [], {}
         pool = torch.cuda.graph_pool_handle()
-        if self.world_size == 1:
-            segs = [self._seg_compute]
-        elif self.xgmi is not None:          # the all-reduce is a kernel: the whole step is one graph
-            segs = [self._eager_step]
-        else:
-            segs = [self._seg_compute, self._seg_apply]
+        segs = [self._eager_step] if self.single_graph else [self._seg_compute, self._seg_apply]
         for fn in segs:
-            g = torch.cuda.CUDAGraph()
-            s = torch.cuda.Stream(device=self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
-                with torch.cuda.graph(g, pool=pool, stream=s):
-                    fn()
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            self.graphs.append(g)
+            self.graphs.append(self._capture_one(fn, pool))
+        if self.single_graph:
+            self.chains[1] = self.graphs[0]
+            k = 2
+            while k <= int(steps_per_graph):
+                self.chains[k] = self._capture_one(lambda k=k: [self._eager_step() for _ in range(k)], pool)
+                k *= 2
         torch.cuda.synchronize(self.device)
 
+    def run(self, n: int):
+        """``n`` training steps: longest chains first, then the binary decomposition of the rest."""
+        n = int(n)
+        if not self.chains:
+            for _ in range(n):
+                self.step()
+            return
+        for k in sorted(self.chains, reverse=True):
+            while n >= k:
+                self.chains[k].replay()
+                self.host_step += k
+                n -= k
+
     def step(self):
-        self._maybe_new_epoch()
         if not self.graphs:
             self._eager_step()
         elif len(self.graphs) == 1:

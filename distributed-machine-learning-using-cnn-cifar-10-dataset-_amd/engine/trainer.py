@@ -34,9 +34,17 @@ from ..utils.events import EventsWriter, MetricsLog
 from ..utils.trace import Tracer
 
 
+EXIT_COMM_FAILURE = 75      # a peer stopped participating / no device progress: the launcher restarts
+
+
+class CommFailure(RuntimeError):
+    """The gradient exchange can no longer complete (dead peer, stalled collective)."""
+
+
 # --- engine adapters: one interface over the fused HIP engine and the eager torch engine ------------
 class _FusedAdapter:
     kind = "fused"
+    TUNE_ITERS = 20
 
     def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, data, labels):
         from .fused import FusedCifarEngine
@@ -45,20 +53,47 @@ class _FusedAdapter:
                                     lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                     staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
                                     crop_offset=((32 - cfg.crop) // 2,) * 2, comm_dtype=cfg.comm_dtype,
-                                    dtype=cfg.dtype, allreduce=cfg.allreduce, dp_schedule=cfg.dp_schedule)
+                                    dtype=cfg.dtype, allreduce=cfg.allreduce,
+                                    dp_schedule="serial" if cfg.dp_schedule == "auto" else cfg.dp_schedule)
+        self.cfg = cfg
         self.graph = cfg.graph
         from ..models import cifar_cnn as M
         self.specs = M.PARAM_SPECS
 
-    def start(self):
-        pass
+    def start(self, log=print):
+        """Before the loop: one eager step (lazy code-object load, LDS attributes), then capture the
+        step and its chains.  With --dp_schedule=auto and enough steps left, both DP schedules are
+        timed on real training steps (max over ranks: one decision everywhere) and the faster kept."""
+        if not self.graph or self.cfg.generations <= self.global_step:
+            return
+        self.eng.step()
+        self.eng.capture(self.cfg.steps_per_graph)
+        windows = 4 * (self.TUNE_ITERS + self.cfg.steps_per_graph)
+        if (self.cfg.dp_schedule == "auto" and self.eng.dp and hasattr(self.eng, "tune_schedule")
+                and self.cfg.generations - self.global_step >= 10 * windows):
+            self.eng.tune_schedule(iters=self.TUNE_ITERS, steps_per_graph=self.cfg.steps_per_graph, log=log)
+
+    def run(self, n: int):
+        """``n`` training steps, as chained graph replays once captured (asynchronous)."""
+        if self.eng.graphs:
+            self.eng.run(n)
+        else:
+            for _ in range(n):
+                self.eng.step()
 
     def step(self):
-        self.eng.step()
-        if self.graph and not self.eng.graphs:
-            # the first step runs eagerly (lazy code-object load, LDS attributes); then the whole
-            # step is captured once and replayed as a HIP graph
-            self.eng.capture()
+        self.run(1)
+
+    def device_event(self):
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
+    def check_comm(self):
+        try:
+            self.eng.check_comm()
+        except RuntimeError as e:
+            raise CommFailure(str(e)) from e
 
     @property
     def global_step(self) -> int:
@@ -101,6 +136,7 @@ class _FusedResNetAdapter(_FusedAdapter):
                                      lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                      staircase=cfg.lr_schedule == "staircase", comm_dtype=cfg.comm_dtype,
                                      allreduce=cfg.allreduce)
+        self.cfg = cfg
         self.graph = cfg.graph
         self.specs, self.state_specs = R.PARAM_SPECS, R.STATE_SPECS
 
@@ -136,11 +172,25 @@ class _EagerAdapter:
                                crop=cfg.crop, seed=cfg.seed, augment=cfg.augment)
         self.specs = self.tr.model.specs
 
-    def start(self):
+    def start(self, log=print):
         pass
+
+    def run(self, n: int):
+        for _ in range(n):
+            self.tr.step()
 
     def step(self):
         self.tr.step()
+
+    def device_event(self):
+        if self.tr.device.type != "cuda":
+            return None
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
+    def check_comm(self):
+        pass
 
     @property
     def global_step(self) -> int:
@@ -179,21 +229,26 @@ def pick_impl(cfg: C.TrainConfig, device: torch.device) -> str:
     if cfg.impl != "auto":
         return cfg.impl
     if (device.type == "cuda" and cfg.model == "cifar_cnn" and cfg.dtype in ("bf16", "fp8") and cfg.crop == 24
-            and cfg.batch_size % 16 == 0 and not cfg.augment):
-        return "fused"
+            and not cfg.augment):
+        return "fused"                    # any batch size: masked tail rows (engine/fused.py)
     if (device.type == "cuda" and cfg.model == "resnet20" and cfg.dtype == "bf16" and cfg.crop == 32
             and cfg.batch_size % 16 == 0 and not cfg.augment):
         return "fused"
     return "eager"
 
 
-def _fault_injection(step: int, rank: int):
+def _fault_step() -> Optional[int]:
     """Test hook: DMLC_FAULT_STEP / DMLC_FAULT_RANK kill this rank hard at a step,
     on the first attempt only (DMLC_RESTART_COUNT is set by the launcher)."""
     fs = os.environ.get("DMLC_FAULT_STEP")
     if fs is None or int(os.environ.get("DMLC_RESTART_COUNT", "0")) > 0:
-        return
-    if step == int(fs) and rank == int(os.environ.get("DMLC_FAULT_RANK", "0")):
+        return None
+    return int(fs)
+
+
+def _fault_injection(step: int, rank: int):
+    fs = _fault_step()
+    if fs is not None and step == fs and rank == int(os.environ.get("DMLC_FAULT_RANK", "0")):
         print(f"[fault-injection] rank {rank} exiting at global_step {step}", flush=True)
         os._exit(17)
 
@@ -238,30 +293,66 @@ class Session:
             self.ckpt.save(self.engine.global_step, self.engine.tf_tensors())
 
     # --- main loop -----------------------------------------------------------------------------------
+    def _chunk(self, gs: int, i: int) -> int:
+        """Steps until the next host-side event: an output / eval point (local iteration counts, as in
+        the reference), the StopAtStep target, a fault-injection step; 1 under a torch.profiler
+        window (it counts steps)."""
+        cfg = self.cfg
+        n = min(cfg.generations - gs, cfg.output_every - i % cfg.output_every, cfg.eval_every - i % cfg.eval_every)
+        fs = _fault_step()
+        if fs is not None and gs < fs:
+            n = min(n, fs - gs)
+        if cfg.trace == "torch":
+            n = 1
+        return max(1, n)
+
+    def _wait_progress(self, ev):
+        """Device progress watchdog: the previous chunk must finish within the process-group timeout.
+        Collectives captured inside a graph are invisible to the process group's own watchdog, and a
+        stalled one would otherwise hold this rank forever; an xGMI barrier that timed out has set the
+        engine's error word, which check_comm() turns into a CommFailure."""
+        if ev is None:
+            return
+        deadline = time.time() + self.cfg.pg_timeout_s
+        while not ev.query():
+            if time.time() > deadline:
+                raise CommFailure(f"no device progress for {self.cfg.pg_timeout_s:.0f} s "
+                                  f"(rank {self.info.rank}, global_step ~{self.engine.global_step})")
+            time.sleep(0.0002)
+        self.engine.check_comm()
+
     def run(self) -> Dict[str, float]:
         cfg, eng = self.cfg, self.engine
         self.restore()
         self.save(force=True)            # CheckpointSaverHook.after_create_session
-        eng.start()
+        eng.start(log=self.log)
         self.log(f"[dmlc] engine={self.impl} model={cfg.model} dtype={cfg.dtype} batch={cfg.batch_size} "
                  f"world={self.info.world_size} device={self.info.device}")
         self.log("Starting Training")
-        i = 0
+        start = eng.global_step
         last_t, last_step = time.time(), eng.global_step
         result = {}
+        pending = None
         while eng.global_step < cfg.generations:        # StopAtStepHook(last_step=GENERATIONS)
             _fault_injection(eng.global_step, self.info.rank)
-            with self.tracer.range("step"):
-                eng.step()
+            i = eng.global_step - start                  # local iterations so far (the reference's i)
+            n = self._chunk(eng.global_step, i)
+            with self.tracer.range("steps"):
+                eng.run(n)
             self.tracer.step_done()
-            if (i + 1) % cfg.output_every == 0:
+            ev = eng.device_event()
+            self._wait_progress(pending)                 # one chunk in flight behind the host
+            pending = ev
+            i += n
+            if i % cfg.output_every == 0:
+                self._wait_progress(pending)
                 with self.tracer.range("stats"):
                     st = eng.stats()
                 now = time.time()
                 steps = eng.global_step - last_step
                 ips = steps * cfg.batch_size * self.info.world_size / max(1e-9, now - last_t)
                 self.log("global_step %s, task:%d_step %d, training accuracy %g"
-                         % (eng.global_step, cfg.task_index, i, st["accuracy"]))
+                         % (eng.global_step, cfg.task_index, i - 1, st["accuracy"]))
                 self.metrics.write(step=eng.global_step, loss=st["loss"], accuracy=st["accuracy"], lr=st["lr"],
                                    images_per_sec=ips, step_ms=1000.0 * (now - last_t) / max(1, steps))
                 if self.events is not None:
@@ -270,17 +361,20 @@ class Session:
                                                           "learning_rate": st["lr"]})
                 last_t, last_step = now, eng.global_step
                 result = dict(st, images_per_sec=ips)
-            if (i + 1) % cfg.eval_every == 0:
+            if i % cfg.eval_every == 0:
+                self._wait_progress(pending)
                 with self.tracer.range("eval"):
                     acc = eng.evaluate(*self.test, max_batches=cfg.eval_batches)
                 self.log(" --- Test Accuracy = {:.2f}%.".format(100.0 * acc))
                 self.metrics.write(step=eng.global_step, test_accuracy=acc)
                 result["test_accuracy"] = acc
+                last_t = time.time()                      # eval time is not training throughput
             if self.ckpt is not None and self.ckpt.due():
+                self._wait_progress(pending)             # never save weights of a broken exchange
                 with self.tracer.range("checkpoint"):
                     self.save()
-            i += 1
         eng.sync()
+        self._wait_progress(pending)
         self.tracer.close()
         self.save(force=True)            # CheckpointSaverHook.end
         result["global_step"] = eng.global_step
@@ -311,6 +405,12 @@ def main(argv=None) -> int:
         if info.rank == 0:
             print(f"done: {res}", flush=True)
         D.report_done(info)
+    except CommFailure as e:
+        # fail fast: a dead peer must not leave this rank training on un-reduced gradients or
+        # waiting forever in a collective; exit without the (collective) teardown, the launcher
+        # restarts the world from the latest checkpoint (RecoverableSession, cifar10cnn.py:222)
+        print(f"[dmlc] rank {info.rank}: gradient exchange failed: {e}; exiting for restart", flush=True)
+        os._exit(EXIT_COMM_FAILURE)
     finally:
         D.shutdown(info)
     return 0

@@ -39,8 +39,10 @@ def test_bool_flags():
 
 
 def test_dp_schedule_flag():
-    assert cli.parse([])[0].dp_schedule == "serial"
+    assert cli.parse([])[0].dp_schedule == "auto"
     assert cli.parse(["--dp_schedule=overlap"])[0].dp_schedule == "overlap"
+    assert cli.parse(["--dp_schedule=serial"])[0].dp_schedule == "serial"
+    assert cli.parse(["--steps_per_graph=4"])[0].steps_per_graph == 4
     with pytest.raises(SystemExit):
         cli.parse(["--dp_schedule=ring"])
 
@@ -185,3 +187,33 @@ def test_launcher_fault_injection_resumes_from_checkpoint(tmp_path):
     path = CK.latest_checkpoint(str(tmp_path))
     assert path.endswith("model.ckpt-15")
     assert int(CK.read_bundle(path)["global_step"]) == 15
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_self_launches_two_ranks(tmp_path):
+    """``python bench.py --gpus 2`` without a torchrun environment starts its own two ranks (before
+    any GPU call) and the JSON line proves the world it ran in."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--impl", "eager",
+                          "--batch", "8", "--steps", "2", "--warmup", "1", "--dataset-size", "256"],
+                         env=env, capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout              # rank 0 only
+    rec = lines[0]
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    comm = rec["config"]["comm"]
+    assert comm["world_size_seen"] == 2 and comm["backend"] == "gloo", comm
+    assert rec["config"]["global_batch"] == 16
+
+
+@pytest.mark.timeout(120)
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    env = dict(os.environ, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29999")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--impl", "eager",
+                          "--batch", "8", "--steps", "1", "--warmup", "1", "--dataset-size", "64"],
+                         env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 3, (out.returncode, out.stderr[-2000:])

@@ -40,7 +40,7 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedu
         eng.step()
     torch.cuda.synchronize()
     torch.save({"flat": eng.flat_params(), "step": eng.global_step(),
-                "shards": [eng.epoch_permutation(0).cpu()]}, os.path.join(out, f"r{rank}.pt"))
+                "batches": [eng.batch_indices(s) for s in range(steps)]}, os.path.join(out, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
@@ -61,12 +61,12 @@ def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype, all
     r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
     assert r0["step"] == r1["step"] == steps
     assert torch.equal(r0["flat"], r1["flat"])           # replicas identical after every step
-    # single process, batch 2B made of the two ranks' batches of each step
-    s0, s1 = r0["shards"][0], r1["shards"][0]
-    union = torch.cat([torch.cat([s0[i * B:(i + 1) * B], s1[i * B:(i + 1) * B]]) for i in range(len(s0) // B)])
+    # single process, batch 2B: the generated order makes its batch of every step exactly the two
+    # ranks' batches of that step, in rank order (data/order.py)
     x, y = _data()
     ref = FusedCifarEngine(2 * B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False)
-    ref.epoch_permutation = lambda epoch: union.to(torch.int32)
+    for s in range(steps):
+        assert torch.equal(ref.batch_indices(s), torch.cat([r0["batches"][s], r1["batches"][s]]))
     init = ref.flat_params().clone()
     for _ in range(steps):
         ref.step()
@@ -90,9 +90,10 @@ def _tune_rank(rank, world, port, out, allreduce):
     eng.step()
     eng.capture(steps_per_graph=2)
     best = eng.tune_schedule(iters=3, steps_per_graph=2)
+    captured = eng._captured_schedule
     eng.run(3)
     torch.cuda.synchronize()
-    torch.save({"flat": eng.flat_params(), "step": eng.global_step(), "best": best,
+    torch.save({"flat": eng.flat_params(), "step": eng.global_step(), "best": best, "captured": captured,
                 "info": dict(eng.comm_info)}, os.path.join(out, f"t{rank}.pt"))
     dist.destroy_process_group()
 
@@ -101,7 +102,8 @@ def _tune_rank(rank, world, port, out, allreduce):
 @pytest.mark.parametrize("allreduce", ["rccl", "xgmi"])
 def test_dp2_tune_schedule_agrees_across_ranks(tmp_path, allreduce):
     """tune_schedule(): both schedules timed (max over ranks), one decision on every rank, the
-    replicas stay identical and every timed step counts (1 + 2x(2 + 3) tuning + 3 = 14 steps)."""
+    replicas stay identical, the graphs kept are the winner's, and every timed step counts
+    (1 + 2 rounds x 2 schedules x (2 + 3) tuning + 3 = 24 steps)."""
     import torch.multiprocessing as mp
     from dmlc.cli import free_port
     mp.spawn(_tune_rank, args=(2, free_port(), str(tmp_path), allreduce), nprocs=2, join=True)
@@ -109,6 +111,54 @@ def test_dp2_tune_schedule_agrees_across_ranks(tmp_path, allreduce):
     t1 = torch.load(tmp_path / "t1.pt", weights_only=True)
     assert t0["best"] == t1["best"] in ("overlap", "serial")
     assert t0["info"]["schedule"] == t0["best"] and set(t0["info"]["schedule_us"]) == {"overlap", "serial"}
-    assert t0["step"] == t1["step"] == 14
+    assert t0["captured"] == t0["best"] and t1["captured"] == t1["best"]
+    assert t0["step"] == t1["step"] == 24
     assert torch.equal(t0["flat"], t1["flat"])
     assert torch.isfinite(t0["flat"]).all()
+
+
+def _nccl1_rank(rank, world, port, out, steps):
+    sys.path.insert(0, REPO)
+    import datetime
+    import torch.distributed as dist
+    import dmlc  # noqa: F401
+    from dmlc.engine.fused import FusedCifarEngine
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60), device_id=torch.device("cuda", 0))
+    x, y = _data()
+    res = {}
+    for sched in ("serial", "overlap"):
+        eng = FusedCifarEngine(32, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dp_force=True,
+                               dp_schedule=sched, allreduce="rccl")
+        assert eng.dp and eng.capture_comm and eng.single_graph, (eng.dp, eng.capture_comm)
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(steps - 1)
+        torch.cuda.synchronize()
+        res[sched] = {"flat": eng.flat_params(), "step": eng.global_step(), "info": dict(eng.comm_info)}
+    torch.save(res, os.path.join(out, "nccl1.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_captured_rccl_allreduce_world1_equals_single_gpu(tmp_path):
+    """The RCCL path with the all-reduce captured inside the step graph (capture_comm) and chained
+    steps, on a 1-rank nccl group (dp_force: the DP step -- reduce-only SGD, all-reduce, apply-only
+    SGD -- runs at world size 1).  A 1-rank sum is the identity, so it must equal the plain
+    single-GPU step bit for bit, for both step schedules."""
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    from dmlc.engine.fused import FusedCifarEngine
+    steps = 11
+    mp.spawn(_nccl1_rank, args=(1, free_port(), str(tmp_path), steps), nprocs=1, join=True)
+    res = torch.load(tmp_path / "nccl1.pt", weights_only=True)
+    x, y = _data()
+    ref = FusedCifarEngine(32, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False)
+    for _ in range(steps):
+        ref.step()
+    torch.cuda.synchronize()
+    for sched, r in res.items():
+        assert r["step"] == steps, sched
+        assert r["info"]["captured_comm"] and r["info"]["backend"] == "nccl", r["info"]
+        assert torch.equal(r["flat"], ref.flat_params()), sched

@@ -45,8 +45,7 @@ def test_forward_logits_match_reference(B):
 def test_gradients_match_reference(B):
     data, labels = _synthetic(4 * B, seed=3)
     eng = FusedCifarEngine(B, data, labels, seed=2)
-    eng._maybe_new_epoch()
-    idx = eng.perm[:B].cpu()
+    idx = eng.batch_indices(eng.host_step)
     grad = eng.compute_gradients().cpu()
     _, _, gref = _ref_grads(eng.flat_params(), data, labels, idx)
     gref = gref.cpu()
@@ -83,15 +82,17 @@ def test_merged_wgrad_launch_matches_two_kernels(B, g2, monkeypatch):
 
 
 def test_multi_step_graph_run_equals_eager_steps():
-    """run(n) replays a graph of 3 chained steps inside each epoch and single steps across epoch
-    boundaries; the result is bit-identical to n eager steps (same batches, same LR schedule)."""
+    """run(n) replays chains of 8/4/2/1 captured steps straight across epoch boundaries (the batch
+    order is generated in-kernel from the step counter); the result is bit-identical to n eager
+    steps (same batches, same LR schedule)."""
     B = 32
-    data, labels = _synthetic(5 * B, seed=9)          # period 5: chunks of 3 must stop at boundaries
+    data, labels = _synthetic(5 * B, seed=9)          # period 5: every chain crosses an epoch boundary
     kw = dict(seed=11, lr=1e-4, decay_steps=4, relu_logits=False)     # stays finite: NaN != NaN
     a = FusedCifarEngine(B, data, labels, **kw)
     b = FusedCifarEngine(B, data, labels, **kw)
     a.step()
-    a.capture(steps_per_graph=3)
+    a.capture(steps_per_graph=8)
+    assert sorted(a.chains) == [1, 2, 4, 8]
     a.run(20)
     for _ in range(21):
         b.step()
@@ -107,8 +108,7 @@ def test_sgd_step_matches_reference_update():
     data, labels = _synthetic(4 * B, seed=5)
     eng = FusedCifarEngine(B, data, labels, seed=4, lr=0.01)
     before = eng.flat_params().clone()
-    eng._maybe_new_epoch()
-    idx = eng.perm[:B].cpu()
+    idx = eng.batch_indices(eng.host_step)
     eng.step()
     torch.cuda.synchronize()
     after = eng.flat_params()
@@ -182,3 +182,61 @@ def test_fused_conv12_forward_equals_two_launches(monkeypatch):
         assert torch.equal(getattr(fused, n), getattr(split, n)), n
     assert torch.equal(lf, ls)
 
+
+
+def test_generated_order_in_kernels_matches_host_twin():
+    """The kernels' in-place Feistel order (common.h order_perm) picks exactly the rows the host
+    twin (data/order.py) names, at epoch starts, ends and far-away steps: the forward through the
+    generated order is bit-identical to the forward through the explicit index list."""
+    B = 32
+    data, labels = _synthetic(1000, seed=13)           # period 31
+    eng = FusedCifarEngine(B, data, labels, seed=14)
+    for step in (0, 1, 30, 31, 62, 1000, 123457):
+        eng.set_step(step)
+        eng._forward(eng.order_desc, eng.step_t, eng.period, train=False, logits_out=eng.logits_buf)
+        gen = eng.logits_buf.clone()
+        ref = eng.forward_logits(eng.batch_indices(step))
+        assert torch.equal(gen, ref), step
+
+
+def test_chained_run_across_n8_shard_epochs_equals_eager():
+    """The N=8 shard case: 50k rows / 8 ranks at B=256 is a 24-step epoch per rank.  A 6250-row
+    dataset gives one rank that epoch length; 48 steps as chained graph replays (two epoch
+    boundaries inside chains, no host work between them) are bit-identical to 48 eager steps."""
+    B = 256
+    data, labels = _synthetic(6250, seed=15)
+    kw = dict(seed=16, lr=1e-4, relu_logits=False)
+    a = FusedCifarEngine(B, data, labels, **kw)
+    b = FusedCifarEngine(B, data, labels, **kw)
+    assert a.period == 24
+    a.step()
+    a.capture()
+    a.run(47)
+    for _ in range(48):
+        b.step()
+    torch.cuda.synchronize()
+    assert a.global_step() == b.global_step() == 48
+    assert torch.isfinite(a.flat_params()).all()
+    assert torch.equal(a.flat_params(), b.flat_params())
+
+
+@pytest.mark.parametrize("B", [1, 2, 100, 127])
+def test_any_batch_size_masked_tail(B):
+    """Batches that are not a multiple of the 16-row tile: the kernels run on the padded batch, the
+    head gives padding rows zero weight -- gradients, loss and accuracy are those of the B real rows."""
+    data, labels = _synthetic(max(512, 4 * B), seed=17)
+    eng = FusedCifarEngine(B, data, labels, seed=18, lr=0.01)
+    assert eng.Bv == B and eng.B % 16 == 0 and eng.B - B < 16
+    idx = eng.batch_indices(0)
+    assert idx.numel() == B
+    grad = eng.compute_gradients().cpu().clone()
+    logits, loss, gref = _ref_grads(eng.flat_params(), data, labels, idx)
+    got_logits = eng.forward_logits(idx)
+    assert got_logits.shape == (B, 10)
+    assert _rel(got_logits, logits) < 1e-2, _rel(got_logits, logits)
+    g = gref.cpu()
+    assert _rel(grad, g) < 2e-2, _rel(grad, g)
+    eng.step()
+    torch.cuda.synchronize()
+    st = eng.read_stats(1)
+    assert abs(st["loss"] - float(loss)) < 1e-2 * max(1.0, abs(float(loss))), (st, float(loss))

@@ -37,7 +37,7 @@ def _rank(rank, world, port, out, graph, allreduce):
     eng.step()
     torch.cuda.synchronize()
     torch.save({"flat": eng.flat_params(), "state": eng.state.cpu(), "step": eng.global_step(),
-                "shard": eng.epoch_permutation(0).cpu()}, os.path.join(out, f"r{rank}.pt"))
+                "batch": eng.batch_indices(0)}, os.path.join(out, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
@@ -55,10 +55,8 @@ def test_resnet_dp2_matches_mean_of_rank_gradients(tmp_path, graph, allreduce):
     grads = []
     for k in (0, 1):
         ref = FusedResNetEngine(B, x, y, device="cuda:0", seed=5, lr=LR)
-        shard = r[k]["shard"]
-        ref.epoch_permutation = lambda epoch, s=shard: torch.cat([s, s]).to(torch.int32)   # row 0 = this rank's batch
         init = ref.flat_params().clone()
-        grads.append(ref.compute_gradients().cpu().clone())
+        grads.append(ref.compute_gradients(idx=r[k]["batch"]).cpu().clone())   # rank k's batch of step 0
     expect = -LR * (grads[0] + grads[1]) / 2
     got = r[0]["flat"] - init
     rel = float((got - expect).norm() / expect.norm())

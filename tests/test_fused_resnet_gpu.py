@@ -109,8 +109,7 @@ def test_forward_logits_match_reference(B):
 def test_each_kernel_matches_fp32_ops(B):
     data, labels = _data(4 * B, seed=3)
     eng = FusedResNetEngine(B, data, labels, seed=2)
-    eng._maybe_new_epoch()
-    idx = eng.perm[:B].cpu()
+    idx = eng.batch_indices(eng.host_step)
     eng.compute_gradients()
     errs = local_layer_errors(eng, data, labels, idx)
     bad = {k: v for k, v in errs.items() if v > 3e-2}
@@ -123,8 +122,7 @@ def test_end_to_end_gradients_close_to_fp32_model():
     B = 64
     data, labels = _data(4 * B, seed=3)
     eng = FusedResNetEngine(B, data, labels, seed=2)
-    eng._maybe_new_epoch()
-    idx = eng.perm[:B].cpu()
+    idx = eng.batch_indices(eng.host_step)
     grad = eng.compute_gradients().cpu()
     _, _, gref, _ = _ref(eng.flat_params(), eng.state.cpu(), data, labels, idx)
     cos = float(F.cosine_similarity(grad, gref, dim=0))
@@ -139,8 +137,7 @@ def test_sgd_step_and_bn_running_stats():
     data, labels = _data(4 * B, seed=5)
     eng = FusedResNetEngine(B, data, labels, seed=4, lr=0.05)
     before, st0 = eng.flat_params().clone(), eng.state.cpu().clone()
-    eng._maybe_new_epoch()
-    idx = eng.perm[:B].cpu()
+    idx = eng.batch_indices(eng.host_step)
     eng.step()
     torch.cuda.synchronize()
     _, loss, gref, st_ref = _ref(before, st0, data, labels, idx)

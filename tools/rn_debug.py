@@ -19,8 +19,7 @@ def main():
     data = torch.randint(0, 256, (4 * B, 32, 32, 3), dtype=torch.uint8, generator=g)
     labels = torch.randint(0, 10, (4 * B,), dtype=torch.int32, generator=g)
     eng = FusedResNetEngine(B, data, labels, seed=2)
-    eng._maybe_new_epoch()
-    idx = eng.perm[:B].cpu()
+    idx = eng.batch_indices(eng.host_step)
     eng.compute_gradients()
     for k, v in local_layer_errors(eng, data, labels, idx).items():
         print(f"{k:10s} {v:.5f}")

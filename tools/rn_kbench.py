@@ -46,7 +46,7 @@ def main():
     res = {"variant": os.environ.get("DMLC_VARIANT", ""), "batch": a.batch}
     for l, (_, ci, co, h, s) in enumerate(LAYERS):
         if l == 0:
-            f = lambda: o.rn_fwd(ci, co, h, s, eng.data, eng.perm, eng.step_t, eng.period, 0, 0, None, None, None,
+            f = lambda: o.rn_fwd(ci, co, h, s, eng.data, eng.order_desc, eng.step_t, eng.period, 0, 0, None, None, None,
                                  None, None, 0, None, eng.wf[0], eng.z[0], eng.stat[0])
         else:
             p = l - 1
@@ -64,7 +64,7 @@ def main():
                 o.rn_dgrad(ci, co, h, s, eng.gy[l], eng.z[l], eng.stat[l], eng.red[l], eng.gamma[l], eng.wd[l],
                            eng.a[p], eng.z[p], eng.stat[p], gsc, scm, eng.gy[p], eng.red[p]), a.iters)
     res["head"] = timeit(lambda: o.rn_head(eng.z[18], eng.stat[18], eng.gamma[18], eng.beta[18], eng.a[16], eng.fcw,
-                                           eng.fcb, eng.labels, eng.perm, eng.step_t, eng.period, 1.0 / eng.B,
+                                           eng.fcb, eng.labels, eng.order_desc, eng.step_t, eng.period, 1.0 / eng.B,
                                            eng.gy[18], eng.red[18], eng.fc_part, eng.loss_img, eng.correct_img,
                                            None), a.iters)
     res["sgd"] = timeit(lambda: eng._sgd(mode=0), a.iters)
