@@ -195,6 +195,10 @@ def main():
         for k in sorted(getattr(eng, "chains", {}) or {}):
             eng.run(k)
             graph_warm += k
+        # ... and rehearse the timed region's own replay sequence once (short runs only)
+        if args.steps <= 64:
+            eng.run(args.steps)
+            graph_warm += args.steps
     # run(n): n complete steps, as chained graph replays (fused engines) or n step() calls
     run = getattr(eng, "run", None) if capture is not None else None
     if run is None:

@@ -15,6 +15,11 @@ for s in $STEPS; do
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; ok $? tests ;;
     bench) timeout -k 10 300 python bench.py --steps 200 --warmup 20 > gpurun_out/bench.log 2>&1; ok $? bench ;;
     fused) timeout -k 10 400 python -u -m pytest tests/test_fused_gpu.py tests/test_fused_dp_gpu.py tests/test_fp8_gpu.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_fused.log 2>&1; ok $? fused ;;
+    fault) timeout -k 10 400 python -u -m pytest tests/test_fault_gpu.py -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_fault.log 2>&1; ok $? fault ;;
+    b20) timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/bench20.log 2>&1; ok $? b20 ;;
+    b400) timeout -k 10 200 python bench.py --steps 400 --warmup 20 > gpurun_out/bench400.log 2>&1; ok $? b400 ;;
+    b1024) timeout -k 10 200 python bench.py --steps 200 --warmup 20 --batch 1024 > gpurun_out/bench1024.log 2>&1; ok $? b1024 ;;
+    lat) timeout -k 10 200 python tools/launch_latency.py > gpurun_out/launch_latency.json 2> gpurun_out/launch_latency.err; ok $? lat ;;
     kbench) timeout -k 10 200 python tools/kbench.py > gpurun_out/kbench.json 2> gpurun_out/kbench.err; ok $? kbench ;;
     ktiming) DMLC_TIMING=1 timeout -k 10 200 python tools/ktiming.py > gpurun_out/ktiming.json 2> gpurun_out/ktiming.err; ok $? ktiming ;;
     rn) timeout -k 10 300 python bench.py --model resnet20 --steps 100 --warmup 10 > gpurun_out/bench_rn.log 2>&1; ok $? rn ;;
