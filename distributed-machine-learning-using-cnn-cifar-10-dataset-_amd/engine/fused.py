@@ -143,7 +143,6 @@ class FusedCifarEngine:
         self.fc1_split = fc1_split or self._pick_fc1_split(B)
         # both weight gradients run in ONE launch (ops.wgrad: no stream fork/join in the graph);
         # DMLC_SPLIT_WGRAD=1 runs them as two kernels on forked streams instead (A/B comparisons)
-        import os
         self.merged_wgrad = os.environ.get("DMLC_SPLIT_WGRAD", "0") != "1"
         # conv1 and conv2 forward in one launch (bf16 path; DMLC_SPLIT_FWD=1: two launches)
         self.fused_fwd = os.environ.get("DMLC_SPLIT_FWD", "0") != "1"
