@@ -42,6 +42,40 @@ DEV void stage_conv1_input(bf16* xin, const uint8_t* src, int cy, int cx, int ti
   }
 }
 
+// conv1 implicit GEMM of one wave: co tiles 2cp, 2cp+1 (weights wa in registers) x pixel tiles
+// 9pq .. 9pq+8.  Software-pipelined: the 5 B fragments of pixel tile t+1 are read from LDS while tile
+// t's 10 MFMAs run (wait_lds retires tile t's reads first; see common.h).
+DEV void conv1_mfma(const bf16* xin, const bf16x8 (&wa)[2][5], f32x4 (&acc)[2][9], int pq, int g, int li) {
+  auto load_tile = [&](int t, bf16x8 (&bx)[5]) {
+    const int px = (pq * 9 + t) * 16 + li;
+    const int y = px / 24, x = px - (px / 24) * 24;
+    const bf16* base = xin + (y * 32 + x + 2 * g) * 4;   // k = 8g..8g+7 -> kw = 2g,2g+1 ; ci 0..3
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh) {
+      const bf16* p = base + kh * 128;
+      bx[kh] = cat44(*reinterpret_cast<const bf16x4*>(p), *reinterpret_cast<const bf16x4*>(p + 4));
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < 9; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
+  bf16x8 BX[2][5];
+  load_tile(0, BX[0]);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int cur = t & 1;
+    wait_lds();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < 9) load_tile(t + 1, BX[cur ^ 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh) {
+      acc[0][t] = mfma16(wa[0][kh], BX[cur][kh], acc[0][t]);
+      acc[1][t] = mfma16(wa[1][kh], BX[cur][kh], acc[1][t]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -71,21 +105,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 1);
 
   f32x4 acc[2][9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int px = (pq * 9 + t) * 16 + li;
-    const int y = px / 24, x = px - (px / 24) * 24;
-    const bf16* base = xin + (y * 32 + x + 2 * g) * 4;   // k = 8g..8g+7 -> kw = 2g,2g+1 ; ci 0..3
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh) {
-      const bf16* p = base + kh * 128;
-      const bf16x8 bx = cat44(*reinterpret_cast<const bf16x4*>(p), *reinterpret_cast<const bf16x4*>(p + 4));
-      acc[0][t] = mfma16(wa[0][kh], bx, acc[0][t]);
-      acc[1][t] = mfma16(wa[1][kh], bx, acc[1][t]);
-    }
-  }
+  conv1_mfma(xin, wa, acc, pq, g, li);
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -142,36 +162,62 @@ template <int NPX>
 DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][NPX], int pg, int cp,
                     int g, int li, int tid) {
   const int w = tid >> 6, lane = tid & 63, sw = li & 7;
-  int pb[NPX];
+  // Per-lane LDS element offsets, computed once: every fragment read of the loop is then one
+  // ds_read_b128 at (offset register + compile-time immediate), no per-chunk address VALU (the swizzle
+  // arithmetic had made this loop VALU-issue-bound: ~3 integer ops per MFMA).
+  //  * B (input image, swzpad layout): tile t's pixel for tap (kh, kw) is pb[t] + 16 kh + kw and its
+  //    XOR key is (key0 + kw + 4 kh) & 7 (no carry out of the 16-wide row: x + kw <= 15), so the
+  //    lane's offset is xo[t][d][s] + (16 kh + kw) * 64 with d = (kw + 4 kh) & 7;
+  //  * A (weight slice, chunk c ^ (row & 7)): kw * 64 + ao[s].
+  int xo[NPX][8][2];
 #pragma unroll
   for (int t = 0; t < NPX; ++t) {
     const int px = 16 * (pg + 4 * t) + li;
-    const int y = px / 12;
-    pb[t] = y * 16 + (px - y * 12);
+    const int y = px / 12, x = px - y * 12;
+    const int pb = y * 16 + x, key0 = (x + 4 * y) & 7;
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) xo[t][d][s] = pb * 64 + (((4 * s + g) ^ ((key0 + d) & 7)) << 3);
   }
+  int ao[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) ao[s] = (32 * cp + li) * 320 + (((4 * s + g) ^ sw) << 3);
 #pragma unroll
   for (int t = 0; t < NPX; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
   ws_dma(Wg, 0, ws, w, lane);
   __syncthreads();                                       // (waits vmcnt(0): the DMA has landed)
+  // One k-chunk (kw, s) = 2 A + NPX B fragments.  The fragments of chunk j+1 are read into the other
+  // register set BEFORE chunk j's MFMAs issue, so the LDS latency of a chunk hides behind the previous
+  // chunk's MFMAs (lgkmcnt waits for the older reads only) instead of one exposed latency per chunk.
+  auto load_chunk = [&](int kh, int j, bf16x8& a0, bf16x8& a1, bf16x8 (&bx)[NPX]) {
+    const int kw = j >> 1, s = j & 1;
+    const bf16* wr = ws + (kh & 1) * WS_ELEMS + kw * 64 + ao[s];
+    a0 = lds_b128(wr);
+    a1 = lds_b128(wr + 16 * 320);
+#pragma unroll
+    for (int t = 0; t < NPX; ++t) bx[t] = lds_b128(xin + xo[t][(kw + 4 * kh) & 7][s] + (kh * 16 + kw) * 64);
+  };
 #pragma unroll
   for (int kh = 0; kh < 5; ++kh) {
     if (kh < 4) ws_dma(Wg, kh + 1, ws + ((kh + 1) & 1) * WS_ELEMS, w, lane);   // buffer freed by the last barrier
-    const bf16* wr0 = ws + (kh & 1) * WS_ELEMS + (32 * cp + li) * 320;
-    const bf16* wr1 = wr0 + 16 * 320;
+    bf16x8 A0[2], A1[2], BX[2][NPX];
+    load_chunk(kh, 0, A0[0], A1[0], BX[0]);
 #pragma unroll
-    for (int kw = 0; kw < 5; ++kw) {
+    for (int j = 0; j < 10; ++j) {
+      const int cur = j & 1;
+      // chunk j's reads (issued one chunk ago) complete; then chunk j+1's reads go out ahead of chunk
+      // j's MFMAs (sched barriers keep the scheduler from sinking them back next to their use)
+      wait_lds();
+      __builtin_amdgcn_sched_barrier(0);
+      if (j + 1 < 10) load_chunk(kh, j + 1, A0[cur ^ 1], A1[cur ^ 1], BX[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int c = ((kw * 8 + s * 4 + g) ^ sw) * 8;
-        const bf16x8 a0 = lds_b128(wr0 + c);
-        const bf16x8 a1 = lds_b128(wr1 + c);
-#pragma unroll
-        for (int t = 0; t < NPX; ++t) {
-          const bf16x8 bx = lds_b128(xin + swzpad(pb[t] + kh * 16 + kw, 4 * s + g));
-          acc[0][t] = mfma16(a0, bx, acc[0][t]);
-          acc[1][t] = mfma16(a1, bx, acc[1][t]);
-        }
+      for (int t = 0; t < NPX; ++t) {
+        acc[0][t] = mfma16(A0[cur], BX[cur][t], acc[0][t]);
+        acc[1][t] = mfma16(A1[cur], BX[cur][t], acc[1][t]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (kh < 4) __syncthreads();                         // next slice landed; this one fully read
   }
@@ -330,21 +376,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
 
   {
     f32x4 acc[2][9];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int px = (pq * 9 + t) * 16 + li;
-      const int y = px / 24, x = px - (px / 24) * 24;
-      const bf16* base = xin + (y * 32 + x + 2 * g) * 4;
-#pragma unroll
-      for (int kh = 0; kh < 5; ++kh) {
-        const bf16* p = base + kh * 128;
-        const bf16x8 bx = cat44(*reinterpret_cast<const bf16x4*>(p), *reinterpret_cast<const bf16x4*>(p + 4));
-        acc[0][t] = mfma16(wa[0][kh], bx, acc[0][t]);
-        acc[1][t] = mfma16(wa[1][kh], bx, acc[1][t]);
-      }
-    }
+    conv1_mfma(xin, wa, acc, pq, g, li);
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll

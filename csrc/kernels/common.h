@@ -41,6 +41,12 @@ DEV bf16x8 tr_frag(const bf16* p0, const bf16* p1) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
+// s_waitcnt lgkmcnt(0) as a real instruction the waitcnt pass accounts for (vmcnt / expcnt left at
+// their maxima).  Software-pipelined loops use it to retire the PREVIOUS chunk's LDS reads before
+// issuing the next chunk's: the compiler would otherwise wait lgkmcnt(0) right before an MFMA, i.e.
+// also for the reads just issued for the next chunk, exposing one LDS latency per chunk.
+DEV void wait_lds() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
 DEV bf16x8 lds_b128(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 DEV bf16x8 glb_b128(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 

@@ -20,6 +20,7 @@ for s in $STEPS; do
     b400) timeout -k 10 200 python bench.py --steps 400 --warmup 20 > gpurun_out/bench400.log 2>&1; ok $? b400 ;;
     b1024) timeout -k 10 200 python bench.py --steps 200 --warmup 20 --batch 1024 > gpurun_out/bench1024.log 2>&1; ok $? b1024 ;;
     lat) timeout -k 10 200 python tools/launch_latency.py > gpurun_out/launch_latency.json 2> gpurun_out/launch_latency.err; ok $? lat ;;
+    cnn) timeout -k 10 400 python -u -m pytest tests/test_cnn_kernels_gpu.py tests/test_fused_gpu.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_cnn.log 2>&1; ok $? cnn ;;
     kbench) timeout -k 10 200 python tools/kbench.py > gpurun_out/kbench.json 2> gpurun_out/kbench.err; ok $? kbench ;;
     ktiming) DMLC_TIMING=1 timeout -k 10 200 python tools/ktiming.py > gpurun_out/ktiming.json 2> gpurun_out/ktiming.err; ok $? ktiming ;;
     rn) timeout -k 10 300 python bench.py --model resnet20 --steps 100 --warmup 10 > gpurun_out/bench_rn.log 2>&1; ok $? rn ;;
