@@ -61,7 +61,7 @@ inline DmlcIndexSrc index_src(const Tensor& idx, const c10::optional<Tensor>& co
                 "order: half_bits must be the smallest h with 4^h >= n");
     TORCH_CHECK(world >= 1 && rank >= 0 && rank < world, "order: bad rank/world");
     TORCH_CHECK(bvalid >= 1 && bvalid <= B, "order: bvalid must be in [1, B]");
-    TORCH_CHECK(period * world * bvalid <= n, "order: an epoch of period steps must fit in the dataset");
+    TORCH_CHECK(period == n / (world * bvalid), "order: period must be n / (world * bvalid) steps per epoch");
     TORCH_CHECK(seed >= 0 && seed <= 0xffffffffll, "order: seed must be a uint32");
     s.idx_base = nullptr;
     s.n = (int)n; s.half_bits = (int)hb; s.world = (int)world; s.rank = (int)rank; s.bvalid = (int)bvalid;

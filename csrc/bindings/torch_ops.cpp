@@ -16,10 +16,17 @@ namespace {
 
 using namespace dmlc_bind;
 
+// optional [B, 3072] uint8 raw-image copy (forward writes it, the conv1 weight gradient reads it)
+uint8_t* xraw_ptr(const c10::optional<Tensor>& xraw, int64_t B) {
+  if (!xraw.has_value()) return nullptr;
+  check(*xraw, "xraw", at::kByte, {B, 3072});
+  return xraw->data_ptr<uint8_t>();
+}
+
 
 void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
                int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& out, const Tensor& am,
-               const c10::optional<Tensor>& amax) {
+               const c10::optional<Tensor>& amax, const c10::optional<Tensor>& xraw) {
   const int64_t B = out.size(0);
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
@@ -36,6 +43,7 @@ void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   a.w = w1f.data_ptr(); a.bias = b1.data_ptr<float>();
   a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>();
   a.amax = nullptr;
+  a.xraw = xraw_ptr(xraw, B);
   if (amax.has_value()) {
     check_numel(*amax, "amax", at::kFloat, 2);
     a.amax = amax->data_ptr<float>();
@@ -75,7 +83,8 @@ void fp8_roundtrip(const Tensor& x, const Tensor& y, double scale) {
 
 void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
                 int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& p1, const Tensor& am1,
-                const Tensor& w2f, const Tensor& b2, const Tensor& p2, const Tensor& am2) {
+                const Tensor& w2f, const Tensor& b2, const Tensor& p2, const Tensor& am2,
+                const c10::optional<Tensor>& xraw) {
   const int64_t B = p1.size(0);
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
@@ -94,6 +103,7 @@ void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tenso
   a1.B = (int)B; a1.cy = (int)cy; a1.cx = (int)cx;
   a1.w = w1f.data_ptr(); a1.bias = b1.data_ptr<float>(); a1.out = p1.data_ptr(); a1.am = am1.data_ptr<uint8_t>();
   a1.amax = nullptr;
+  a1.xraw = xraw_ptr(xraw, B);
   DmlcConv2FwdArgs a2;
   a2.in = p1.data_ptr(); a2.w = w2f.data_ptr(); a2.bias = b2.data_ptr<float>();
   a2.out = p2.data_ptr(); a2.am = am2.data_ptr<uint8_t>(); a2.B = (int)B;
@@ -130,7 +140,7 @@ void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const 
 
 void conv1_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
                  int64_t cy, int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1,
-                 const Tensor& partb1) {
+                 const Tensor& partb1, const c10::optional<Tensor>& xraw) {
   const int64_t B = dp1.size(0), g1 = part1.size(0);
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
@@ -146,6 +156,7 @@ void conv1_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tens
   a.cy = (int)cy; a.cx = (int)cx;
   a.dp1 = dp1.data_ptr(); a.am1 = am1.data_ptr<uint8_t>();
   a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1; a.B = (int)B;
+  a.xraw = xraw_ptr(xraw, B);
   CHECK_HIP(dmlc_conv1_wgrad(&a, stream_of(dp1)));
 }
 
@@ -165,7 +176,8 @@ void conv2_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const
 
 void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
            int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
-           const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2) {
+           const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2,
+           const c10::optional<Tensor>& xraw) {
   const int64_t B = dp1.size(0), g1 = part1.size(0), g2 = groups2, slabs2 = (groups2 + 1) / 2;
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
@@ -186,6 +198,7 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
   a.w1.cy = (int)cy; a.w1.cx = (int)cx;
   a.w1.dp1 = dp1.data_ptr(); a.w1.am1 = am1.data_ptr<uint8_t>();
   a.w1.part1 = part1.data_ptr<float>(); a.w1.partb1 = partb1.data_ptr<float>(); a.w1.g1 = (int)g1; a.w1.B = (int)B;
+  a.w1.xraw = xraw_ptr(xraw, B);
   a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr<float>();
   a.w2.partb2 = partb2.data_ptr<float>(); a.w2.g2 = (int)g2; a.w2.B = (int)B;
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
@@ -299,7 +312,8 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
          const Tensor& fc3t, const Tensor& fc3d, const Tensor& step, double lr0, double decay, double decay_steps,
          bool staircase, const Tensor& ticket, const Tensor& loss_part, const Tensor& correct_part,
          const Tensor& stats, const c10::optional<Tensor>& w2f8, const c10::optional<Tensor>& amax_w,
-         const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize, int64_t batch) {
+         const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize, int64_t batch,
+         const c10::optional<Tensor>& bidx, const c10::optional<Tensor>& order) {
   TORCH_CHECK(roles >= 0 && roles <= 2, "sgd roles must be 0..2");
   TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
   TORCH_CHECK(off.size() == 10, "off must have 10 entries");
@@ -358,6 +372,21 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
     check_numel(*scale_w, "scale_w", at::kFloat, 2);
     a.w2f8 = w2f8->data_ptr<uint8_t>(); a.amax_w = amax_w->data_ptr<float>(); a.scale_w = scale_w->data_ptr<float>();
   }
+  a.bidx = nullptr; a.bidx_n = 0;
+  memset(&a.next, 0, sizeof(a.next));
+  if (bidx.has_value()) {
+    TORCH_CHECK(order.has_value(), "sgd: bidx needs the order descriptor");
+    dev(*bidx, "bidx");
+    TORCH_CHECK(bidx->scalar_type() == at::kInt && bidx->dim() == 1 && bidx->numel() >= 1 &&
+                    bidx->numel() <= 4096, "bidx must be int32 [Bpad <= 4096]");
+    TORCH_CHECK(!order->is_cuda() && order->scalar_type() == at::kLong && order->numel() == 6,
+                "sgd: order must be the host int64 [6] descriptor");
+    const int64_t* d = order->data_ptr<int64_t>();
+    TORCH_CHECK(d[2] >= 1 && d[4] >= 1, "sgd: bad order descriptor");
+    a.next = index_src(*order, step, d[0] / (d[2] * d[4]), bidx->numel());   // validates it
+    TORCH_CHECK(a.next.idx_base == nullptr, "sgd: order must be the host descriptor");
+    a.bidx = bidx->data_ptr<int>(); a.bidx_n = (int)bidx->numel();
+  }
   CHECK_HIP(dmlc_sgd(&a, stream_of(master)));
 }
 
@@ -365,20 +394,21 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
 
 TORCH_LIBRARY(dmlc, m) {
   m.def("conv1_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
-        "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? amax=None) -> ()");
+        "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? amax=None, Tensor(d!)? xraw=None) -> ()");
   m.def("conv2_fwd_fp8(Tensor inp, Tensor w8, Tensor b2, Tensor amax_x, Tensor scale_w, Tensor? counter, "
         "Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("fp8_roundtrip(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("conv2_fwd(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("conv12_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
-        "Tensor(a!) p1, Tensor(b!) am1, Tensor w2f, Tensor b2, Tensor(c!) p2, Tensor(d!) am2) -> ()");
+        "Tensor(a!) p1, Tensor(b!) am1, Tensor w2f, Tensor b2, Tensor(c!) p2, Tensor(d!) am2, "
+        "Tensor(e!)? xraw=None) -> ()");
   m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv1_wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
-        "Tensor(a!) part1, Tensor(b!) partb1) -> ()");
+        "Tensor(a!) part1, Tensor(b!) partb1, Tensor? xraw=None) -> ()");
   m.def("conv2_wgrad(Tensor p1, Tensor dy2, Tensor(a!) part2, Tensor(b!) partb2) -> ()");
   m.def("wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor(a!) part1, Tensor(b!) partb1, Tensor p1, Tensor dy2, Tensor(c!) part2, Tensor(d!) partb2, "
-        "int groups2) -> ()");
+        "int groups2, Tensor? xraw=None) -> ()");
   m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params) -> ()");
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
@@ -389,7 +419,7 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
-        "bool finalize, int batch) -> ()");
+        "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

@@ -42,6 +42,7 @@ struct DmlcConv1FwdArgs {
   uint8_t* am;              // [B][12][12][64] argmax (0..8) in the pool window, 255 = no gradient
   float* amax;              // nullable: fp8 path, float[2] running max of the pooled output, slot
                             //   (step & 1) accumulated (atomic max), slot (step+1) & 1 zeroed
+  uint8_t* xraw;            // nullable: copy of each row's raw uint8 image [B][3072] for the wgrad
 };
 
 // conv2 5x5 (64->64) + bias + ReLU + maxpool 3x3/2 TF-SAME.  One workgroup per image.
@@ -83,6 +84,7 @@ struct DmlcConv2DgradArgs {
 struct DmlcConv1WgradArgs {
   const uint8_t* data;      // [N][32][32][3]
   DmlcIndexSrc src;
+  const uint8_t* xraw;      // nullable: the forward's copy [B][3072] (row b) instead of data[src(b)]
   int cy, cx;
   const void* dp1;          // bf16 [B][12][12][64]  grad wrt pool1 output
   const uint8_t* am1;       // [B][12][12][64]
@@ -177,6 +179,12 @@ struct DmlcSgdArgs {
   // publish stats (their last arriver).
   int roles;
   int finalize;
+  // next step's batch rows (nullable): the finalizing launch writes bidx[b] = the generated-order row
+  // of batch row b at step+1 (next = the generated-order descriptor; its counter is unused), so the
+  // data-consuming kernels of every step read ONE index per row (explicit list, period 1) instead of
+  // evaluating the Feistel order themselves (~150 scalar instructions per row per wave).
+  int* bidx; int bidx_n;
+  DmlcIndexSrc next;
 };
 
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);

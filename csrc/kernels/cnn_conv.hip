@@ -31,12 +31,23 @@ namespace dmlc {
 constexpr int C1_XIN = 28 * 32 * 4;        // 3584 bf16
 constexpr int C1_OUT = 576 * 64;           // 36864 bf16
 
-DEV void stage_conv1_input(bf16* xin, const uint8_t* src, int cy, int cx, int tid) {
+// The whole 3 KB uint8 image in ONE 16-byte load per thread (threads 0..191) into LDS (`raw`), and
+// optionally out to xraw (the weight-gradient kernel then reads it without the index -> dataset
+// chain); then expanded from LDS.  Call stage_conv1_raw, barrier, stage_conv1_input.
+DEV void stage_conv1_raw(uint8_t* raw, const uint8_t* src, uint8_t* xraw, int tid) {
+  if (tid < 192) {
+    const uint4 v = reinterpret_cast<const uint4*>(src)[tid];
+    reinterpret_cast<uint4*>(raw)[tid] = v;
+    if (xraw) reinterpret_cast<uint4*>(xraw)[tid] = v;
+  }
+}
+
+DEV void stage_conv1_input(bf16* xin, const uint8_t* raw, int cy, int cx, int tid) {
   for (int p = tid; p < 28 * 32; p += NT) {
     const int r = p >> 5, c = p & 31;
     const int iy = r - 2, ix = c - 2;
     const bool ok = iy >= 0 && iy < 24 && ix >= 0 && ix < 24;
-    const uint8_t* s = src + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);     // branch-free loads
+    const uint8_t* s = raw + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);
     const float c0 = s[0], c1 = s[1], c2 = s[2];
     *reinterpret_cast<bf16x4*>(xin + p * 4) = ok ? pack4(c0, c1, c2, 0.f) : pack4(0.f, 0.f, 0.f, 0.f);
   }
@@ -86,7 +97,10 @@ __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 
   const int img = batch_index(a.src, a.B, b);
-  stage_conv1_input(xin, a.data + (size_t)img * 3072, a.cy, a.cx, tid);
+  uint8_t* raw = reinterpret_cast<uint8_t*>(cout);          // the conv output region is free until the epilogue
+  stage_conv1_raw(raw, a.data + (size_t)img * 3072, a.xraw ? a.xraw + (size_t)b * 3072 : nullptr, tid);
+  __syncthreads();
+  stage_conv1_input(xin, raw, a.cy, a.cx, tid);
 
   // A operand: weights [64 co][160 k]; this wave owns co tiles 2cp, 2cp+1 (32 channels) and the
   // pixel tiles 9pq .. 9pq+8 (of 36): every B fragment read from LDS feeds two MFMAs.
@@ -354,7 +368,10 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 
   const int img = batch_index(a1.src, a1.B, b);
-  stage_conv1_input(xin, a1.data + (size_t)img * 3072, a1.cy, a1.cx, tid);
+  uint8_t* raw = reinterpret_cast<uint8_t*>(cout);          // the conv1 output region is free until its epilogue
+  stage_conv1_raw(raw, a1.data + (size_t)img * 3072, a1.xraw ? a1.xraw + (size_t)b * 3072 : nullptr, tid);
+  __syncthreads();
+  stage_conv1_input(xin, raw, a1.cy, a1.cx, tid);
   // conv2's padded input: zero halo (rows/cols 0,1,14,15); the interior comes from pool1
   for (int s = tid; s < 2048; s += NT) {
     const int pix = s >> 3, c = s & 7, r = pix >> 4, col = pix & 15;

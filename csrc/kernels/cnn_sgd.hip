@@ -258,6 +258,11 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
   DMLC_STAMP(DMLC_TK_SGD, 1);
 
   if (!(a.mode == 0 || a.mode == 2) || !a.finalize) return;
+  // the next step's batch rows (no kernel of this step reads bidx any more: they all ran before)
+  if (a.bidx && (int)blockIdx.x * 256 < a.bidx_n) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r < a.bidx_n) a.bidx[r] = order_row(a.next, step + 1, r);
+  }
   // last arriver: bump global_step, publish stats, re-arm the ticket for the next launch (the engine
   // zeroes it once at creation; every launch that starts also completes, so it stays consistent).
   // Nothing is published THROUGH the ticket (loss/accuracy partials come from an earlier launch and

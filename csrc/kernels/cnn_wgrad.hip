@@ -63,15 +63,17 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
   const int cI = tid % 192, cD2 = 1024 + (tid & 127), cA1 = 512 + (tid & 63);
   uint4 vI, vD0, vD1, vD2, vA0, vA1;
   auto load = [&](int idx, int bb) {
-    const uint4* si = reinterpret_cast<const uint4*>(a.data + (size_t)idx * 3072);
+    const uint4* si = reinterpret_cast<const uint4*>(a.xraw ? a.xraw + (size_t)bb * 3072 : a.data + (size_t)idx * 3072);
     const uint4* sd = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.dp1) + (size_t)bb * 9216);
     const uint4* sa = reinterpret_cast<const uint4*>(a.am1 + (size_t)bb * 9216);
     vI = si[cI];
     vD0 = sd[tid]; vD1 = sd[tid + 512]; vD2 = sd[cD2];
     vA0 = sa[tid]; vA1 = sa[cA1];
   };
-  load(batch_index(a.src, a.B, b0 < last ? b0 : last), b0);
-  int nidx = batch_index(a.src, a.B, b0 + 1 < last ? b0 + 1 : last);
+  // with the forward's image copy (xraw) no dataset index is needed at all
+  auto row_index = [&](int bb) { return a.xraw ? 0 : batch_index(a.src, a.B, bb); };
+  load(row_index(b0 < last ? b0 : last), b0);
+  int nidx = row_index(b0 + 1 < last ? b0 + 1 : last);
   for (int b = b0; b < b1; ++b) {
     __syncthreads();                           // previous image's MFMA reads are done
     reinterpret_cast<uint4*>(img)[cI] = vI;
@@ -81,7 +83,7 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
     reinterpret_cast<uint4*>(ams)[tid] = vA0;
     reinterpret_cast<uint4*>(ams)[cA1] = vA1;
     load(nidx, b + 1 < last ? b + 1 : last);   // prefetch the next image while this one computes
-    nidx = batch_index(a.src, a.B, b + 2 < last ? b + 2 : last);
+    nidx = row_index(b + 2 < last ? b + 2 : last);
     __syncthreads();
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 1);
     // (a) shifted channel planes straight from the uint8 image: task (yy, x8, kw) -> planes

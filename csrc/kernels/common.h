@@ -134,6 +134,16 @@ DEV uint32_t order_perm(uint32_t pos, uint32_t n, int half_bits, uint32_t seed, 
   return x;
 }
 
+// Generated-order dataset row of batch row b at global step `step` (api.h DmlcIndexSrc).
+template <class Src>
+DEV int order_row(const Src& s, int64_t step, int b) {
+  const uint32_t epoch = (uint32_t)(step / s.period);
+  const int64_t j = step - (int64_t)epoch * s.period;
+  const int bb = b < s.bvalid ? b : s.bvalid - 1;
+  const uint32_t pos = (uint32_t)((j * s.world + s.rank) * s.bvalid + bb);
+  return (int)order_perm(pos, (uint32_t)s.n, s.half_bits, s.seed, epoch);
+}
+
 // Sample index of batch row b (api.h DmlcIndexSrc: explicit list or generated epoch order).
 template <class Src>
 DEV int batch_index(const Src& s, int B, int b) {
@@ -142,12 +152,7 @@ DEV int batch_index(const Src& s, int B, int b) {
     if (s.counter) row = (int)(*s.counter % (int64_t)s.period);
     return s.idx_base[row * B + b];
   }
-  const int64_t step = *s.counter;
-  const uint32_t epoch = (uint32_t)(step / s.period);
-  const int64_t j = step - (int64_t)epoch * s.period;
-  const int bb = b < s.bvalid ? b : s.bvalid - 1;
-  const uint32_t pos = (uint32_t)((j * s.world + s.rank) * s.bvalid + bb);
-  return (int)order_perm(pos, (uint32_t)s.n, s.half_bits, s.seed, epoch);
+  return order_row(s, *s.counter, b);
 }
 
 // 16-byte chunk swizzle for [pixel][64 x bf16] LDS images (128-B rows): chunk c of pixel p is

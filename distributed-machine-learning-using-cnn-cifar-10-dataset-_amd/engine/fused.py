@@ -102,7 +102,13 @@ class FusedCifarEngine:
         self.n_data = self.data.shape[0]
         self.order = OrderSpec(self.n_data, Bv, world_size, rank, seed)
         self.period = self.order.period          # steps per epoch
-        self.order_desc = self.order.descriptor()   # host int64 [6]: the kernels' index source
+        self.order_desc = self.order.descriptor()   # host int64 [6]: the generated order
+        # this step's batch rows (int32 [B], rows >= Bv repeat the last): written for step s+1 by the
+        # finalizing SGD launch of step s (cnn_sgd.hip), so each data kernel reads one index per row;
+        # set from the host whenever the step counter is set from the host
+        self.bidx = torch.zeros(B, dtype=torch.int32, device=dev)
+        # raw uint8 images of the step's rows, written by the forward for the conv1 weight gradient
+        self.xraw = torch.zeros(B, 3072, dtype=torch.uint8, device=dev)
 
         # --- parameters + shadows -------------------------------------------------------------
         if flat_params is None:
@@ -217,6 +223,7 @@ class FusedCifarEngine:
                                   captured_comm=bool(self.capture_comm or self.xgmi is not None))
         self.side_stream = torch.cuda.Stream(device=dev)
         self.host_step = 0
+        self._sync_bidx()
         self.refresh_shadows()
 
     # ------------------------------------------------------------------------------------------
@@ -237,6 +244,10 @@ class FusedCifarEngine:
     def set_step(self, step: int):
         self.step_t.fill_(int(step))
         self.host_step = int(step)
+        self._sync_bidx()
+
+    def _sync_bidx(self):
+        self.bidx.copy_(self._padded(self.batch_indices(self.host_step)))
 
     # --- data order ---------------------------------------------------------------------------
     def epoch_permutation(self, epoch: int) -> torch.Tensor:
@@ -261,10 +272,10 @@ class FusedCifarEngine:
         o, p = self.ops, self.pv
         if self.fused_fwd and not self.fp8:        # conv1 + pool1 + conv2 + pool2 in one launch
             o.conv12_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
-                         self.am1, self.w2f, p["conv2_bias"], self.p2, self.am2)
+                         self.am1, self.w2f, p["conv2_bias"], self.p2, self.am2, self.xraw if train else None)
         else:
             o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
-                        self.am1, self.amax_x if self.fp8 else None)
+                        self.am1, self.amax_x if self.fp8 else None, self.xraw if train else None)
         if self.fp8:
             o.conv2_fwd_fp8(self.p1, self.w2f8, p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
         elif not self.fused_fwd:
@@ -282,11 +293,11 @@ class FusedCifarEngine:
 
     def _conv_backward(self, src=None):
         o = self.ops
-        idx, counter, period = src or (self.order_desc, self.step_t, self.period)
+        idx, counter, period = src or (self.bidx, None, 1)
         o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         if self.merged_wgrad:
             o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
-                    self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2)
+                    self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw)
             return
         # the two weight-gradient kernels are independent: fork them onto two streams (two parallel
         # branches of the captured graph) so they share the chip
@@ -295,7 +306,7 @@ class FusedCifarEngine:
         with torch.cuda.stream(self.side_stream):
             o.conv2_wgrad(self.p1, self.dy2, self.part2, self.partb2)
         o.conv1_wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
-                      self.part1, self.partb1)
+                      self.part1, self.partb1, self.xraw)
         main.wait_stream(self.side_stream)
 
     def _sgd(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True):
@@ -304,7 +315,7 @@ class FusedCifarEngine:
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                      self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
                                                                       if self.fp8 else (None, None, None)),
-                     roles, finalize, self.Bv)
+                     roles, finalize, self.Bv, self.bidx, self.order_desc)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -340,7 +351,7 @@ class FusedCifarEngine:
 
     # segments of one step: each is a capturable list of launches on the current stream
     def _seg_compute_a(self):
-        self._forward(self.order_desc, self.step_t, self.period, train=True)
+        self._forward(self.bidx, None, 1, train=True)
         self._fc_backward()
 
     def _seg_compute_b(self):

@@ -48,28 +48,28 @@ def main():
     torch.cuda.synchronize()
     o, p = eng.ops, eng.pv
     res = {}
-    res["conv1_fwd"] = timeit(lambda: o.conv1_fwd(eng.data, eng.order_desc, eng.step_t, eng.period, eng.cy, eng.cx, eng.w1f,
-                                                  p["conv1_bias"], eng.p1, eng.am1), a.iters)
+    res["conv1_fwd"] = timeit(lambda: o.conv1_fwd(eng.data, eng.bidx, None, 1, eng.cy, eng.cx, eng.w1f,
+                                                  p["conv1_bias"], eng.p1, eng.am1, None, eng.xraw), a.iters)
     res["conv2_fwd"] = timeit(lambda: o.conv2_fwd(eng.p1, eng.w2f, p["conv2_bias"], eng.p2, eng.am2), a.iters)
-    res["conv12_fwd"] = timeit(lambda: o.conv12_fwd(eng.data, eng.order_desc, eng.step_t, eng.period, eng.cy, eng.cx,
+    res["conv12_fwd"] = timeit(lambda: o.conv12_fwd(eng.data, eng.bidx, None, 1, eng.cy, eng.cx,
                                                     eng.w1f, p["conv1_bias"], eng.p1, eng.am1, eng.w2f,
-                                                    p["conv2_bias"], eng.p2, eng.am2), a.iters)
+                                                    p["conv2_bias"], eng.p2, eng.am2, eng.xraw), a.iters)
     f = eng._fc1_fwd
     res["fc1_fwd_gemm"] = timeit(lambda: o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"]), a.iters)
     B = eng.B
     res["head"] = timeit(lambda: o.head(eng.h1part, p["full_bias_1"], eng.fc2t, p["full_bias_2"], eng.fc3t,
-                                        p["full_bias_3"], eng.fc3d, eng.fc2n, eng.labels, eng.order_desc, eng.step_t,
-                                        eng.period, 1.0 / B, True, True, eng.h1, eng.h2, eng.dl, eng.dh1, eng.dh2,
+                                        p["full_bias_3"], eng.fc3d, eng.fc2n, eng.labels, eng.bidx, None,
+                                        1, 1.0 / B, True, True, eng.h1, eng.h2, eng.dl, eng.dh1, eng.dh2,
                                         eng.loss_part, eng.correct_part, None), a.iters)
     res["fc_bwd_gemm"] = timeit(eng._fc_backward, a.iters)
     res["conv2_dgrad"] = timeit(lambda: o.conv2_dgrad(eng.dp2, eng.am2, eng.w2d, eng.dp1, eng.dy2), a.iters)
-    res["conv1_wgrad"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.order_desc, eng.step_t, eng.period, eng.cy, eng.cx,
-                                                      eng.dp1, eng.am1, eng.part1, eng.partb1), a.iters)
+    res["conv1_wgrad"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx,
+                                                      eng.dp1, eng.am1, eng.part1, eng.partb1, eng.xraw), a.iters)
     if not eng.merged_wgrad:
         res["conv2_wgrad"] = timeit(lambda: o.conv2_wgrad(eng.p1, eng.dy2, eng.part2, eng.partb2), a.iters)
-    res["wgrad_merged"] = timeit(lambda: o.wgrad(eng.data, eng.order_desc, eng.step_t, eng.period, eng.cy, eng.cx,
+    res["wgrad_merged"] = timeit(lambda: o.wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx,
                                                  eng.dp1, eng.am1, eng.part1, eng.partb1, eng.p1, eng.dy2,
-                                                 eng.part2, eng.partb2, eng.groups2), a.iters)
+                                                 eng.part2, eng.partb2, eng.groups2, eng.xraw), a.iters)
     res["conv_bwd"] = timeit(eng._conv_backward, a.iters)
     res["sgd_reduce_only"] = timeit(lambda: eng._sgd(mode=1), a.iters)
     res["sgd_full"] = timeit(lambda: eng._sgd(mode=0), a.iters)
