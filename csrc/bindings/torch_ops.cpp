@@ -138,6 +138,36 @@ void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const 
   CHECK_HIP(dmlc_conv2_dgrad(&a, stream_of(dp2)));
 }
 
+void conv2_dgrad_w1(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const c10::optional<Tensor>& dp1,
+                    const Tensor& dy2, const Tensor& am1, const Tensor& xraw, int64_t cy, int64_t cx,
+                    const Tensor& part1, const Tensor& partb1) {
+  const int64_t B = dp2.size(0);
+  check(dp2, "dp2", at::kBFloat16, {B, 6, 6, 64});
+  check(am2, "am2", at::kByte, {B, 6, 6, 64});
+  check(w2d, "w2d", at::kBFloat16, {64, 1600});
+  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
+  check(am1, "am1", at::kByte, {B, 12, 12, 64});
+  TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
+  check(part1, "part1", at::kFloat, {B, 80, 64});
+  check(partb1, "partb1", at::kFloat, {B, 64});
+  c10::DeviceGuard guard(dp2.device());
+  DmlcConv2DgradArgs a;
+  a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
+  a.dp1 = nullptr;
+  if (dp1.has_value()) {
+    check(*dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+    a.dp1 = dp1->data_ptr();
+  }
+  a.dy2 = dy2.data_ptr(); a.B = (int)B;
+  DmlcConv1WgradArgs w;
+  memset(&w, 0, sizeof(w));
+  w.xraw = xraw_ptr(xraw, B);
+  w.cy = (int)cy; w.cx = (int)cx;
+  w.am1 = am1.data_ptr<uint8_t>(); w.part1 = part1.data_ptr<float>(); w.partb1 = partb1.data_ptr<float>();
+  w.g1 = (int)B; w.B = (int)B;
+  CHECK_HIP(dmlc_conv2_dgrad_w1(&a, &w, stream_of(dp2)));
+}
+
 void conv1_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
                  int64_t cy, int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1,
                  const Tensor& partb1, const c10::optional<Tensor>& xraw) {
@@ -177,16 +207,18 @@ void conv2_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const
 void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
            int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
            const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2,
-           const c10::optional<Tensor>& xraw) {
-  const int64_t B = dp1.size(0), g1 = part1.size(0), g2 = groups2, slabs2 = (groups2 + 1) / 2;
+           const c10::optional<Tensor>& xraw, bool with_conv1) {
+  const int64_t B = p1.size(0), g1 = with_conv1 ? part1.size(0) : 0, g2 = groups2, slabs2 = (groups2 + 1) / 2;
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
-  TORCH_CHECK(g1 >= 1 && g1 <= B && g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
+  TORCH_CHECK((!with_conv1 || (g1 >= 1 && g1 <= B)) && g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
   TORCH_CHECK(part2.size(0) == slabs2, "wgrad: conv2 slabs must be ceil(groups2 / 2)");
-  check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
-  check(am1, "am1", at::kByte, {B, 12, 12, 64});
-  check(part1, "part1", at::kFloat, {g1, 80, 64});
-  check(partb1, "partb1", at::kFloat, {g1, 64});
+  if (with_conv1) {
+    check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+    check(am1, "am1", at::kByte, {B, 12, 12, 64});
+    check(part1, "part1", at::kFloat, {g1, 80, 64});
+    check(partb1, "partb1", at::kFloat, {g1, 64});
+  }
   check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
   check(part2, "part2", at::kFloat, {slabs2, 1600, 64});
@@ -403,12 +435,14 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(a!) p1, Tensor(b!) am1, Tensor w2f, Tensor b2, Tensor(c!) p2, Tensor(d!) am2, "
         "Tensor(e!)? xraw=None) -> ()");
   m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
+  m.def("conv2_dgrad_w1(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!)? dp1, Tensor(b!) dy2, Tensor am1, Tensor xraw, "
+        "int cy, int cx, Tensor(c!) part1, Tensor(d!) partb1) -> ()");
   m.def("conv1_wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor(a!) part1, Tensor(b!) partb1, Tensor? xraw=None) -> ()");
   m.def("conv2_wgrad(Tensor p1, Tensor dy2, Tensor(a!) part2, Tensor(b!) partb2) -> ()");
   m.def("wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor(a!) part1, Tensor(b!) partb1, Tensor p1, Tensor dy2, Tensor(c!) part2, Tensor(d!) partb2, "
-        "int groups2, Tensor? xraw=None) -> ()");
+        "int groups2, Tensor? xraw=None, bool with_conv1=True) -> ()");
   m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params) -> ()");
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
@@ -429,6 +463,7 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("conv2_fwd_fp8", &conv2_fwd_fp8);
   m.impl("fp8_roundtrip", &fp8_roundtrip);
   m.impl("conv2_dgrad", &conv2_dgrad);
+  m.impl("conv2_dgrad_w1", &conv2_dgrad_w1);
   m.impl("conv1_wgrad", &conv1_wgrad);
   m.impl("conv2_wgrad", &conv2_wgrad);
   m.impl("wgrad", &wgrad);

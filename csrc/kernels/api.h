@@ -194,6 +194,8 @@ hipError_t dmlc_conv12_fwd(const DmlcConv1FwdArgs* a1, const DmlcConv2FwdArgs* a
 hipError_t dmlc_conv2_fwd_fp8(const DmlcConv2FwdFp8Args* a, hipStream_t s);
 hipError_t dmlc_fp8_roundtrip(const float* x, float* y, int n, float scale, hipStream_t s);
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s);
+// conv2 dgrad + the conv1 weight gradient of each image (one slab per image: w1->g1 == B, xraw set)
+hipError_t dmlc_conv2_dgrad_w1(const DmlcConv2DgradArgs* a, const DmlcConv1WgradArgs* w1, hipStream_t s);
 hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s);
 hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s);

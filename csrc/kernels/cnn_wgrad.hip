@@ -18,16 +18,11 @@
 // Both: the NEXT image's global data is prefetched into registers while the current image is being
 // computed (one exposed memory latency per block instead of one per image); results are fp32
 // split-K partial slabs, one per image group, reduced in fixed order by the SGD kernel.
-#include "conv_common.h"
+#include "w1_common.h"
 
 namespace dmlc {
 
 // ---------------------------------------------------------------------------------------------
-constexpr int W1_DY_LD = 72;                  // dY1 LDS row stride (bf16): 144 B, tr reads conflict-free
-constexpr int W1_PL = 28 * 24 + 8;            // shifted-plane stride (bf16): 1360 B, b128 reads conflict-free
-constexpr int W1_DYT = 576 * W1_DY_LD;        // bf16 elements
-constexpr int W1_XS = 16 * W1_PL;
-constexpr int W1T = 512;                      // 8 waves (2 per SIMD) for the VALU-heavy gather phases
 // dY1 | shifted planes | pool1 grad (bf16) | raw uint8 image [32][32][3] | argmax bytes | reduction
 constexpr size_t W1_LDS = (size_t)(W1_DYT + W1_XS + 9216) * 2 + 3072 + 9216 + (W1T / 64) * 64 * 4;
 
@@ -39,12 +34,12 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
   uint8_t* ams = img + 3072;
   float* red = reinterpret_cast<float*>(ams + 9216);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int g = lane >> 4, li = lane & 15;
   const int ch = w & 1, ks = w >> 1;                     // MFMA: co tiles 2ch, 2ch+1; k-steps ks mod 4
   const int b0 = grp * a.B / a.g1, b1 = (grp + 1) * a.B / a.g1;
   DMLC_STAMP(DMLC_TK_W1, 0);
 
-  for (int e = tid; e < W1_PL / 8; e += W1T) *reinterpret_cast<bf16x8*>(xs + 15 * W1_PL + e * 8) = bf16x8{};
+  w1_zero_plane15(xs, tid);
 
   f32x4 acc[2][5];
 #pragma unroll
@@ -86,82 +81,15 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
     nidx = row_index(b + 2 < last ? b + 2 : last);
     __syncthreads();
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 1);
-    // (a) shifted channel planes straight from the uint8 image: task (yy, x8, kw) -> planes
-    //     kw*3+{0,1,2}, 8 pixels: plane[kw*3+ci][yy][x] = crop[ci][yy-2][x+kw-2] (0 outside the crop)
-    for (int task = tid; task < 28 * 3 * 5; task += W1T) {
-      const int kw = task % 5, r = task / 5, x8 = r % 3, yy = r / 3, iy = yy - 2;
-      const bool rok = iy >= 0 && iy < 24;
-      const uint8_t* srow = img + ((a.cy + (rok ? iy : 0)) * 32 + a.cx) * 3;
-      bf16x8 o0, o1, o2;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int ix = x8 * 8 + kw + j - 2;
-        const bool ok = rok && ix >= 0 && ix < 24;
-        const uint8_t* px = srow + (ok ? ix : 0) * 3;
-        const float f0 = px[0], f1 = px[1], f2 = px[2];
-        o0[j] = (bf16)(ok ? f0 : 0.f); o1[j] = (bf16)(ok ? f1 : 0.f); o2[j] = (bf16)(ok ? f2 : 0.f);
-      }
-      bf16* dst = xs + (kw * 3) * W1_PL + yy * 24 + x8 * 8;
-      *reinterpret_cast<bf16x8*>(dst) = o0;
-      *reinterpret_cast<bf16x8*>(dst + W1_PL) = o1;
-      *reinterpret_cast<bf16x8*>(dst + 2 * W1_PL) = o2;
-    }
-    // (b) pool1 / ReLU backward -> dY1 (bf16, LDS) + bias-grad sums (fp32)
-    for (int task = tid; task < 144 * 8; task += W1T) {
-      const int win = task >> 3, c = task & 7, py = win / 12, px = win - py * 12;
-      float o[4][8];
-      pool_bwd_2x2<12>(dps, ams, py, px, c, o);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
-        *reinterpret_cast<bf16x8*>(dyt + (y * 24 + x) * W1_DY_LD + c * 8) = to_bf16x8(o[k]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bsum[j] += o[k][j];
-      }
-    }
+    w1_planes(xs, img, a.cy, a.cx, tid);
+    w1_pool_bwd(dyt, dps, ams, bsum, tid);
     __syncthreads();
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 2);
-    // (c) MFMA: this wave's k-steps s = ks, ks+4, ... of the 18 (32 pixels each), co tiles 2ch, 2ch+1
-    for (int s = ks; s < 18; s += 4) {
-      const int rA = 32 * s + 8 * g + q, rB = rA + 4;
-      bf16x8 af[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int ct = 2 * ch + h;
-        af[h] = tr_frag(dyt + rA * W1_DY_LD + 16 * ct + 4 * p, dyt + rB * W1_DY_LD + 16 * ct + 4 * p);
-      }
-      const int r0 = 32 * s + 8 * g, y = r0 / 24, x0 = r0 - y * 24;
-#pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        const bf16x8 bx = lds_b128(xs + li * W1_PL + (y + t) * 24 + x0);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) acc[h][t] = mfma16(af[h], bx, acc[h][t]);
-      }
-    }
+    w1_mfma(dyt, xs, acc, ks, ch, g, li);
   }
-  // cross-wave reduction (fixed order) through the dY region, then the fp32 slab [80 k''][64 co]
   __syncthreads();
   DMLC_STAMP(DMLC_TK_W1, 3);
-  f32x4* fl = reinterpret_cast<f32x4*>(smem);
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int t = 0; t < 5; ++t) fl[(ks * 20 + (2 * ch + h) * 5 + t) * 64 + lane] = acc[h][t];
-  block_chunk_sum(bsum, red, tid);
-  __syncthreads();
-  float* out = a.part1 + (size_t)grp * 80 * 64;
-  for (int e = tid; e < 20 * 64; e += W1T) {
-    const f32x4 s = ((fl[e] + fl[1280 + e]) + (fl[2560 + e] + fl[3840 + e]));
-    const int tile = e >> 6, ln = e & 63, ct = tile / 5, t = tile - ct * 5;
-    const int co = 16 * ct + 4 * (ln >> 4), kk = 16 * t + (ln & 15);
-    *reinterpret_cast<f32x4*>(out + kk * 64 + co) = s;
-  }
-  if (tid < 64) {
-    float sb = 0.f;
-#pragma unroll
-    for (int k = 0; k < W1T / 64; ++k) sb += red[k * 64 + tid];
-    a.partb1[grp * 64 + tid] = sb;
-  }
+  w1_flush(smem, red, acc, bsum, a.part1 + (size_t)grp * 80 * 64, a.partb1 + grp * 64, ks, ch, lane, tid);
   DMLC_STAMP(DMLC_TK_W1, 4);
 }
 

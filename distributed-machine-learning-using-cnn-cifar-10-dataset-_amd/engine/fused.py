@@ -152,7 +152,24 @@ class FusedCifarEngine:
         self.merged_wgrad = os.environ.get("DMLC_SPLIT_WGRAD", "0") != "1"
         # conv1 and conv2 forward in one launch (bf16 path; DMLC_SPLIT_FWD=1: two launches)
         self.fused_fwd = os.environ.get("DMLC_SPLIT_FWD", "0") != "1"
-        if self.merged_wgrad:
+        # DMLC_FUSED_W1=1: the conv1 weight gradient inside the conv2-dgrad launch (one slab per image,
+        # dp1 stays in LDS) and a conv2-only weight-gradient launch on the whole chip.  Measured at
+        # B=256 (r2): dgrad+w1 18.4 us + conv2 wgrad (40 pairs) 18.7 us = 37.1 us vs dgrad 11.2 us +
+        # merged wgrad ~26 us -- equal, and the SGD pays for 256 per-image slabs: off by default.
+        self.fused_w1 = self.merged_wgrad and os.environ.get("DMLC_FUSED_W1", "0") == "1"
+        self.keep_dp1 = False          # tests: also write the pool1 gradient to global memory
+        if self.fused_w1:
+            # conv2 wgrad: one 8-wave block per (kh, pair of image groups); the whole chip is its
+            # own, so more pairs than with conv1 alongside (DMLC_W2_PAIRS overrides; more slabs cost
+            # the SGD kernel 410 KB of fp32 reads each)
+            if g2:
+                pairs = (g2 + 1) // 2
+            else:
+                pairs = int(os.environ.get("DMLC_W2_PAIRS", "0")) or max(1, min(B // 2, 51, round(B * 40 / 256)))
+            self.groups2 = g2 or 2 * pairs
+            self.g2 = pairs
+            self.g1 = B                                  # conv1: one slab per image
+        elif self.merged_wgrad:
             # conv2: pairs of ~4.6-image groups (one 8-wave block per (kh, pair), one slab per pair);
             # conv1: exactly the CUs the conv2 blocks leave while that is >= B/4 blocks (one wave of
             # workgroups; 5*pairs + g1 > 256 costs ~10 us).  B=256: 28 pairs + g1=116 -> 24.0 us vs
@@ -294,6 +311,13 @@ class FusedCifarEngine:
     def _conv_backward(self, src=None):
         o = self.ops
         idx, counter, period = src or (self.bidx, None, 1)
+        if self.fused_w1:
+            o.conv2_dgrad_w1(self.dp2, self.am2, self.w2d, self.dp1 if self.keep_dp1 else None, self.dy2, self.am1,
+                             self.xraw, self.cy, self.cx, self.part1, self.partb1)
+            o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
+                    self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw,
+                    False)
+            return
         o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         if self.merged_wgrad:
             o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,

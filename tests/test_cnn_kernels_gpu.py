@@ -39,6 +39,7 @@ def cnn_local_errors(eng, data, labels, idx):
     """{check: rel error} for every kernel of one training step on dataset rows ``idx``."""
     dev = eng.device
     B = eng.Bv
+    eng.keep_dp1 = True                  # the fused dgrad keeps dp1 in LDS unless asked for a copy
     eng.compute_gradients(idx=idx)
     torch.cuda.synchronize()
     flat = eng.flat_params().to(dev)

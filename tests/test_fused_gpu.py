@@ -68,7 +68,7 @@ def test_merged_wgrad_launch_matches_two_kernels(B, g2, monkeypatch):
     conv2 gradient equal up to fp32 summation order -- including an odd group count (idle half)."""
     data, labels = _synthetic(4 * B, seed=7)
     eng = FusedCifarEngine(B, data, labels, seed=6, g2=g2)
-    assert eng.merged_wgrad and eng.groups2 == g2 and eng.g2 == (g2 + 1) // 2
+    assert eng.merged_wgrad and not eng.fused_w1 and eng.groups2 == g2 and eng.g2 == (g2 + 1) // 2
     g_merged = eng.compute_gradients().cpu().clone()
     monkeypatch.setenv("DMLC_SPLIT_WGRAD", "1")
     ref = FusedCifarEngine(B, data, labels, seed=6, g1=eng.g1, g2=g2)
@@ -256,3 +256,30 @@ def test_any_batch_size_masked_tail(B):
     st = eng.read_stats(1)
     assert abs(st["loss"] - want_loss) < 1e-4 * max(1.0, abs(want_loss)), (st, want_loss, float(loss))
     assert abs(st["accuracy"] - want_acc) < 1e-6, (st, want_acc)
+
+
+@pytest.mark.parametrize("B", [64, 256])
+def test_fused_dgrad_conv1_wgrad_matches_separate_launches(B, monkeypatch):
+    """ops.conv2_dgrad_w1 (conv2 dgrad + the conv1 weight gradient of each image in one launch, one
+    slab per image) + the conv2-only weight-gradient launch vs the separate dgrad / merged wgrad
+    launches: dy2 and the conv2 gradient bit-identical, the conv1 slabs of each split group summed
+    equal to that group's slab, the whole gradient equal up to fp32 summation order."""
+    data, labels = _synthetic(4 * B, seed=8)
+    monkeypatch.setenv("DMLC_FUSED_W1", "1")
+    fused = FusedCifarEngine(B, data, labels, seed=9)
+    assert fused.fused_w1 and fused.g1 == B
+    g_f = fused.compute_gradients().cpu().clone()
+    monkeypatch.setenv("DMLC_FUSED_W1", "0")
+    ref = FusedCifarEngine(B, data, labels, seed=9, g2=fused.groups2)
+    assert not ref.fused_w1
+    g_r = ref.compute_gradients().cpu().clone()
+    assert torch.equal(fused.dy2, ref.dy2)
+    assert torch.equal(fused.part2, ref.part2) and torch.equal(fused.partb2, ref.partb2)
+    for grp in range(ref.g1):                        # the split kernel's groups: images [b0, b1)
+        b0, b1 = grp * B // ref.g1, (grp + 1) * B // ref.g1
+        want = ref.part1[grp]
+        got = fused.part1[b0:b1].sum(0)
+        assert torch.allclose(got, want, rtol=1e-4, atol=1e-5 * float(want.abs().max()) + 1e-12), grp
+    for s in M.PARAM_SPECS:
+        a, b = g_f[s.offset:s.offset + s.numel], g_r[s.offset:s.offset + s.numel]
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()) + 1e-12), s.name

@@ -63,13 +63,19 @@ def main():
                                         eng.loss_part, eng.correct_part, None), a.iters)
     res["fc_bwd_gemm"] = timeit(eng._fc_backward, a.iters)
     res["conv2_dgrad"] = timeit(lambda: o.conv2_dgrad(eng.dp2, eng.am2, eng.w2d, eng.dp1, eng.dy2), a.iters)
-    res["conv1_wgrad"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx,
-                                                      eng.dp1, eng.am1, eng.part1, eng.partb1, eng.xraw), a.iters)
+    if eng.fused_w1:
+        res["conv2_dgrad_w1"] = timeit(lambda: o.conv2_dgrad_w1(eng.dp2, eng.am2, eng.w2d, None, eng.dy2, eng.am1,
+                                                                eng.xraw, eng.cy, eng.cx, eng.part1, eng.partb1),
+                                       a.iters)
+    if not eng.fused_w1:
+        res["conv1_wgrad"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx, eng.dp1,
+                                                          eng.am1, eng.part1, eng.partb1, eng.xraw), a.iters)
     if not eng.merged_wgrad:
         res["conv2_wgrad"] = timeit(lambda: o.conv2_wgrad(eng.p1, eng.dy2, eng.part2, eng.partb2), a.iters)
     res["wgrad_merged"] = timeit(lambda: o.wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx,
                                                  eng.dp1, eng.am1, eng.part1, eng.partb1, eng.p1, eng.dy2,
-                                                 eng.part2, eng.partb2, eng.groups2, eng.xraw), a.iters)
+                                                 eng.part2, eng.partb2, eng.groups2, eng.xraw,
+                                                 not eng.fused_w1), a.iters)
     res["conv_bwd"] = timeit(eng._conv_backward, a.iters)
     res["sgd_reduce_only"] = timeit(lambda: eng._sgd(mode=1), a.iters)
     res["sgd_full"] = timeit(lambda: eng._sgd(mode=0), a.iters)
@@ -77,7 +83,8 @@ def main():
     eng.capture()
     res["step_graph"] = timeit(lambda: eng.graphs[0].replay(), a.iters)
     res["sum_kernels"] = sum(v for k, v in res.items()
-                             if not k.startswith("step") and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad")
+                             if not k.startswith("step") and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad",
+                                                                   "conv2_dgrad" if eng.fused_w1 else "conv2_dgrad_w1")
                              and k not in (("conv1_fwd", "conv2_fwd") if eng.fused_fwd else ("conv12_fwd",)))
     cfg = dict(batch=a.batch, g1=eng.g1, g2=eng.g2, fc1_split=eng.fc1_split)
     print(json.dumps({"config": cfg, "us": {k: round(v, 2) for k, v in res.items()}}), flush=True)

@@ -17,7 +17,17 @@ pass() {
   echo "[pmc $name] rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 }
-pass sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+PASSES=${PMC_PASSES:-sq fetch write}
+for p in $PASSES; do
+  case $p in
+    sq) pass sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES GRBM_GUI_ACTIVE ;;
+    issue) pass issue SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU ;;
+    fetch) pass fetch FETCH_SIZE ;;
+    write) pass write WRITE_SIZE ;;
+  esac
+done
+echo "pmc done"
+exit 0
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 echo "pmc done"

@@ -44,6 +44,8 @@ def main():
                 merged[k][c] = (sum(per.values()) / max(1, len(per)), len(per))
     cols = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_LDS_IDX_ACTIVE",
             "SQ_LDS_BANK_CONFLICT", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "FETCH_SIZE", "WRITE_SIZE"]
+    extra = sorted({c for m in merged.values() for c in m} - set(cols))
+    cols = [c for c in cols if any(c in m for m in merged.values())] + extra
     print("per dispatch means (counters summed over all instances of one dispatch)")
     hdr = ["kernel", "n"] + cols + ["mfma_busy%", "lds_conflict%", "fetch_MB(x2)", "write_MB"]
     print(" | ".join(hdr))
