@@ -31,13 +31,19 @@ Geom geom(int64_t cin, int64_t cout, int64_t hin, int64_t stride) {
 
 // per-layer statistics accumulators: fp64 [NSLOT][2][64] (sum, sum of squares / R1, R2)
 void check_stat(const Tensor& t, const char* n) { check_numel(t, n, at::kDouble, DMLC_RN_NSLOT * 128); }
+// deterministic-mode side buffer of one statistic: [B][128] fp32 partials + the group tickets
+float* det_ptr(const c10::optional<Tensor>& det, int64_t B) {
+  if (!det.has_value()) return nullptr;
+  check_numel(*det, "det", at::kFloat, B * 128 + DMLC_RN_DET_TICKETS);
+  return det->data_ptr<float>();
+}
 
 void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::optional<Tensor>& data,
             const c10::optional<Tensor>& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
             int64_t cx, const c10::optional<Tensor>& z_prev, const c10::optional<Tensor>& stat_prev,
             const c10::optional<Tensor>& gamma_prev, const c10::optional<Tensor>& beta_prev,
             const c10::optional<Tensor>& sc_src, int64_t sc_mode, const c10::optional<Tensor>& a_out, const Tensor& w,
-            const Tensor& z, const Tensor& stat) {
+            const Tensor& z, const Tensor& stat, const c10::optional<Tensor>& stat_det) {
   const Geom g = geom(cin, cout, hin, stride);
   const int64_t B = z.size(0);
   check(w, "w", at::kBFloat16, {g.cout, g.kp()});
@@ -73,6 +79,7 @@ void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::o
     a.a_out = a_out->data_ptr(); a.inv_n_prev = 1.f / (float)(B * hin * hin);
   }
   a.w = w.data_ptr(); a.z = z.data_ptr(); a.stat = stat.data_ptr<double>();
+  a.stat_det = det_ptr(stat_det, B);
   c10::DeviceGuard guard(z.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_fwd(&gc, &a, stream_of(z)));
@@ -82,7 +89,7 @@ DmlcRnDgradArgs dgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
                            const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd,
                            const Tensor& a_prev, const Tensor& z_prev, const Tensor& stat_prev,
                            const c10::optional<Tensor>& gy_sc, int64_t sc_mode, const Tensor& gy_prev,
-                           const Tensor& red_prev) {
+                           const Tensor& red_prev, const c10::optional<Tensor>& red_det) {
   TORCH_CHECK(cin >= 16, "rn_dgrad: the stem has no input gradient");
   const int64_t B = gy.size(0), ho = g.hout();
   check(gy, "gy", at::kBFloat16, {B, ho, ho, cout});
@@ -109,16 +116,17 @@ DmlcRnDgradArgs dgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
   a.inv_n_prev = 1.f / (float)(B * hin * hin);
   a.gy_sc = sc_mode ? gy_sc->data_ptr() : nullptr; a.sc_mode = (int)sc_mode;
   a.gy_prev = gy_prev.data_ptr(); a.red_prev = red_prev.data_ptr<double>(); a.B = (int)B;
+  a.red_det = det_ptr(red_det, B);
   return a;
 }
 
 void rn_dgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
               const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
               const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
-              const Tensor& gy_prev, const Tensor& red_prev) {
+              const Tensor& gy_prev, const Tensor& red_prev, const c10::optional<Tensor>& red_det) {
   const Geom g = geom(cin, cout, hin, stride);
   const DmlcRnDgradArgs a = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
-                                       gy_sc, sc_mode, gy_prev, red_prev);
+                                       gy_sc, sc_mode, gy_prev, red_prev, red_det);
   c10::DeviceGuard guard(gy.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_dgrad(&gc, &a, stream_of(gy)));
@@ -171,10 +179,10 @@ void rn_wgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10:
 void rn_bwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
             const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
             const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
-            const Tensor& gy_prev, const Tensor& red_prev, const Tensor& part) {
+            const Tensor& gy_prev, const Tensor& red_prev, const Tensor& part, const c10::optional<Tensor>& red_det) {
   const Geom g = geom(cin, cout, hin, stride);
   const DmlcRnDgradArgs d = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
-                                       gy_sc, sc_mode, gy_prev, red_prev);
+                                       gy_sc, sc_mode, gy_prev, red_prev, red_det);
   const DmlcRnWgradArgs w = wgrad_args(g, cin, cout, hin, c10::nullopt, c10::nullopt, c10::nullopt, 1, 0, 0, a_prev, gy,
                                        z, stat, red, gamma, part);
   c10::DeviceGuard guard(gy.device());
@@ -186,7 +194,7 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
              const Tensor& fcw, const Tensor& fcb, const Tensor& labels, const Tensor& idx,
              const c10::optional<Tensor>& counter, int64_t period, double inv_batch, const Tensor& gy,
              const Tensor& red, const Tensor& fc_part, const Tensor& loss_img, const Tensor& correct_img,
-             const c10::optional<Tensor>& logits) {
+             const c10::optional<Tensor>& logits, const c10::optional<Tensor>& red_det) {
   const int64_t B = z.size(0);
   check(z, "z", at::kBFloat16, {B, 8, 8, 64});
   check_stat(stat, "stat"); check_stat(red, "red");
@@ -209,6 +217,7 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
   check_order_fits(a.src, labels.size(0));
   a.inv_batch = (float)inv_batch;
   a.gy = gy.data_ptr(); a.red = red.data_ptr<double>(); a.fc_part = fc_part.data_ptr<float>();
+  a.red_det = det_ptr(red_det, B);
   a.loss_img = loss_img.data_ptr<float>(); a.correct_img = correct_img.data_ptr<int>();
   a.logits_out = nullptr;
   if (logits.has_value()) {
@@ -300,19 +309,20 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
 TORCH_LIBRARY_FRAGMENT(dmlc, m) {
   m.def("rn_fwd(int cin, int cout, int hin, int stride, Tensor? data, Tensor? idx, Tensor? counter, int period, "
         "int cy, int cx, Tensor? z_prev, Tensor? stat_prev, Tensor? gamma_prev, Tensor? beta_prev, Tensor? sc_src, "
-        "int sc_mode, Tensor(a!)? a_out, Tensor w, Tensor(b!) z, Tensor(c!) stat) -> ()");
+        "int sc_mode, Tensor(a!)? a_out, Tensor w, Tensor(b!) z, Tensor(c!) stat, Tensor(d!)? stat_det=None) -> ()");
   m.def("rn_dgrad(int cin, int cout, int hin, int stride, Tensor gy, Tensor z, Tensor stat, Tensor red, "
         "Tensor gamma, Tensor wd, Tensor a_prev, Tensor z_prev, Tensor stat_prev, Tensor? gy_sc, int sc_mode, "
-        "Tensor(a!) gy_prev, Tensor(b!) red_prev) -> ()");
+        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!)? red_det=None) -> ()");
   m.def("rn_wgrad(int cin, int cout, int hin, int stride, Tensor? data, Tensor? idx, Tensor? counter, int period, "
         "int cy, int cx, Tensor? x, Tensor gy, Tensor z, Tensor stat, Tensor red, Tensor gamma, "
         "Tensor(a!) part) -> ()");
   m.def("rn_bwd(int cin, int cout, int hin, int stride, Tensor gy, Tensor z, Tensor stat, Tensor red, "
         "Tensor gamma, Tensor wd, Tensor a_prev, Tensor z_prev, Tensor stat_prev, Tensor? gy_sc, int sc_mode, "
-        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part) -> ()");
+        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part, Tensor(d!)? red_det=None) -> ()");
   m.def("rn_head(Tensor z, Tensor stat, Tensor gamma, Tensor beta, Tensor sc, Tensor fcw, Tensor fcb, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, Tensor(a!) gy, Tensor(b!) red, "
-        "Tensor(c!) fc_part, Tensor(d!) loss_img, Tensor(e!) correct_img, Tensor(f!)? logits) -> ()");
+        "Tensor(c!) fc_part, Tensor(d!) loss_img, Tensor(e!) correct_img, Tensor(f!)? logits, "
+        "Tensor(g!)? red_det=None) -> ()");
   m.def("rn_sgd(Tensor(a!) master, Tensor(b!)? grad, float grad_scale, Tensor(c!) state, int[] conv_off, "
         "int[] gamma_off, int[] beta_off, int[] mm_off, int[] mv_off, int fcw_off, int fcb_off, Tensor[] part, "
         "Tensor(d!)[] wf, Tensor(e!)[] wd, Tensor stat, Tensor red, Tensor fc_part, Tensor loss_img, "

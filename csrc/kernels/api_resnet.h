@@ -1,7 +1,10 @@
 // Host-side launch API of the fused ResNet-20 kernels (csrc/kernels/resnet.hip).
 //
-// Conventions: activations NHWC bf16; per-layer BatchNorm statistics are fp64 accumulators
-// (atomicAdd of per-block fp32 partials into one of NSLOT copies; zeroed once per step); conv weights have two bf16 shadows:
+// Conventions: activations NHWC bf16; per-layer BatchNorm statistics live in NSLOT fp64 slots per
+// layer (slot = producing block & 7).  Deterministic mode (`det` side buffer set): every producing
+// block stores its fp32 partials, and the last block of each slot's group (per-group ticket) sums the
+// group's partials in block order into the slot -- bitwise reproducible, no zeroing.  Otherwise: fp64
+// atomicAdd into the slot (zeroed once per step).  Conv weights have two bf16 shadows:
 //   fwd   w [COUT][KP]  k  = tap*CINP + ci        (tap = kh*3 + kw, CINP = max(CIN, 8), KP = 9*CINP -> x32)
 //   dgrad wd [CIN][KPD] k' = tap'*COUT + co       (tap' = 8 - tap: rotated 180 degrees, KPD = 9*COUT -> x32)
 // Layer l computes z_l = conv_l(x_l) with x_l = a_{l-1}, a = relu(bn(z) [+ shortcut]).
@@ -27,6 +30,7 @@ struct DmlcRnFwdArgs {
   const void* w;             // bf16 [COUT][KP]
   void* z;                   // bf16 [B][Hout][Hout][COUT]
   double* stat;              // [NSLOT][2][64] accumulators of layer l
+  float* stat_det;           // nullable: deterministic side buffer [B][128] fp32 partials + 8x32 tickets
   int B;
 };
 
@@ -40,6 +44,7 @@ struct DmlcRnDgradArgs {
   int sc_mode;               // 1 identity, 2 subsample (gy_sc is [B][Hin/2][Hin/2][2*CIN])
   void* gy_prev;             // bf16 [B][Hin][Hin][CIN]
   double* red_prev;          // [NSLOT][2][64]
+  float* red_det;            // nullable: deterministic side buffer of red_prev (see stat_det)
   int B;
 };
 
@@ -58,6 +63,7 @@ struct DmlcRnHeadArgs {
   const int* labels; DmlcIndexSrc src; float inv_batch;
   void* gy;                  // bf16 [B][8][8][64] g_y_18
   double* red;               // [NSLOT][2][64] reductions of layer 18
+  float* red_det;            // nullable: deterministic side buffer of red
   float* fc_part;            // [B][656] per-image dW_fc (640) + db_fc (10) + pad
   float* loss_img; int* correct_img;    // [B]
   float* logits_out;         // nullable [B][10]
@@ -66,6 +72,7 @@ struct DmlcRnHeadArgs {
 
 #define DMLC_RN_LAYERS 19
 #define DMLC_RN_NSLOT 8      // fp64 statistics accumulators per layer: [NSLOT][2][64] (slot = block & 7)
+#define DMLC_RN_DET_TICKETS (8 * 32)   // uints after the [nblk][128] partials of a det side buffer
 struct DmlcRnSgdArgs {
   float* master; int nparams;
   float* grad; float grad_scale;   // DP: modes 1 (write) / 2 (read, scaled)

@@ -77,10 +77,76 @@ DEV uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint2, v).x;
 }
 
+// Deterministic slot flush: this block's 2 x C fp32 channel partials go to its row of the side buffer
+// `det` ([nblk][128] fp32, then DMLC_RN_DET_TICKETS uints) with device-coherent (sc1) stores; once
+// they are acknowledged the block takes a ticket of its group (blocks b with b & 7 == slot), and the
+// group's last arriver sums the group's rows in block order (fp64) into the slot with a plain store
+// -- the consumers run in later launches.  No fp64 atomics: the sums are bitwise reproducible (graph
+// replay == eager launches).  t1/t2 valid in threads tid < C; every thread of the block must call.
+template <int C>
+DEV void det_flush(float t1, float t2, double* dst, float* det, int nblk, int tid) {
+  __shared__ int flag[1];
+  const int b = blockIdx.x, slot = b & (NSLOT - 1);
+  if (tid < C) {
+    __hip_atomic_store(det + (size_t)b * 128 + tid, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(det + (size_t)b * 128 + 64 + tid, t2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): this thread's partial stores acknowledged
+  __syncthreads();
+  if (tid == 0) {
+    unsigned* tk = reinterpret_cast<unsigned*>(det + (size_t)nblk * 128) + slot * 32;
+    const unsigned gsize = (unsigned)((nblk - slot + NSLOT - 1) / NSLOT);
+    const bool last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
+    if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
+    flag[0] = last ? 1 : 0;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  // the group's rows: 8 loads in flight per thread (independent relaxed atomics), summed in block
+  // order; 2 threads per statistic each take every other row, combined in fixed order through LDS
+  __shared__ double part2[2][128];
+  const int e = tid & 127, h = tid >> 7;              // statistic, half of the group's rows
+  const int rows = (nblk - slot + NSLOT - 1) / NSLOT;
+  // device-coherent (sc1) loads, 8 in flight per thread: issued as one asm block (the compiler puts a
+  // vmcnt(0) behind every atomic load), rows past the group clamped to row `slot` and weighted 0
+  double s = 0.0;
+  if (tid < 256 && (e & 63) < C) {
+    for (int r0 = h; r0 < rows; r0 += 16) {
+      const float* p[8];
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = r0 + 2 * u < rows ? r0 + 2 * u : 0;
+        p[u] = det + (size_t)(slot + NSLOT * r) * 128 + e;
+      }
+      asm volatile(
+          "global_load_dword %0, %8, off sc1\n\t"
+          "global_load_dword %1, %9, off sc1\n\t"
+          "global_load_dword %2, %10, off sc1\n\t"
+          "global_load_dword %3, %11, off sc1\n\t"
+          "global_load_dword %4, %12, off sc1\n\t"
+          "global_load_dword %5, %13, off sc1\n\t"
+          "global_load_dword %6, %14, off sc1\n\t"
+          "global_load_dword %7, %15, off sc1\n\t"
+          "s_waitcnt vmcnt(0)"
+          : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+          : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+          : "memory");
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += r0 + 2 * u < rows ? (double)v[u] : 0.0;
+    }
+  }
+  if (tid < 256) part2[h][e] = s;
+  __syncthreads();
+  if (tid < 128 && (e & 63) < C) dst[slot * 128 + e] = part2[0][e] + part2[1][e];
+}
+
 // block-level channel reduction of per-lane partials (lanes with equal li share a channel group) and
-// one fp64 atomic per channel into this block's slot
+// either the deterministic slot flush (det != null) or one fp64 atomic per channel into this block's
+// slot
 template <int CT, int C>
-DEV void reduce_flush(float (&s1)[4], float (&s2)[4], float* red, double* dst, int w, int g, int li, int tid) {
+DEV void reduce_flush(float (&s1)[4], float (&s2)[4], float* red, double* dst, int w, int g, int li, int tid,
+                      float* det = nullptr, int nblk = 0) {
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -94,11 +160,17 @@ DEV void reduce_flush(float (&s1)[4], float (&s2)[4], float* red, double* dst, i
     }
   }
   __syncthreads();
+  float t1 = 0.f, t2 = 0.f;
   if (tid < C) {
-    float t1 = 0.f, t2 = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 4; ++ww)
       if (ww % CT == tid / 16) { t1 += red[(ww * 2) * 64 + tid]; t2 += red[(ww * 2 + 1) * 64 + tid]; }
+  }
+  if (det) {
+    det_flush<C>(t1, t2, dst, det, nblk, tid);
+    return;
+  }
+  if (tid < C) {
     double* d = dst + (blockIdx.x & (NSLOT - 1)) * 128;
     RN_ATOMIC_ADD(d + tid, (double)t1);
     RN_ATOMIC_ADD(d + 64 + tid, (double)t2);
@@ -246,7 +318,7 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s1[r] += acc[i][r]; s2[r] += acc[i][r] * acc[i][r]; }
   }
-  reduce_flush<F::CT, COUT>(s1, s2, red, a.stat, w, g, li, tid);
+  reduce_flush<F::CT, COUT>(s1, s2, red, a.stat, w, g, li, tid, a.stat_det, a.B);
 }
 
 // ================================ dgrad ========================================================
@@ -388,7 +460,7 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
     }
     *reinterpret_cast<bf16x4*>(gyo + px * CIN + c0) = pack4(gy[0], gy[1], gy[2], gy[3]);
   }
-  reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid);
+  reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid, a.red_det, a.B);
 }
 
 // ================================ wgrad ========================================================
@@ -662,10 +734,16 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   redl[0][w][c] = r1;
   redl[1][w][c] = r2;
   __syncthreads();
+  const float t1 = tid < 64 ? redl[0][0][tid] + redl[0][1][tid] + redl[0][2][tid] + redl[0][3][tid] : 0.f;
+  const float t2 = tid < 64 ? redl[1][0][tid] + redl[1][1][tid] + redl[1][2][tid] + redl[1][3][tid] : 0.f;
+  if (a.red_det) {
+    det_flush<64>(t1, t2, a.red, a.red_det, a.B, tid);
+    return;
+  }
   if (tid < 64) {
     double* d = a.red + (b & (NSLOT - 1)) * 128;
-    RN_ATOMIC_ADD(d + tid, (double)(redl[0][0][tid] + redl[0][1][tid] + redl[0][2][tid] + redl[0][3][tid]));
-    RN_ATOMIC_ADD(d + 64 + tid, (double)(redl[1][0][tid] + redl[1][1][tid] + redl[1][2][tid] + redl[1][3][tid]));
+    RN_ATOMIC_ADD(d + tid, (double)t1);
+    RN_ATOMIC_ADD(d + 64 + tid, (double)t2);
   }
 }
 

@@ -89,7 +89,8 @@ class FusedResNetEngine:
                  decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, world_size: int = 1,
                  rank: int = 0, process_group=None, seed: int = 0, groups: Optional[List[int]] = None,
                  stats_len: int = 4096, comm_dtype: str = "fp32", wgrad_branch: Optional[bool] = None,
-                 allreduce: str = "auto", capture_comm: Optional[bool] = None, dp_force: bool = False):
+                 allreduce: str = "auto", capture_comm: Optional[bool] = None, dp_force: bool = False,
+                 deterministic: Optional[bool] = None):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -159,6 +160,17 @@ class FusedResNetEngine:
         # [stat | red] fp64 sums, NSLOT copies per layer (see csrc/kernels/resnet.hip)
         self.acc = torch.zeros(2, NL, NSLOT, 128, dtype=torch.float64, device=dev)
         self.stat, self.red = self.acc[0], self.acc[1]
+        # deterministic BN statistics (default): per-block fp32 partials + per-slot group tickets, the
+        # group's last block sums its partials in block order into the slot (resnet.hip det_flush) --
+        # bitwise reproducible, no per-step zeroing; DMLC_RN_DETERMINISTIC=0: fp64 atomics
+        if deterministic is None:
+            deterministic = os.environ.get("DMLC_RN_DETERMINISTIC", "1") != "0"
+        self.deterministic = bool(deterministic)
+        self.det = (torch.zeros(2, NL, B * 128 + 8 * 32, dtype=torch.float32, device=dev)
+                    if self.deterministic else None)
+        det = (lambda k, l: self.det[k][l]) if self.deterministic else (lambda k, l: None)
+        self._det_stat = [det(0, l) for l in range(NL)]
+        self._det_red = [det(1, l) for l in range(NL)]
         self.groups = groups or [self._pick_groups(B, ci, co) for _, ci, co, _, _ in LAYERS]
         self.part = [z(g, _kp(ci), co, dt=torch.float32) for g, (_, ci, co, _, _) in zip(self.groups, LAYERS)]
         self.fc_part = z(B, 656, dt=torch.float32)
@@ -223,11 +235,12 @@ class FusedResNetEngine:
     # --- kernels ------------------------------------------------------------------------------
     def _forward(self, idx, counter, period, logits_out=None):
         o = self.ops
-        self.acc.zero_()
+        if not self.deterministic:
+            self.acc.zero_()
         for l, (_, ci, co, h, s) in enumerate(LAYERS):
             if l == 0:
                 o.rn_fwd(ci, co, h, s, self.data, idx, counter, period, 0, 0, None, None, None, None, None, 0, None,
-                         self.wf[0], self.z[0], self.stat[0])
+                         self.wf[0], self.z[0], self.stat[0], self._det_stat[0])
                 continue
             p = l - 1
             sc_mode, sc_src = 0, None
@@ -235,10 +248,10 @@ class FusedResNetEngine:
                 sc_mode = _block_sc_mode(p)
                 sc_src = self.a[p - 2]
             o.rn_fwd(ci, co, h, s, None, None, None, 1, 0, 0, self.z[p], self.stat[p], self.gamma[p], self.beta[p],
-                     sc_src, sc_mode, self.a[p], self.wf[l], self.z[l], self.stat[l])
+                     sc_src, sc_mode, self.a[p], self.wf[l], self.z[l], self.stat[l], self._det_stat[l])
         o.rn_head(self.z[18], self.stat[18], self.gamma[18], self.beta[18], self.a[16], self.fcw, self.fcb,
                   self.labels, idx, counter, period, 1.0 / (self.B * self.world_size), self.gy[18], self.red[18],
-                  self.fc_part, self.loss_img, self.correct_img, logits_out)
+                  self.fc_part, self.loss_img, self.correct_img, logits_out, self._det_red[18])
 
     def _wgrad(self, l):
         _, ci, co, h, s = LAYERS[l]
@@ -264,7 +277,7 @@ class FusedResNetEngine:
                     gy_sc = self.gy[l + 1]
                 o.rn_bwd(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
                          self.a[l - 1], self.z[l - 1], self.stat[l - 1], gy_sc, sc_mode, self.gy[l - 1],
-                         self.red[l - 1], self.part[l])
+                         self.red[l - 1], self.part[l], self._det_red[l - 1])
             self._wgrad(0)
             return
         for l in range(NL - 1, -1, -1):
@@ -284,7 +297,8 @@ class FusedResNetEngine:
                 sc_mode = _block_sc_mode(l + 1)
                 gy_sc = self.gy[l + 1]
             o.rn_dgrad(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
-                       self.a[p], self.z[p], self.stat[p], gy_sc, sc_mode, self.gy[p], self.red[p])
+                       self.a[p], self.z[p], self.stat[p], gy_sc, sc_mode, self.gy[p], self.red[p],
+                       self._det_red[p])
         if side is not main:
             main.wait_stream(side)
 
