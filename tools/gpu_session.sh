@@ -19,6 +19,7 @@ for s in $STEPS; do
     b20) timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/bench20.log 2>&1; ok $? b20 ;;
     b400) timeout -k 10 200 python bench.py --steps 400 --warmup 20 > gpurun_out/bench400.log 2>&1; ok $? b400 ;;
     b1024) timeout -k 10 200 python bench.py --steps 200 --warmup 20 --batch 1024 > gpurun_out/bench1024.log 2>&1; ok $? b1024 ;;
+    rnprof) rm -rf gpurun_out/rnprof; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rnprof -o run -- python3 bench.py --model resnet20 --steps 30 --warmup 5 > gpurun_out/rnprof.log 2>&1; ok $? rnprof ;;
     lat) timeout -k 10 200 python tools/launch_latency.py > gpurun_out/launch_latency.json 2> gpurun_out/launch_latency.err; ok $? lat ;;
     cnn) timeout -k 10 400 python -u -m pytest tests/test_cnn_kernels_gpu.py tests/test_fused_gpu.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_cnn.log 2>&1; ok $? cnn ;;
     kbench) timeout -k 10 200 python tools/kbench.py > gpurun_out/kbench.json 2> gpurun_out/kbench.err; ok $? kbench ;;
