@@ -114,7 +114,7 @@ def parse():
                          "the timed region) and keep the faster")
     ap.add_argument("--capture-comm", choices=["auto", "on", "off"], default="auto",
                     help="RCCL all-reduce inside the step HIP graph (auto: on over nccl)")
-    ap.add_argument("--steps-per-graph", type=int, default=8, help="longest chain of steps per graph replay")
+    ap.add_argument("--steps-per-graph", type=int, default=32, help="longest chain of steps per graph replay")
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
     ap.add_argument("--dataset-size", type=int, default=50000)
