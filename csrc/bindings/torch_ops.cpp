@@ -208,11 +208,12 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
            int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
            const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2,
            const c10::optional<Tensor>& xraw, bool with_conv1) {
-  const int64_t B = p1.size(0), g1 = with_conv1 ? part1.size(0) : 0, g2 = groups2, slabs2 = (groups2 + 1) / 2;
+  const int64_t B = p1.size(0), g1 = with_conv1 ? part1.size(0) : 0, g2 = groups2;
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
   TORCH_CHECK((!with_conv1 || (g1 >= 1 && g1 <= B)) && g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
-  TORCH_CHECK(part2.size(0) == slabs2, "wgrad: conv2 slabs must be ceil(groups2 / 2)");
+  TORCH_CHECK(part2.size(0) == g2, "wgrad: one conv2 slab per image group");
+  TORCH_CHECK(g1 + 4 * g2 <= 1024, "wgrad: too many workgroups");
   if (with_conv1) {
     check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
     check(am1, "am1", at::kByte, {B, 12, 12, 64});
@@ -221,8 +222,8 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
   }
   check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  check(part2, "part2", at::kFloat, {slabs2, 1600, 64});
-  check(partb2, "partb2", at::kFloat, {slabs2, 64});
+  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+  check(partb2, "partb2", at::kFloat, {g2, 64});
   c10::DeviceGuard guard(dp1.device());
   DmlcWgradArgs a;
   a.w1.data = data.data_ptr<uint8_t>(); a.w1.src = index_src(idx, counter, period, B);

@@ -94,17 +94,17 @@ struct DmlcConv1WgradArgs {
   int B;
 };
 
-// conv2 weight gradient: blocks (kh, image group); fp32 partial slab per group.
+// conv2 weight gradient: blocks (input-channel quarter, image group); fp32 partial slab per group.
 struct DmlcConv2WgradArgs {
   const void* p1;           // bf16 [B][12][12][64]   (conv2 input)
   const void* dy2;          // bf16 [B][144][64]      (conv2 pre-activation gradient)
   float* part2;             // [g2][1600][64]
-  float* partb2;            // [g2][64] conv2 bias-grad partials (written by the kh == 0 blocks)
+  float* partb2;            // [g2][64] conv2 bias-grad partials (written by the c4 == 0 blocks)
   int g2;
   int B;
 };
 
-// Both weight gradients in one launch (blocks [0,g1): conv1; then conv2 as 4-wave halves).
+// Both weight gradients in one launch (blocks [0,g1): conv1; then 4 * g2 conv2 blocks, one slab per group).
 struct DmlcWgradArgs {
   DmlcConv1WgradArgs w1;
   DmlcConv2WgradArgs w2;

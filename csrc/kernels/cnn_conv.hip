@@ -92,7 +92,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* xin = reinterpret_cast<bf16*>(smem);
   bf16* cout = xin + C1_XIN;
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15, cp = w & 1, pq = w >> 1;
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 
@@ -175,7 +175,7 @@ DEV void ws_dma(const bf16* Wg, int kh, bf16* buf, int w, int lane) {
 template <int NPX>
 DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][NPX], int pg, int cp,
                     int g, int li, int tid) {
-  const int w = tid >> 6, lane = tid & 63, sw = li & 7;
+  const int w = wave_id(), lane = tid & 63, sw = li & 7;
   // Per-lane LDS element offsets, computed once: every fragment read of the loop is then one
   // ds_read_b128 at (offset register + compile-time immediate), no per-chunk address VALU (the swizzle
   // arithmetic had made this loop VALU-issue-bound: ~3 integer ops per MFMA).
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd(DmlcConv2FwdArgs a) {
   bf16* xin = reinterpret_cast<bf16*>(smem);
   bf16* cout = xin + C2_XIN;
   bf16* ws = cout + C2_OUT;
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15;
   const bf16* in = reinterpret_cast<const bf16*>(a.in) + (size_t)b * 9216;
   DMLC_STAMP(DMLC_TK_CONV2_FWD, 0);
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
   bf16* dp2 = outs + C2_OUT;                                    // [36][64] staged pool2 grad
   uint8_t* am2 = reinterpret_cast<uint8_t*>(dp2 + 2304);        // [36][64] staged argmax
   bf16* ws = reinterpret_cast<bf16*>(am2 + 2304);               // weight slices (conv2_core)
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15;
   DMLC_STAMP(DMLC_TK_DGRAD, 0);
   stage16<288>(dp2, reinterpret_cast<const bf16*>(a.dp2) + (size_t)b * 2304, tid);
@@ -354,10 +354,10 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
 // conv2 only (more CUs for it), and dp1 never goes through global memory.  One fp32 slab per image.
 // LDS: [0, 32K) conv2 core input, then the shifted planes (w1_common.h) | [32K, 50K) dp1 [144][64]
 // unswizzled | dp2 + argmax2 | weight slices (80 KB), then dY1 / the reduction buffer | argmax1 |
-// reduction rows | raw image.
+// raw image.
 constexpr size_t DW_OUTS = C2_XIN * 2, DW_DP2 = DW_OUTS + C2_OUT * 2, DW_AM2 = DW_DP2 + 2304 * 2;
-constexpr size_t DW_WS = DW_AM2 + 2304, DW_AM1 = DW_WS + (size_t)W1_DYT * 2, DW_RED = DW_AM1 + 9216;
-constexpr size_t DW_IMG = DW_RED + W1T * 4, DW_LDS = DW_IMG + 3072;
+constexpr size_t DW_WS = DW_AM2 + 2304, DW_AM1 = DW_WS + ((size_t)W1_DYT * 2 > WS_BYTES ? (size_t)W1_DYT * 2 : WS_BYTES);
+constexpr size_t DW_IMG = DW_AM1 + 9216, DW_LDS = DW_IMG + 3072;
 static_assert(DW_WS + WS_BYTES <= DW_AM1 && W1_FL_BYTES <= (size_t)W1_DYT * 2, "dgrad+w1 LDS map");
 static_assert((size_t)W1_XS * 2 <= DW_OUTS && DW_LDS <= 160 * 1024, "dgrad+w1 LDS map");
 
@@ -376,9 +376,8 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_w1(DmlcConv2DgradArgs a, 
   uint8_t* am2 = reinterpret_cast<uint8_t*>(smem + DW_AM2);
   bf16* ws = reinterpret_cast<bf16*>(smem + DW_WS);
   uint8_t* am1 = reinterpret_cast<uint8_t*>(smem + DW_AM1);
-  float* red = reinterpret_cast<float*>(smem + DW_RED);
   uint8_t* img = reinterpret_cast<uint8_t*>(smem + DW_IMG);
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15;
   DMLC_STAMP(DMLC_TK_DGRAD, 0);
   // the conv1 wgrad operands of this image: in flight during the whole conv2 dgrad
@@ -423,11 +422,11 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_w1(DmlcConv2DgradArgs a, 
   bf16* xs = dyp;
   bf16* dyt = ws;
   const int ch = w & 1, ks = w >> 1;
-  w1_zero_plane15(xs, tid);
+  w1_ones_plane15(xs, tid);
+  w1_zero_dy(dyt, tid);
+  lds_barrier();
   w1_planes(xs, img, w1.cy, w1.cx, tid);
-  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  w1_pool_bwd(dyt, outs, am1, bsum, tid);
-  __syncthreads();
+  w1_pool_bwd(dyt, outs, am1, w, lane);            // ends with a barrier: dY1 and the planes complete
   f32x4 acc[2][5];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -435,8 +434,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_w1(DmlcConv2DgradArgs a, 
     for (int t = 0; t < 5; ++t) acc[h][t] = zero4();
   w1_mfma(dyt, xs, acc, ks, ch, g, li);
   __syncthreads();
-  w1_flush(reinterpret_cast<char*>(ws), red, acc, bsum, w1.part1 + (size_t)b * 80 * 64, w1.partb1 + b * 64, ks, ch,
-           lane, tid);
+  w1_flush(reinterpret_cast<char*>(ws), acc, w1.part1 + (size_t)b * 80 * 64, w1.partb1 + b * 64, ks, ch, lane, tid);
   DMLC_STAMP(DMLC_TK_DGRAD, 4);
 }
 
@@ -457,7 +455,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
   bf16* xin2 = reinterpret_cast<bf16*>(smem + C12_XIN2);
   bf16* cout2 = reinterpret_cast<bf16*>(smem + C12_OUT2);
   bf16* ws = reinterpret_cast<bf16*>(smem + C12_WS);
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15, cp = w & 1, pq = w >> 1;
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 

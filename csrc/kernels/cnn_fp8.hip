@@ -87,7 +87,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd_fp8(DmlcConv2FwdFp8Args a) 
   uint8_t* x8 = reinterpret_cast<uint8_t*>(smem);
   uint8_t* ws = x8 + X8_BYTES;
   bf16* cout = reinterpret_cast<bf16*>(ws + 2 * W8_SLICE);
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15, cp = w & 1, pg = w >> 1;
   const int slot = a.counter ? (int)(*a.counter & 1) : 0;
   const float sx = 448.f / fmaxf(a.amax_x[slot], 1e-20f), sw = a.scale_w[slot];

@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
   DMLC_STAMP(DMLC_TK_GEMM, 0);
   if (P.c_mode == 3) { colsum_block(P, local, reinterpret_cast<float*>(smem)); return; }
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15;
   const int per_split = P.tiles_m * P.tiles_n;
   const int split = local / per_split, t = local - split * per_split;

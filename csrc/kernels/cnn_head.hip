@@ -53,7 +53,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
   bf16* dh2s = reinterpret_cast<bf16*>(smem + L::DH2);
   bf16* dls = reinterpret_cast<bf16*>(smem + L::DL);
   float (*lg)[17] = reinterpret_cast<float (*)[17]>(smem + L::LG);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int r0 = blockIdx.x * RB;
   const bool rv = li < RB;                      // this lane's row column is a real batch row

@@ -30,6 +30,10 @@ DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 
 DEV f32x4 zero4() { f32x4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
 
+// the wave's index in its workgroup as a wave-uniform (SGPR) value: the compiler cannot prove
+// threadIdx.x >> 6 uniform, and everything derived from it would otherwise be VALU work
+DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of row q, columns 4p..4p+3
 // of a 4x16 block of 16-bit elements; lane i of the group receives column i (row q in element q).
 // Two reads (rows kb..kb+3 and kb+4..kb+7) give the 8-element MFMA fragment of one column.

@@ -131,7 +131,7 @@ DEV bf16x8 to_bf16x8(const float (&v)[8]) {
 
 // Reduce per-thread channel sums (thread's chunk = tid & 7) over the workgroup: red[waves][64] partials.
 DEV void block_chunk_sum(float (&v)[8], float* red /*[waves][64]*/, int tid) {
-  const int lane = tid & 63, w = tid >> 6;
+  const int lane = tid & 63, w = wave_id();
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float s = v[j];

@@ -210,7 +210,7 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
   bf16* xs = reinterpret_cast<bf16*>(smem);
   float* red = reinterpret_cast<float*>(smem + F::XB);          // [4][2][64]
   float* cf = red + 4 * 2 * 64;                                  // [2][64] BN scale / shift of layer l-1
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15;
 
   // ---- prologue: padded input image (stem: dataset gather; else BN-apply of layer l-1) ----
   if constexpr (CIN == 3) {
@@ -342,7 +342,7 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
   bf16* gs = reinterpret_cast<bf16*>(smem);
   float* red = reinterpret_cast<float*>(smem + D::GB);           // [4][2][64]
   float* cf = red + 4 * 2 * 64;                                   // [5][64]: A, Bc, Cc (layer l); mean, rstd (l-1)
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15;
 
   if (tid < COUT) {
     float A, Bc, Cc;
@@ -497,7 +497,7 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
   bf16* xs = reinterpret_cast<bf16*>(smem);                       // [NB][XE]
   bf16* gz = xs + NB * G::XE;                                     // [NB][GE]
   float* cf = reinterpret_cast<float*>(gz + NB * G::GE);          // [3][64]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int b0 = grp * a.B / a.G, b1 = (grp + 1) * a.B / a.G;
 
   if (tid < COUT) {
@@ -650,7 +650,7 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   __shared__ float pool_part[4][64];
   __shared__ float pooled[64], dlog[16], gpool[64], cf[2][64];
   __shared__ float redl[2][4][64];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int c = lane;                           // thread -> channel c, pixels w, w+4, ... (16 each)
   if (tid < 64) {
     float mean, rstd;

@@ -4,8 +4,9 @@
 // /root/reference/cifar10cnn.py:107 via the autodiff of :163).
 //
 //   dW1[k''][co] = sum_px X[px][k''] dY1[px][co],  k'' = kh*16 + kw*3 + ci  (k'' % 16 == 15 unused)
-//  * dY1 (the conv1 output gradient) is produced in LDS by the TF-SAME pool1 backward in "2x2
-//    ownership" form from the pool1 gradient + argmax bytes (conv_common.h pool_bwd_2x2);
+//  * dY1 (the conv1 output gradient) is produced in LDS by the TF-SAME pool1 backward, scattered
+//    from the pool1 gradient + argmax bytes in 4 deterministic phases (w1_pool_bwd);
+//  * the bias gradient comes out of the same MFMAs (a ones plane in the unused K'' row 15);
 //  * X is kept as 15 channel-planar, column-shifted copies of the padded 28x24 crop (plane kw*3+ci =
 //    Xpad[ci][y][x+kw]) so a K'' tile of 16 is one kernel row (15 taps + 1 zero plane) and every B
 //    fragment is ONE aligned ds_read_b128 of 8 consecutive pixels;
@@ -16,16 +17,22 @@
 
 namespace dmlc {
 
-constexpr int W1_DY_LD = 72;                  // dY1 LDS row stride (bf16): 144 B, tr reads conflict-free
+// dY1 LDS row stride (bf16): 128 B, one dword bank per channel pair whatever the pixel -- the
+// scatter's random-row writes are conflict-free; the MFMA's tr reads of it are 4-way (fewer bytes)
+constexpr int W1_DY_LD = 64;
 constexpr int W1_PL = 28 * 24 + 8;            // shifted-plane stride (bf16): 1360 B, b128 reads conflict-free
 constexpr int W1_DYT = 576 * W1_DY_LD;        // bf16 elements
 constexpr int W1_XS = 16 * W1_PL;
 constexpr int W1T = 512;                      // 8 waves (2 per SIMD) for the VALU-heavy gather phases
-constexpr int W1_FL_BYTES = 4 * 20 * 64 * 16; // cross-wave reduction buffer (f32x4 per lane per tile)
+constexpr int W1_FL_BYTES = 4 * 10 * 64 * 16; // cross-wave reduction buffer (f32x4 per lane per tile, 2 rounds)
 
-// plane 15 (the zero K'' row of every kernel-row tile)
-DEV void w1_zero_plane15(bf16* xs, int tid) {
-  for (int e = tid; e < W1_PL / 8; e += W1T) *reinterpret_cast<bf16x8*>(xs + 15 * W1_PL + e * 8) = bf16x8{};
+// plane 15 (the unused K'' row of every kernel-row tile) holds ONES: row 15 of each kernel-row
+// tile of the MFMA product is then sum_px dY1[px][co], the conv1 bias gradient, for free
+DEV void w1_ones_plane15(bf16* xs, int tid) {
+  bf16x8 one;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) one[j] = (bf16)1.0f;
+  for (int e = tid; e < W1_PL / 8; e += W1T) *reinterpret_cast<bf16x8*>(xs + 15 * W1_PL + e * 8) = one;
 }
 
 // (a) shifted channel planes straight from the uint8 image in LDS: task (yy, x8, kw) -> planes
@@ -51,68 +58,113 @@ DEV void w1_planes(bf16* xs, const uint8_t* img, int cy, int cx, int tid) {
   }
 }
 
-// (b) pool1 / ReLU backward -> dY1 (bf16, LDS) + bias-grad sums (fp32).  dps: pool1 gradient, LDS
-//     [144][64] bf16 unswizzled; ams: argmax bytes [144][64].
-DEV void w1_pool_bwd(bf16* dyt, const bf16* dps, const uint8_t* ams, float (&bsum)[8], int tid) {
-  for (int task = tid; task < 144 * 8; task += W1T) {
-    const int win = task >> 3, c = task & 7, py = win / 12, px = win - py * 12;
-    float o[4][8];
-    pool_bwd_2x2<12>(dps, ams, py, px, c, o);
+// (b) pool1 / ReLU backward -> dY1 (bf16, LDS) as a SCATTER: every pool1 window adds its gradient
+//     to its argmax pixel (read-modify-write into a zeroed tile) instead of every pixel gathering from
+//     the up-to-4 windows that may have picked it (~10 VALU per output element).  One instruction
+//     covers the 64 channels of one window (lanes 0-31: even channels, 32-63: odd), so with 128-B
+//     dY1 rows its 32-lane groups hit 32 distinct banks whatever pixels the argmaxes pick (a lane per
+//     window instead measured 55 % of the LDS cycles in bank conflicts).  Windows whose (py, px)
+//     parities agree never overlap: the 4 parity classes run as 4 barrier-separated phases (36
+//     windows each, window l -> wave l % 8), so no two adds of one phase hit the same element and an
+//     element that receives several gradients receives them in the fixed phase order --
+//     deterministic.  The first add into an element is exact (0 + bf16), the second is one rounding,
+//     like the rounding of an fp32 sum.  (LDS bf16 atomics instead: 2x slower.)
+DEV int w1_class_window(int ph, int l) {      // pool1 window (py * 12 + px) of class ph, index l < 36
+  const int r = l / 6;
+  return (2 * r + (ph >> 1)) * 12 + 2 * (l - r * 6) + (ph & 1);
+}
+
+DEV void w1_zero_dy(bf16* dyt, int tid) {
+  for (int e = tid; e < W1_DYT / 8; e += W1T) *reinterpret_cast<bf16x8*>(dyt + e * 8) = bf16x8{};
+}
+
+// dps: pool1 gradient [144][64] bf16, ams: argmax bytes [144][64] (255 = no gradient), both in LDS.
+// Call after w1_zero_dy + a barrier; ends with a barrier (dY1 complete).
+DEV void w1_pool_bwd(bf16* dyt, const bf16* dps, const uint8_t* ams, int w, int lane) {
+  // (d / 3) * 24 + d % 3 for the in-window position d = 3 dy + dx, 6 bits per entry; code 255 reads
+  // bits 58.. (shift taken mod 64): offset 0, and adds 0 to the window's own corner element
+  constexpr uint64_t kOff = 0ull | 1ull << 6 | 2ull << 12 | 24ull << 18 | 25ull << 24 | 26ull << 30 | 48ull << 36 |
+                            49ull << 42 | 50ull << 48;
+  const int ch = 2 * (lane & 31) + (lane >> 5);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
-      *reinterpret_cast<bf16x8*>(dyt + (y * 24 + x) * W1_DY_LD + c * 8) = to_bf16x8(o[k]);
+  for (int ph = 0; ph < 4; ++ph) {
+    // straight-line reads for all 5 items (the 5th exists for waves 0-3 only; the others read
+    // window 35 again and write nothing), so their LDS latencies overlap
+    int addr[5];
+    float add[5], old[5];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) bsum[j] += o[k][j];
+    for (int k = 0; k < 5; ++k) {            // windows w, w + 8, ... (< 36) of this class
+      const int l = min(w + 8 * k, 35);
+      const int win = w1_class_window(ph, l), py = win / 12, px = win - py * 12;
+      const uint32_t code = ams[win * 64 + ch];
+      const float f = (float)dps[win * 64 + ch];
+      addr[k] = ((py * 48 + 2 * px) + (int)((kOff >> ((6 * code) & 63u)) & 63u)) * W1_DY_LD + ch;
+      add[k] = code < 9 ? f : 0.f;
     }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) old[k] = (float)dyt[addr[k]];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dyt[addr[k]] = (bf16)(old[k] + add[k]);
+    if (w < 4) dyt[addr[4]] = (bf16)(old[4] + add[4]);
+    lds_barrier();
   }
 }
 
 // (c) MFMA over one image: this wave's k-steps s = ks, ks+4, ... of the 18 (32 pixels each), co
-//     tiles 2ch, 2ch+1, kernel rows t = 0..4 (16 K'' each)
+//     tiles 2ch, 2ch+1, kernel rows t = 0..4 (16 K'' each).  Software-pipelined: the next k-step's
+//     7 fragments are read under this k-step's 10 MFMAs (two waves per SIMD do not hide an LDS
+//     latency per k-step).
 DEV void w1_mfma(const bf16* dyt, const bf16* xs, f32x4 (&acc)[2][5], int ks, int ch, int g, int li) {
   const int q = li >> 2, p = li & 3;
-  for (int s = ks; s < 18; s += 4) {
+  auto frags = [&](int s, bf16x8 (&af)[2], bf16x8 (&bx)[5]) {
     const int rA = 32 * s + 8 * g + q, rB = rA + 4;
-    bf16x8 af[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int ct = 2 * ch + h;
       af[h] = tr_frag(dyt + rA * W1_DY_LD + 16 * ct + 4 * p, dyt + rB * W1_DY_LD + 16 * ct + 4 * p);
     }
-    const int r0 = 32 * s + 8 * g, y = r0 / 24, x0 = r0 - y * 24;
+    const bf16* xp = xs + li * W1_PL + 32 * s + 8 * g;   // pixel row y, column x0: y * 24 + x0 = 32 s + 8 g
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-      const bf16x8 bx = lds_b128(xs + li * W1_PL + (y + t) * 24 + x0);
+    for (int t = 0; t < 5; ++t) bx[t] = lds_b128(xp + t * 24);
+  };
+  bf16x8 af[2], bx[5];
+  frags(ks, af, bx);
+  for (int s = ks; s < 18; s += 4) {
+    bf16x8 an[2], bn[5];
+    wait_lds();                                // this k-step's fragments have landed
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 4 < 18) frags(s + 4, an, bn);      // uniform per wave
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) acc[h][t] = mfma16(af[h], bx, acc[h][t]);
-    }
+    for (int t = 0; t < 5; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) acc[h][t] = mfma16(af[h], bx[t], acc[h][t]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) af[h] = an[h];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) bx[t] = bn[t];
   }
 }
 
-// Cross-wave reduction (fixed order) through `fl` (W1_FL_BYTES of LDS no longer read by anyone),
-// then the fp32 slab out[80 k''][64 co] and the bias-grad row outb[64].  Call after a barrier that
-// retired every wave's MFMA reads of the region; red: LDS [8][64] floats.
-DEV void w1_flush(char* fl_mem, float* red, const f32x4 (&acc)[2][5], float (&bsum)[8], float* out, float* outb,
-                  int ks, int ch, int lane, int tid) {
+// Cross-wave reduction (fixed order) through `fl` (W1_FL_BYTES of LDS no longer read by anyone), one
+// co-tile half per round, then the fp32 slab out[80 k''][64 co] and the bias-grad row outb[64]
+// (= row 15, the ones plane).  Call after a barrier that retired every wave's MFMA reads of the region.
+DEV void w1_flush(char* fl_mem, const f32x4 (&acc)[2][5], float* out, float* outb, int ks, int ch, int lane,
+                  int tid) {
   f32x4* fl = reinterpret_cast<f32x4*>(fl_mem);
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < 2; ++h) {
+    if (h) lds_barrier();                      // round 0's reads are done
 #pragma unroll
-    for (int t = 0; t < 5; ++t) fl[(ks * 20 + (2 * ch + h) * 5 + t) * 64 + lane] = acc[h][t];
-  block_chunk_sum(bsum, red, tid);
-  __syncthreads();
-  for (int e = tid; e < 20 * 64; e += W1T) {
-    const f32x4 s = ((fl[e] + fl[1280 + e]) + (fl[2560 + e] + fl[3840 + e]));
-    const int tile = e >> 6, ln = e & 63, ct = tile / 5, t = tile - ct * 5;
-    const int co = 16 * ct + 4 * (ln >> 4), kk = 16 * t + (ln & 15);
-    *reinterpret_cast<f32x4*>(out + kk * 64 + co) = s;
-  }
-  if (tid < 64) {
-    float sb = 0.f;
-#pragma unroll
-    for (int k = 0; k < W1T / 64; ++k) sb += red[k * 64 + tid];
-    outb[tid] = sb;
+    for (int t = 0; t < 5; ++t) fl[(ks * 10 + ch * 5 + t) * 64 + lane] = acc[h][t];
+    lds_barrier();
+    for (int e = tid; e < 10 * 64; e += W1T) {
+      const f32x4 s = ((fl[e] + fl[640 + e]) + (fl[1280 + e] + fl[1920 + e]));
+      const int tile = e >> 6, ln = e & 63, cp = tile / 5, t = tile - cp * 5;
+      const int co = 16 * (2 * cp + h) + 4 * (ln >> 4), kk = 16 * t + (ln & 15);
+      *reinterpret_cast<f32x4*>(out + kk * 64 + co) = s;
+      if (kk == 15) *reinterpret_cast<f32x4*>(outb + co) = s;
+    }
   }
 }
 

@@ -158,34 +158,27 @@ class FusedCifarEngine:
         # merged wgrad ~26 us -- equal, and the SGD pays for 256 per-image slabs: off by default.
         self.fused_w1 = self.merged_wgrad and os.environ.get("DMLC_FUSED_W1", "0") == "1"
         self.keep_dp1 = False          # tests: also write the pool1 gradient to global memory
+        # conv2 weight gradient: one block per (input-channel quarter, image group), one fp32 slab per
+        # group (self.g2 = groups = slabs the SGD kernel reduces); conv1: one block per image group.
+        # DMLC_W2_GROUPS / DMLC_W1_GROUPS override the defaults (kbench sweeps).
+        env_g2 = int(os.environ.get("DMLC_W2_GROUPS", "0")) or None
+        env_g1 = int(os.environ.get("DMLC_W1_GROUPS", "0")) or None
+        g2 = g2 or env_g2
+        g1 = g1 or env_g1
         if self.fused_w1:
-            # conv2 wgrad: one 8-wave block per (kh, pair of image groups); the whole chip is its
-            # own, so more pairs than with conv1 alongside (DMLC_W2_PAIRS overrides; more slabs cost
-            # the SGD kernel 410 KB of fp32 reads each)
-            if g2:
-                pairs = (g2 + 1) // 2
-            else:
-                pairs = int(os.environ.get("DMLC_W2_PAIRS", "0")) or max(1, min(B // 2, 51, round(B * 40 / 256)))
-            self.groups2 = g2 or 2 * pairs
-            self.g2 = pairs
-            self.g1 = B                                  # conv1: one slab per image
+            # conv1 runs inside the conv2-dgrad launch (one slab per image): the conv2 weight
+            # gradient has the whole chip
+            self.g2 = g2 or max(1, min(B, 64, round(B / 4)))
+            self.g1 = B
         elif self.merged_wgrad:
-            # conv2: pairs of ~4.6-image groups (one 8-wave block per (kh, pair), one slab per pair);
-            # conv1: exactly the CUs the conv2 blocks leave while that is >= B/4 blocks (one wave of
-            # workgroups; 5*pairs + g1 > 256 costs ~10 us).  B=256: 28 pairs + g1=116 -> 24.0 us vs
-            # 24.9 (25 + 131) and 34-35 (28 + 128), profiles/r1_v15_kbench_wgrad_sweep.txt
-            if g2 is None:
-                pairs = max(1, min(B // 2, round(B * 7 / 64) if B <= 256 else round(B / 10.24)))
-            else:
-                pairs = (g2 + 1) // 2
-            self.groups2 = g2 or 2 * pairs
-            self.g2 = pairs                              # slabs the SGD kernel reduces
-            left = 256 - 5 * pairs
+            # both in one launch of g1 + 4 * g2 <= 256 blocks (one wave of workgroups)
+            self.g2 = g2 or max(1, min(B, 40, round(B * 40 / 256)))
+            left = 256 - 4 * self.g2
             self.g1 = g1 or max(1, min(B, left if left >= B // 4 else B // 2))
         else:
-            self.g2 = g2 or max(1, min(B, B // 6))      # conv2 wgrad: 5 kh blocks x ~6 images per group
-            self.groups2 = self.g2
+            self.g2 = g2 or max(1, min(B, B // 6))      # conv2 wgrad: 4 ci-quarter blocks x ~6 images per group
             self.g1 = g1 or max(1, min(B, B // 2))      # conv1 wgrad: 2 images per block
+        self.groups2 = self.g2
         self.p1, self.am1 = z(B, 12, 12, 64), z(B, 12, 12, 64, dt=torch.uint8)
         self.p2, self.am2 = z(B, 6, 6, 64), z(B, 6, 6, 64, dt=torch.uint8)
         self.h1part = z(self.fc1_split, B, 384, dt=torch.float32)

@@ -22,7 +22,7 @@ for s in $STEPS; do
     rnprof) rm -rf gpurun_out/rnprof; timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/rnprof -o run -- python3 bench.py --model resnet20 --steps 30 --warmup 5 > gpurun_out/rnprof.log 2>&1; ok $? rnprof ;;
     lat) timeout -k 10 200 python tools/launch_latency.py > gpurun_out/launch_latency.json 2> gpurun_out/launch_latency.err; ok $? lat ;;
     cnn) timeout -k 10 400 python -u -m pytest tests/test_cnn_kernels_gpu.py tests/test_fused_gpu.py -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_cnn.log 2>&1; ok $? cnn ;;
-    kbench) timeout -k 10 200 python tools/kbench.py > gpurun_out/kbench.json 2> gpurun_out/kbench.err; ok $? kbench ;;
+    kbench) timeout -k 10 200 python tools/kbench.py ${KBENCH_ARGS:-} > gpurun_out/kbench.json 2> gpurun_out/kbench.err; ok $? kbench ;;
     ktiming) DMLC_TIMING=1 timeout -k 10 200 python tools/ktiming.py > gpurun_out/ktiming.json 2> gpurun_out/ktiming.err; ok $? ktiming ;;
     rn) timeout -k 10 300 python bench.py --model resnet20 --steps 100 --warmup 10 > gpurun_out/bench_rn.log 2>&1; ok $? rn ;;
     eager) timeout -k 10 300 python bench.py --impl eager --steps 50 --warmup 5 > gpurun_out/bench_eager.log 2>&1; ok $? eager ;;

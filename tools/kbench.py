@@ -2,6 +2,7 @@
 """Per-kernel timing of the fused CIFAR CNN step (each launch repeated back to back, HIP events).
 
   python tools/kbench.py [--batch 256] [--iters 200] [--g1 N] [--g2 N] [--fc1-split N]
+                         [--wgrad-sweep G1:G2,G1:G2,...]
 Prints one JSON line per kernel with the mean µs per launch, plus the whole eager step and the
 graph-replayed step, so kernel changes can be A/B'd on the GPU box without rocprof.
 """
@@ -38,6 +39,8 @@ def main():
     ap.add_argument("--g1", type=int, default=None)
     ap.add_argument("--g2", type=int, default=None)
     ap.add_argument("--fc1-split", type=int, default=None)
+    ap.add_argument("--wgrad-sweep", default="", help="merged weight-gradient launch at other (g1, g2) "
+                    "splits, plus each body alone on g1 / 4*g2 workgroups")
     a = ap.parse_args()
     g = torch.Generator().manual_seed(0)
     data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
@@ -76,6 +79,15 @@ def main():
                                                  eng.dp1, eng.am1, eng.part1, eng.partb1, eng.p1, eng.dy2,
                                                  eng.part2, eng.partb2, eng.groups2, eng.xraw,
                                                  not eng.fused_w1), a.iters)
+    for pair in filter(None, a.wgrad_sweep.split(",")):
+        g1, g2 = (int(v) for v in pair.split(":"))
+        z = lambda *sh: torch.zeros(*sh, device=eng.device, dtype=torch.float32)
+        p1, pb1, p2, pb2 = z(g1, 80, 64), z(g1, 64), z(g2, 1600, 64), z(g2, 64)
+        res[f"wgrad_{g1}_{g2}"] = timeit(lambda: o.wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx, eng.dp1, eng.am1,
+                                                         p1, pb1, eng.p1, eng.dy2, p2, pb2, g2, eng.xraw, True), a.iters)
+        res[f"conv1_wgrad_{g1}"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx, eng.dp1,
+                                                                eng.am1, p1, pb1, eng.xraw), a.iters)
+        res[f"conv2_wgrad_{g2}"] = timeit(lambda: o.conv2_wgrad(eng.p1, eng.dy2, p2, pb2), a.iters)
     res["conv_bwd"] = timeit(eng._conv_backward, a.iters)
     res["sgd_reduce_only"] = timeit(lambda: eng._sgd(mode=1), a.iters)
     res["sgd_full"] = timeit(lambda: eng._sgd(mode=0), a.iters)
@@ -83,7 +95,7 @@ def main():
     eng.capture()
     res["step_graph"] = timeit(lambda: eng.graphs[0].replay(), a.iters)
     res["sum_kernels"] = sum(v for k, v in res.items()
-                             if not k.startswith("step") and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad",
+                             if not k.startswith(("step", "wgrad_", "conv1_wgrad_", "conv2_wgrad_")) and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad",
                                                                    "conv2_dgrad" if eng.fused_w1 else "conv2_dgrad_w1")
                              and k not in (("conv1_fwd", "conv2_fwd") if eng.fused_fwd else ("conv12_fwd",)))
     cfg = dict(batch=a.batch, g1=eng.g1, g2=eng.g2, fc1_split=eng.fc1_split)
