@@ -32,7 +32,10 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15;
   const int ch = w & 1, ks = w >> 1;                     // MFMA: co tiles 2ch, 2ch+1; k-steps ks mod 4
-  const int b0 = grp * a.B / a.g1, b1 = (grp + 1) * a.B / a.g1;
+  // image group grp = images grp, grp + g1, ...: with g1 % 8 == 0 all of them were produced on this
+  // block's XCD (blockIdx % 8) by the forward / dgrad blocks of the same index (placement is a
+  // speed matter only)
+  const int G = a.g1, b0 = grp, last = grp < a.B ? grp + (a.B - 1 - grp) / G * G : grp;
   DMLC_STAMP(DMLC_TK_W1, 0);
 
   w1_ones_plane15(xs, tid);
@@ -46,7 +49,6 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
   // Every load below is unconditional (image indices clamped to the block's last image, surplus
   // threads duplicating chunks): see PrefetchAll.  The dataset row of image b+1 is read one image
   // ahead of its pixels, so no index -> pixels dependency is exposed inside the loop.
-  const int last = b1 > b0 ? b1 - 1 : b0;
   // Per thread: 1 chunk of the whole uint8 image (3072 B = 192 chunks, 16-B aligned dataset rows),
   // 3 of the pool1 gradient (1152), 2 of the argmax bytes (576).  Named registers, not member
   // arrays: with the arrays in a struct hipcc kept them in scratch.
@@ -62,9 +64,9 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
   };
   // with the forward's image copy (xraw) no dataset index is needed at all
   auto row_index = [&](int bb) { return a.xraw ? 0 : batch_index(a.src, a.B, bb); };
-  load(row_index(b0 < last ? b0 : last), b0);
-  int nidx = row_index(b0 + 1 < last ? b0 + 1 : last);
-  for (int b = b0; b < b1; ++b) {
+  load(row_index(b0 < last ? b0 : last), b0 < last ? b0 : last);
+  int nidx = row_index(b0 + G < last ? b0 + G : last);
+  for (int b = b0; b < a.B; b += G) {
     lds_barrier();                             // previous image's MFMA reads are done
     reinterpret_cast<uint4*>(img)[cI] = vI;
     reinterpret_cast<uint4*>(dps)[tid] = vD0;
@@ -73,15 +75,15 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
     reinterpret_cast<uint4*>(ams)[tid] = vA0;
     reinterpret_cast<uint4*>(ams)[cA1] = vA1;
     w1_zero_dy(dyt, tid);
-    load(nidx, b + 1 < last ? b + 1 : last);   // prefetch the next image while this one computes
-    nidx = row_index(b + 2 < last ? b + 2 : last);
+    load(nidx, b + G < last ? b + G : last);   // prefetch the next image while this one computes
+    nidx = row_index(b + 2 * G < last ? b + 2 * G : last);
     lds_barrier();
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 1);
-    if (b == b0 + 1) DMLC_STAMP(DMLC_TK_W1, 6);
+    if (b == b0 + G) DMLC_STAMP(DMLC_TK_W1, 6);
     w1_planes(xs, img, a.cy, a.cx, tid);
     w1_pool_bwd(dyt, dps, ams, w, lane);       // ends with a barrier: dY1 and the planes complete
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 2);
-    if (b == b0 + 1) DMLC_STAMP(DMLC_TK_W1, 7);
+    if (b == b0 + G) DMLC_STAMP(DMLC_TK_W1, 7);
     w1_mfma(dyt, xs, acc, ks, ch, g, li);
     if (b == b0) DMLC_STAMP(DMLC_TK_W1, 5);
   }
@@ -98,7 +100,10 @@ __global__ __launch_bounds__(W1T, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 constexpr int W2T = 512;
-constexpr int W2_LD = 72;                      // dY rows: 144 B, tr reads of rows r / r+4 on other banks
+// dY rows: 128 B with the 16-column tiles XOR-swizzled by row bits 1 and 3 -- the tr reads of rows
+// {r..r+3, r+8..r+11} land on 8 distinct bank windows (a 144-B row stride left them 2-way)
+constexpr int W2_LD = 64;
+DEV int w2_dy_col(int row, int col) { return col ^ (16 * (((row >> 1) & 1) | ((row >> 2) & 2))); }
 constexpr int W2_DY = 160 * W2_LD;             // 144 pixels + 16 zero rows
 constexpr int W2_LDX = 16;                     // conv2 input: 16 channels per padded pixel, 32-B rows
 constexpr int W2_XT = 256 * W2_LDX;            // the padded 16x16 image (halo 2)
@@ -107,15 +112,20 @@ constexpr size_t W2_LDS_MAIN = (size_t)(W2_XT + W2_DY) * 2;
 constexpr size_t W2_LDS_ST = (size_t)(W2T / 64) * 16 * W2_ST * 4;
 constexpr size_t W2_LDS = W2_LDS_MAIN > W2_LDS_ST ? W2_LDS_MAIN : W2_LDS_ST;
 
-// block blk = c4 + 4 * group: input channels 16*c4 .. 16*c4+15 of image group `group`; fills rows
-// (tap, 16*c4 .. 16*c4+15) of slab `group` (the 4 blocks of a group write disjoint quarters)
-DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* smem) {
+// Block blk (base + blk = blockIdx.x) -> (c4, group): input channels 16*c4 .. 16*c4+15 of image group
+// `group` = images group, group + g2, ...; fills rows (tap, 16*c4 .. 16*c4+15) of slab `group` (the
+// 4 blocks of a group write disjoint quarters).  With g2 % 8 == 0 and base % 8 == 0 the 4 blocks of a
+// group sit on one XCD (blockIdx % 8), the one whose dgrad / forward blocks wrote the group's dY2 and
+// input (placement is a speed matter only).  (Double-buffering the image operands in LDS, with or
+// without reading k-step s+1's fragments under k-step s's MFMAs, measured 0.3-1 us slower.)
+DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int base, char* smem) {
   bf16* xt = reinterpret_cast<bf16*>(smem);
   bf16* dyt = xt + W2_XT;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const int c4 = blk & 3, grp = blk >> 2;
-  const int b0 = grp * a.B / a.g2, b1 = (grp + 1) * a.B / a.g2;
+  const bool xcd = a.g2 % 8 == 0 && base % 8 == 0;
+  const int c4 = xcd ? (blk >> 3) & 3 : blk & 3, grp = xcd ? (blk & 7) + 8 * (blk >> 5) : blk >> 2;
+  const int G = a.g2, b0 = grp, last = grp < a.B ? grp + (a.B - 1 - grp) / G * G : grp;
   DMLC_STAMP(DMLC_TK_W2, 0);
 
   // zero the whole padded input once (the interior is overwritten per image) and the 16 pad dY rows
@@ -134,7 +144,6 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* sme
   bf16* xdst = xt + ((xy + 2) * 16 + pxl - xy * 12 + 2) * W2_LDX + 8 * (kx & 1);
   const int kd[3] = {tid, tid + 512, 1024 + (tid & 127)};
   uint4 vx, vd[3];
-  const int last = b1 > b0 ? b1 - 1 : b0;
   auto load = [&](int b) {
     const uint4* x = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.p1) + (size_t)b * 9216);
     const uint4* d = reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.dy2) + (size_t)b * 9216);
@@ -158,20 +167,20 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* sme
   constexpr int T24 = (4 * 16 + 4) * W2_LDX;
 
   load(b0 < last ? b0 : last);
-  for (int b = b0; b < b1; ++b) {
+  for (int b = b0; b < a.B; b += G) {
     lds_barrier();                             // previous image's MFMA reads are done
     *reinterpret_cast<uint4*>(xdst) = vx;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       const int k = kd[i];
-      *reinterpret_cast<uint4*>(dyt + (k >> 3) * W2_LD + (k & 7) * 8) = vd[i];
+      *reinterpret_cast<uint4*>(dyt + (k >> 3) * W2_LD + w2_dy_col(k >> 3, (k & 7) * 8)) = vd[i];
       if (c4 == 0 && (i < 2 || tid < 128)) {   // chunk k & 7 == tid & 7: channels 8c..8c+7
         const uint32_t d4[4] = {vd[i].x, vd[i].y, vd[i].z, vd[i].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) { bsum[2 * j] += bf16_lo(d4[j]); bsum[2 * j + 1] += bf16_hi(d4[j]); }
       }
     }
-    load(b + 1 < last ? b + 1 : last);
+    load(b + G < last ? b + G : last);
     lds_barrier();
     if (b == b0) DMLC_STAMP(DMLC_TK_W2, 1);
 #pragma unroll
@@ -180,7 +189,7 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* sme
       bf16x8 bf[4];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
-        bf[ct] = tr_frag(dyt + rA * W2_LD + 16 * ct + 4 * p, dyt + rB * W2_LD + 16 * ct + 4 * p);
+        bf[ct] = tr_frag(dyt + rA * W2_LD + w2_dy_col(rA, 16 * ct + 4 * p), dyt + rB * W2_LD + w2_dy_col(rB, 16 * ct + 4 * p));
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
         const bf16x8 af = tr_frag(xt + xa[s] + toff[j], xt + xb[s] + toff[j]);
@@ -237,7 +246,7 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, char* sme
 
 __global__ __launch_bounds__(W2T, 1) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv2_wgrad_block(a, blockIdx.x, smem);
+  conv2_wgrad_block(a, blockIdx.x, 0, smem);
 }
 
 // Both weight gradients in ONE launch (no stream fork/join in the step graph): blocks [0, g1) run
@@ -247,7 +256,7 @@ constexpr size_t WG_LDS = W1_LDS > W2_LDS ? W1_LDS : W2_LDS;
 __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if ((int)blockIdx.x < a.w1.g1) conv1_wgrad_block(a.w1, blockIdx.x, smem);
-  else conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, smem);
+  else conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, smem);
 }
 static_assert(W1T == W2T, "k_wgrad runs both bodies with one block size");
 

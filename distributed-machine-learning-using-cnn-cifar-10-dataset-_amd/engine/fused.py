@@ -171,8 +171,11 @@ class FusedCifarEngine:
             self.g2 = g2 or max(1, min(B, 64, round(B / 4)))
             self.g1 = B
         elif self.merged_wgrad:
-            # both in one launch of g1 + 4 * g2 <= 256 blocks (one wave of workgroups)
-            self.g2 = g2 or max(1, min(B, 40, round(B * 40 / 256)))
+            # both in one launch of g1 + 4 * g2 <= 256 blocks (one wave of workgroups); multiples of 8
+            # keep every group's images on one XCD (cnn_wgrad.hip).  B=256: 128 + 4*32 -> 19.1 us vs
+            # 96 + 4*40 -> 19.8, 64 + 4*48 -> 23.4 (r2, register-staged conv1 scatter)
+            g2_ = max(1, min(B, 32, B // 8))
+            self.g2 = g2 or (g2_ // 8 * 8 if g2_ >= 8 else g2_)
             left = 256 - 4 * self.g2
             self.g1 = g1 or max(1, min(B, left if left >= B // 4 else B // 2))
         else:

@@ -8,6 +8,7 @@ graph-replayed step, so kernel changes can be A/B'd on the GPU box without rocpr
 """
 import argparse
 import json
+import re
 import os
 import sys
 
@@ -95,7 +96,8 @@ def main():
     eng.capture()
     res["step_graph"] = timeit(lambda: eng.graphs[0].replay(), a.iters)
     res["sum_kernels"] = sum(v for k, v in res.items()
-                             if not k.startswith(("step", "wgrad_", "conv1_wgrad_", "conv2_wgrad_")) and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad",
+                             if not k.startswith("step") and not re.match(r"(wgrad|conv1_wgrad|conv2_wgrad)_\d", k)
+                             and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad",
                                                                    "conv2_dgrad" if eng.fused_w1 else "conv2_dgrad_w1")
                              and k not in (("conv1_fwd", "conv2_fwd") if eng.fused_fwd else ("conv12_fwd",)))
     cfg = dict(batch=a.batch, g1=eng.g1, g2=eng.g2, fc1_split=eng.fc1_split)
