@@ -11,23 +11,26 @@
 #define DMLC_XGMI_MAX_RANKS 8
 #define DMLC_XGMI_MAX_BLOCKS 128
 #define DMLC_XGMI_HANDLE_BYTES 64   // sizeof(hipIpcMemHandle_t)
+#define DMLC_XGMI_HANDLES 3         // per rank: data buffer, signal block, bf16 wire buffer
 
 extern "C" {
 
-// Create the context: allocate `numel` fp32 elements (zeroed) + the signal block.
+// Create the context: allocate `numel` fp32 elements (zeroed), a bf16 wire buffer of `numel` and the
+// signal block.
 // Returns a context id >= 0, or -1 (error string via dmlc_xgmi_last_error()).
 int dmlc_xgmi_create(int rank, int world, int64_t numel);
 float* dmlc_xgmi_buffer(int ctx);
 int64_t dmlc_xgmi_numel(int ctx);
-// 2 * DMLC_XGMI_HANDLE_BYTES bytes: IPC handle of the data buffer, then of the signal block.
+// DMLC_XGMI_HANDLES * DMLC_XGMI_HANDLE_BYTES bytes: IPC handles of the data buffer, the signal block
+// and the wire buffer.
 int dmlc_xgmi_handles(int ctx, uint8_t* out);
-// all_handles: world * 2 * DMLC_XGMI_HANDLE_BYTES bytes in rank order (own entry ignored).
+// all_handles: world * DMLC_XGMI_HANDLES * DMLC_XGMI_HANDLE_BYTES bytes in rank order (own entry ignored).
 int dmlc_xgmi_open(int ctx, const uint8_t* all_handles);
 // Sum-all-reduce elements [offset, offset + numel) of the buffer across the ranks, in place.
 // offset and numel must be multiples of 4 (16-byte vectors).  Deterministic: element i's sum is
 // computed by one owner rank in fixed rank order and pushed to every peer, so replicas stay
-// bit-identical.
-hipError_t dmlc_xgmi_allreduce(int ctx, int64_t offset, int64_t numel, int blocks, hipStream_t s);
+// bit-identical.  bf16_wire: the values cross the links as bf16 (sums in fp32, result bf16-rounded).
+hipError_t dmlc_xgmi_allreduce(int ctx, int64_t offset, int64_t numel, int blocks, int bf16_wire, hipStream_t s);
 // Sticky error word of the context (device memory): bit 0 = a barrier timed out.
 int dmlc_xgmi_error(int ctx);
 void dmlc_xgmi_destroy(int ctx);

@@ -13,6 +13,10 @@
 //   * two cross-GPU barriers per launch (data ready / pushes landed), one flag slot per
 //     (workgroup, peer) in uncached device memory; epochs are per-workgroup counters in device
 //     memory, so the launch is graph-capturable and replays need no host involvement;
+//   * optional bf16 wire format: each rank first packs its fp32 bucket into a bf16 wire buffer
+//     (also peer-mapped), the owners read bf16, sum in fp32 in rank order and push bf16(sum); every
+//     rank then unpacks the whole bucket from its own wire buffer -- half the link bytes, and every
+//     replica ends with the same bf16-rounded sums (the semantics of an all-reduce of bf16 tensors);
 //   * every spin is bounded (s_memrealtime deadline): a missing peer sets a sticky error word and
 //     the kernel drains instead of hanging the GPU.  The word is mirrored into mapped pinned host
 //     memory, so the training loop polls it with a plain load (no HIP call, no sync) and exits for
@@ -41,6 +45,7 @@ struct XgmiSignal {
 
 struct XgmiArgs {
   float4* bufs[DMLC_XGMI_MAX_RANKS];
+  uint2* wires[DMLC_XGMI_MAX_RANKS];   // bf16 wire buffers (4 bf16 per float4 of the data buffer)
   XgmiSignal* sigs[DMLC_XGMI_MAX_RANKS];
   uint32_t* host_err; // mapped pinned host word (device pointer), or null
   int rank;
@@ -84,31 +89,51 @@ __device__ __forceinline__ void peer_barrier(const XgmiArgs& a, int which, uint3
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
-template <int W>
+__device__ __forceinline__ uint2 pack_bf16x4(float4 v) {
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
+  const b4 r = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+  return __builtin_bit_cast(uint2, r);
+}
+__device__ __forceinline__ float4 unpack_bf16x4(uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+template <int W, bool BF16>
 __global__ __launch_bounds__(XT) void k_xgmi_allreduce(XgmiArgs a) {
   XgmiSignal* self = a.sigs[a.rank];
   __shared__ uint32_t s_e;
   if (threadIdx.x == 0) s_e = ld_sys(&self->epoch[blockIdx.x]) + 1u;
   __syncthreads();
   const uint32_t e = s_e;
+  const int64_t stride = (int64_t)gridDim.x * XT, t0 = (int64_t)blockIdx.x * XT + threadIdx.x;
+  if (BF16)                            // my whole bucket -> my wire buffer (read by the owners)
+    for (int64_t i = a.off4 + t0; i < a.off4 + a.n4; i += stride) a.wires[a.rank][i] = pack_bf16x4(a.bufs[a.rank][i]);
 
   peer_barrier<W>(a, 0, e);            // every rank's gradients are complete
 
   // reduce-scatter of this rank's slice + push of the sums to every rank
   const int64_t lo = a.off4 + a.n4 * a.rank / W, hi = a.off4 + a.n4 * (a.rank + 1) / W;
-  const int64_t stride = (int64_t)gridDim.x * XT;
-  for (int64_t i = lo + (int64_t)blockIdx.x * XT + threadIdx.x; i < hi; i += stride) {
+  for (int64_t i = lo + t0; i < hi; i += stride) {
     float4 v[W];
 #pragma unroll
-    for (int p = 0; p < W; ++p) v[p] = a.bufs[p][i];
+    for (int p = 0; p < W; ++p) v[p] = BF16 ? unpack_bf16x4(a.wires[p][i]) : a.bufs[p][i];
     float4 s = v[0];
 #pragma unroll
     for (int p = 1; p < W; ++p) { s.x += v[p].x; s.y += v[p].y; s.z += v[p].z; s.w += v[p].w; }
+    if (BF16) {
+      const uint2 r = pack_bf16x4(s);
 #pragma unroll
-    for (int p = 0; p < W; ++p) a.bufs[(a.rank + p) % W][i] = s;   // staggered start: links evenly loaded
+      for (int p = 0; p < W; ++p) a.wires[(a.rank + p) % W][i] = r;   // staggered start: links evenly loaded
+    } else {
+#pragma unroll
+      for (int p = 0; p < W; ++p) a.bufs[(a.rank + p) % W][i] = s;
+    }
   }
 
   peer_barrier<W>(a, 1, e);            // every rank's pushes into my buffer landed
+  if (BF16)                            // every slice, mine included, from the bf16 sums
+    for (int64_t i = a.off4 + t0; i < a.off4 + a.n4; i += stride) a.bufs[a.rank][i] = unpack_bf16x4(a.wires[a.rank][i]);
   if (threadIdx.x == 0) st_sys(&self->epoch[blockIdx.x], e);
 }
 
@@ -117,10 +142,12 @@ struct XgmiCtx {
   int rank = 0, world = 1, device = 0;
   int64_t numel = 0;
   float* buf = nullptr;
+  uint16_t* wire = nullptr;          // bf16 wire buffer (numel)
   XgmiSignal* sig = nullptr;
   uint32_t* host_err = nullptr;      // pinned, mapped (host view)
   uint32_t* host_err_dev = nullptr;  // the same word as the kernels address it
   float* peer_buf[DMLC_XGMI_MAX_RANKS] = {};
+  uint16_t* peer_wire[DMLC_XGMI_MAX_RANKS] = {};
   XgmiSignal* peer_sig[DMLC_XGMI_MAX_RANKS] = {};
   bool opened = false;
 };
@@ -154,6 +181,8 @@ int dmlc_xgmi_create(int rank, int world, int64_t numel) {
   hipError_t e = hipGetDevice(&c->device);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->buf), (size_t)numel * sizeof(float));
   if (e == hipSuccess) e = hipMemset(c->buf, 0, (size_t)numel * sizeof(float));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->wire), (size_t)numel * sizeof(uint16_t));
+  if (e == hipSuccess) e = hipMemset(c->wire, 0, (size_t)numel * sizeof(uint16_t));
   if (e == hipSuccess) {
     // flags in uncached device memory: every poll and every remote flag store goes to memory
     e = hipExtMallocWithFlags(reinterpret_cast<void**>(&c->sig), sizeof(XgmiSignal), hipDeviceMallocUncached);
@@ -183,11 +212,13 @@ int dmlc_xgmi_create(int rank, int world, int64_t numel) {
   if (e != hipSuccess) {
     fail("xgmi_create", e);
     if (c->buf) (void)hipFree(c->buf);
+    if (c->wire) (void)hipFree(c->wire);
     if (c->sig) (void)hipFree(c->sig);
     delete c;
     return -1;
   }
   c->peer_buf[rank] = c->buf;
+  c->peer_wire[rank] = c->wire;
   c->peer_sig[rank] = c->sig;
   std::lock_guard<std::mutex> l(g_mu);
   g_ctx.push_back(c);
@@ -215,6 +246,9 @@ int dmlc_xgmi_handles(int id, uint8_t* out) {
   e = hipIpcGetMemHandle(&h, c->sig);
   if (e != hipSuccess) { fail("hipIpcGetMemHandle(sig)", e); return -1; }
   memcpy(out + DMLC_XGMI_HANDLE_BYTES, &h, DMLC_XGMI_HANDLE_BYTES);
+  e = hipIpcGetMemHandle(&h, c->wire);
+  if (e != hipSuccess) { fail("hipIpcGetMemHandle(wire)", e); return -1; }
+  memcpy(out + 2 * DMLC_XGMI_HANDLE_BYTES, &h, DMLC_XGMI_HANDLE_BYTES);
   return 0;
 }
 
@@ -226,7 +260,7 @@ int dmlc_xgmi_open(int id, const uint8_t* all) {
     if (p == c->rank) continue;
     hipIpcMemHandle_t h;
     void* ptr = nullptr;
-    const uint8_t* hp = all + (size_t)p * 2 * DMLC_XGMI_HANDLE_BYTES;
+    const uint8_t* hp = all + (size_t)p * DMLC_XGMI_HANDLES * DMLC_XGMI_HANDLE_BYTES;
     memcpy(&h, hp, DMLC_XGMI_HANDLE_BYTES);
     hipError_t e = hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) { fail("hipIpcOpenMemHandle(buf of rank " + std::to_string(p) + ")", e); return -1; }
@@ -235,18 +269,23 @@ int dmlc_xgmi_open(int id, const uint8_t* all) {
     e = hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) { fail("hipIpcOpenMemHandle(sig of rank " + std::to_string(p) + ")", e); return -1; }
     c->peer_sig[p] = static_cast<XgmiSignal*>(ptr);
+    memcpy(&h, hp + 2 * DMLC_XGMI_HANDLE_BYTES, DMLC_XGMI_HANDLE_BYTES);
+    e = hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) { fail("hipIpcOpenMemHandle(wire of rank " + std::to_string(p) + ")", e); return -1; }
+    c->peer_wire[p] = static_cast<uint16_t*>(ptr);
   }
   c->opened = true;
   return 0;
 }
 
-hipError_t dmlc_xgmi_allreduce(int id, int64_t offset, int64_t numel, int blocks, hipStream_t s) {
+hipError_t dmlc_xgmi_allreduce(int id, int64_t offset, int64_t numel, int blocks, int bf16_wire, hipStream_t s) {
   XgmiCtx* c = get(id);
   if (!c || !c->opened) return hipErrorInvalidValue;
   if (offset < 0 || numel <= 0 || offset % 4 || numel % 4 || offset + numel > c->numel) return hipErrorInvalidValue;
   XgmiArgs a;
   for (int p = 0; p < DMLC_XGMI_MAX_RANKS; ++p) {
     a.bufs[p] = reinterpret_cast<float4*>(c->peer_buf[p]);
+    a.wires[p] = reinterpret_cast<uint2*>(c->peer_wire[p]);
     a.sigs[p] = c->peer_sig[p];
   }
   a.rank = c->rank;
@@ -257,8 +296,11 @@ hipError_t dmlc_xgmi_allreduce(int id, int64_t offset, int64_t numel, int blocks
   if (blocks <= 0) blocks = (int)std::min<int64_t>(64, std::max<int64_t>(4, (shard4 + 2 * XT - 1) / (2 * XT)));
   blocks = std::min(blocks, DMLC_XGMI_MAX_BLOCKS);
   switch (c->world) {
-#define DMLC_XGMI_CASE(W) \
-    case W: hipLaunchKernelGGL(k_xgmi_allreduce<W>, dim3(blocks), dim3(XT), 0, s, a); break;
+#define DMLC_XGMI_CASE(W)                                                                   \
+    case W:                                                                                 \
+      if (bf16_wire) hipLaunchKernelGGL((k_xgmi_allreduce<W, true>), dim3(blocks), dim3(XT), 0, s, a); \
+      else hipLaunchKernelGGL((k_xgmi_allreduce<W, false>), dim3(blocks), dim3(XT), 0, s, a);         \
+      break;
     DMLC_XGMI_CASE(1) DMLC_XGMI_CASE(2) DMLC_XGMI_CASE(3) DMLC_XGMI_CASE(4)
     DMLC_XGMI_CASE(5) DMLC_XGMI_CASE(6) DMLC_XGMI_CASE(7) DMLC_XGMI_CASE(8)
 #undef DMLC_XGMI_CASE
@@ -284,8 +326,10 @@ void dmlc_xgmi_destroy(int id) {
     if (p == c->rank) continue;
     if (c->peer_buf[p]) (void)hipIpcCloseMemHandle(c->peer_buf[p]);
     if (c->peer_sig[p]) (void)hipIpcCloseMemHandle(c->peer_sig[p]);
+    if (c->peer_wire[p]) (void)hipIpcCloseMemHandle(c->peer_wire[p]);
   }
   (void)hipFree(c->buf);
+  (void)hipFree(c->wire);
   (void)hipFree(c->sig);
   if (c->host_err) (void)hipHostFree(c->host_err);
   std::lock_guard<std::mutex> l(g_mu);

@@ -119,14 +119,14 @@ class FusedCifarEngine:
         self.xgmi, self.comm_info = None, {"allreduce": "rccl" if self.dp else "none"}
         self._buckets = {True: (M.FC_BUCKET_OFFSET, self.master.numel() - M.FC_BUCKET_OFFSET),
                          False: (0, M.FC_BUCKET_OFFSET)}
-        if world_size > 1 and dev.type == "cuda" and comm_dtype == "fp32" and allreduce != "rccl":
+        if world_size > 1 and dev.type == "cuda" and comm_dtype in ("fp32", "bf16") and allreduce != "rccl":
             from ..parallel import xgmi as X
             # timed on the call pattern the step will issue: one whole-buffer all-reduce (serial) or
             # the fc bucket then the conv bucket (overlap)
             pattern = ([(0, self.master.numel())] if dp_schedule == "serial"
                        else [self._buckets[True], self._buckets[False]])
             self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev, pattern,
-                                                 mode=allreduce, group=process_group)
+                                                 mode=allreduce, group=process_group, wire=comm_dtype)
         if self.xgmi is not None:
             self.grad = self.xgmi.buf[:self.master.numel()]
             self.grad.zero_()

@@ -127,10 +127,11 @@ class FusedResNetEngine:
         # gradient all-reduce (N>1): xGMI peer-to-peer kernel over an IPC-shared buffer when it
         # self-tests and measures faster than RCCL (parallel/xgmi.py), else RCCL
         self.xgmi, self.comm_info = None, {"allreduce": "rccl" if self.dp else "none"}
-        if world_size > 1 and dev.type == "cuda" and comm_dtype == "fp32" and allreduce != "rccl":
+        if world_size > 1 and dev.type == "cuda" and comm_dtype in ("fp32", "bf16") and allreduce != "rccl":
             from ..parallel import xgmi as X
             self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev,
-                                                 [(0, self.master.numel())], mode=allreduce, group=process_group)
+                                                 [(0, self.master.numel())], mode=allreduce, group=process_group,
+                                                 wire=comm_dtype)
         if self.xgmi is not None:
             self.grad = self.xgmi.buf[:self.master.numel()]
             self.grad.zero_()

@@ -7,7 +7,8 @@ connected by point-to-point xGMI links, and the gradient buckets of this model a
 0.43 MB per step) -- the latency-bound regime of a ring.  :class:`XgmiAllReduce` maps every peer's
 gradient buffer into this process (``hipIpcOpenMemHandle``) and all-reduces with one kernel launch
 per bucket (csrc/kernels/xgmi_allreduce.hip): each rank reduces 1/W of the bucket by reading it
-from all W GPUs at once and pushes the sum back to all of them.  The launch carries its barrier
+from all W GPUs at once and pushes the sum back to all of them (wire format fp32, or bf16 for
+``--comm_dtype bf16``: half the link bytes, sums in fp32).  The launch carries its barrier
 epochs in device memory, so it is captured in the step's HIP graph together with the compute.
 
 :func:`select` decides per job, by measurement: the xGMI path is used only when every rank could
@@ -26,7 +27,7 @@ import torch.distributed as dist
 
 from ..ops import _ext
 
-HANDLE_BYTES = 128
+HANDLE_BYTES = 192                      # 3 IPC handles per rank: data, signals, bf16 wire
 
 
 def _ops():
@@ -39,9 +40,13 @@ class XgmiError(RuntimeError):
 
 
 class XgmiAllReduce:
-    """In-place sum all-reduce of ranges of one IPC-shared fp32 buffer (``self.buf``)."""
+    """In-place sum all-reduce of ranges of one IPC-shared fp32 buffer (``self.buf``).  wire="bf16":
+    the values cross xGMI as bf16 and every replica ends with the bf16-rounded fp32 sums."""
 
-    def __init__(self, numel: int, rank: int, world: int, group=None):
+    def __init__(self, numel: int, rank: int, world: int, group=None, wire: str = "fp32"):
+        if wire not in ("fp32", "bf16"):
+            raise XgmiError(f"unknown wire format {wire!r}")
+        self.bf16 = wire == "bf16"
         if world > 8:
             raise XgmiError("xGMI all-reduce supports up to 8 ranks (one node)")
         ops = _ops()
@@ -60,7 +65,7 @@ class XgmiAllReduce:
 
     def all_reduce(self, offset: int, numel: int, blocks: int = 0):
         """Sum-all-reduce ``buf[offset:offset+numel]`` on the current stream (capturable)."""
-        self.ops.xgmi_allreduce(self.ctx, self.buf, int(offset), int(numel), int(blocks))
+        self.ops.xgmi_allreduce(self.ctx, self.buf, int(offset), int(numel), int(blocks), self.bf16)
 
     def error(self) -> int:
         return int(self.ops.xgmi_error(self.ctx))
@@ -73,9 +78,10 @@ class XgmiAllReduce:
 
     def self_test(self, iters: int = 3) -> bool:
         """Exact-sum check: rank r writes (r+1)*(i%97)/2 + it; every rank must read back the exact
-        sum over ranks at every element (small multiples of 1/2: fp32 sums are exact)."""
+        sum over ranks at every element (small multiples of 1/2: fp32 sums are exact; with the bf16
+        wire the pattern is (r+1)*(i%5)/2 + it, exact in bf16 up to 8 ranks)."""
         n = self.numel
-        pat = torch.remainder(torch.arange(n, device=self.buf.device, dtype=torch.float32), 97.0) * 0.5
+        pat = torch.remainder(torch.arange(n, device=self.buf.device, dtype=torch.float32), 5.0 if self.bf16 else 97.0) * 0.5
         ok = True
         for it in range(iters):
             self.buf.copy_(pat * (self.rank + 1) + it)
@@ -114,11 +120,12 @@ def _time(fn, iters: int, device) -> float:
 
 
 def select(numel: int, rank: int, world: int, device: torch.device, buckets: List[Tuple[int, int]],
-           mode: str = "auto", group=None, log=None) -> Tuple[Optional[XgmiAllReduce], Dict]:
+           mode: str = "auto", group=None, log=None, wire: str = "fp32") -> Tuple[Optional[XgmiAllReduce], Dict]:
     """Collective choice of the gradient all-reduce.  Returns (XgmiAllReduce | None, info).
 
     mode "rccl": never xGMI.  "xgmi": xGMI unless it cannot work (then RCCL).  "auto": like "xgmi",
-    and over RCCL additionally only if measured faster than RCCL on ``buckets`` ((offset, numel))."""
+    and over RCCL additionally only if measured faster than RCCL on ``buckets`` ((offset, numel)),
+    RCCL moving the same wire dtype."""
     info: Dict = {"allreduce": "rccl"}
     if mode == "rccl" or world == 1 or device.type != "cuda" or os.environ.get("DMLC_NO_XGMI"):
         return None, info
@@ -126,7 +133,7 @@ def select(numel: int, rank: int, world: int, device: torch.device, buckets: Lis
     bdev = device if nccl else torch.device("cpu")
     ar, why = None, ""
     try:
-        ar = XgmiAllReduce(numel, rank, world, group)
+        ar = XgmiAllReduce(numel, rank, world, group, wire=wire)
         ok = 1.0
     except Exception as e:                       # noqa: BLE001 -- any failure means: use RCCL
         ok, why = 0.0, f"{type(e).__name__}: {e}"
@@ -145,7 +152,7 @@ def select(numel: int, rank: int, world: int, device: torch.device, buckets: Lis
             log("xgmi all-reduce self-test failed; using RCCL")
         return None, info
     if mode == "auto" and nccl:
-        scratch = torch.zeros(ar.numel, dtype=torch.float32, device=device)
+        scratch = torch.zeros(ar.numel, dtype=torch.bfloat16 if wire == "bf16" else torch.float32, device=device)
 
         def run_x():
             for off, n in buckets:
@@ -164,4 +171,5 @@ def select(numel: int, rank: int, world: int, device: torch.device, buckets: Lis
             ar.close()
             return None, info
     info["allreduce"] = "xgmi"
+    info["wire"] = wire
     return ar, info

@@ -33,6 +33,8 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedu
                            relu_logits=False, comm_dtype=comm_dtype, allreduce=allreduce,
                            dp_schedule=schedule)
     assert eng.comm_info["allreduce"] == ("xgmi" if allreduce == "xgmi" else "rccl"), eng.comm_info
+    if allreduce == "xgmi":
+        assert eng.comm_info["wire"] == comm_dtype, eng.comm_info      # bf16 no longer forces RCCL
     eng.step()
     if graph:
         eng.capture()
@@ -49,7 +51,8 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedu
                          [(False, "fp32", "rccl", "overlap"), (True, "fp32", "rccl", "overlap"),
                           (True, "bf16", "rccl", "overlap"), (False, "fp32", "xgmi", "overlap"),
                           (True, "fp32", "xgmi", "overlap"), (True, "fp32", "rccl", "serial"),
-                          (False, "fp32", "xgmi", "serial"), (True, "fp32", "xgmi", "serial")])
+                          (False, "fp32", "xgmi", "serial"), (True, "fp32", "xgmi", "serial"),
+                          (True, "bf16", "xgmi", "serial")])
 def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype, allreduce, schedule):
     import torch.multiprocessing as mp
     from dmlc.cli import free_port

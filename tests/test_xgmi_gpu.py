@@ -120,3 +120,52 @@ def test_xgmi_missing_peer_times_out(tmp_path):
     from dmlc.cli import free_port
     mp.spawn(_rank_timeout, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
     assert torch.load(tmp_path / "t0.pt", weights_only=True)["err"] & 1
+
+
+def _rank_bf16(rank, world, port, out):
+    dist = _init(rank, world, port)
+    from dmlc.parallel.xgmi import XgmiAllReduce
+    ar = XgmiAllReduce(4096 * 9 + 64, rank, world, wire="bf16")
+    res = {"self_test": ar.self_test()}
+    ar.buf.copy_(_data(rank, ar.numel, 5).cuda())
+    dist.barrier()
+    ar.all_reduce(0, 256)
+    ar.all_reduce(256, ar.numel - 256)
+    torch.cuda.synchronize()
+    res["eager"] = ar.buf.cpu().clone()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        ar.all_reduce(0, ar.numel, 4)
+    torch.cuda.current_stream().wait_stream(s)
+    ar.buf.copy_(_data(rank, ar.numel, 6).cuda())
+    torch.cuda.synchronize()
+    dist.barrier()
+    g.replay()
+    torch.cuda.synchronize()
+    res["graph"] = ar.buf.cpu().clone()
+    res["err"] = ar.error()
+    dist.barrier()
+    ar.close()
+    torch.save(res, os.path.join(out, f"b{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_xgmi_allreduce_bf16_wire(tmp_path):
+    """--comm_dtype bf16 over the xGMI kernel: each rank's values cross as bf16, the owner sums in
+    fp32 in rank order, and every replica receives the same bf16-rounded sums -- equal, bit for bit,
+    to bf16(bf16(x0) + bf16(x1)) computed on the host, on both ranks, eager and graph-replayed."""
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    world = 2
+    mp.spawn(_rank_bf16, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    rs = [torch.load(tmp_path / f"b{r}.pt", weights_only=True) for r in range(world)]
+    n = rs[0]["eager"].numel()
+    bf = lambda t: t.to(torch.bfloat16).float()
+    for key, it in (("eager", 5), ("graph", 6)):
+        want = bf(bf(_data(0, n, it)) + bf(_data(1, n, it)))
+        for r in rs:
+            assert r["self_test"] and r["err"] == 0
+            assert torch.equal(r[key], want), (key, float((r[key] - want).abs().max()))
