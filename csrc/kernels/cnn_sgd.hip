@@ -116,11 +116,11 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   // w2d[ci][((4-kh)*5 + (4-kw))*64 + co] : contiguous in co
   *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.w2d) + (size_t)ci * 1600 + (24 - khw) * 64 + co) =
       pack4(w.x, w.y, w.z, w.w);
-#ifndef DMLC_SGD_NO_W2F
-  bf16* w2f = reinterpret_cast<bf16*>(a.w2f) + krow;  // w2f[co][krow]
-  w2f[(co + 0) * 1600] = (bf16)w.x; w2f[(co + 1) * 1600] = (bf16)w.y;
-  w2f[(co + 2) * 1600] = (bf16)w.z; w2f[(co + 3) * 1600] = (bf16)w.w;
-#endif
+  if (!a.w2f8) {                                      // the bf16 forward's shadow (fp8: not read)
+    bf16* w2f = reinterpret_cast<bf16*>(a.w2f) + krow;  // w2f[co][krow]
+    w2f[(co + 0) * 1600] = (bf16)w.x; w2f[(co + 1) * 1600] = (bf16)w.y;
+    w2f[(co + 2) * 1600] = (bf16)w.z; w2f[(co + 3) * 1600] = (bf16)w.w;
+  }
 }
 
 DEV void conv1_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {

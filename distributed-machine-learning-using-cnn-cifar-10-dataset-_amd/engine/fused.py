@@ -176,8 +176,9 @@ class FusedCifarEngine:
             # 96 + 4*40 -> 19.8, 64 + 4*48 -> 23.4 (r2, register-staged conv1 scatter)
             g2_ = max(1, min(B, 32, B // 8))
             self.g2 = g2 or (g2_ // 8 * 8 if g2_ >= 8 else g2_)
-            left = 256 - 4 * self.g2
-            self.g1 = g1 or max(1, min(B, left if left >= B // 4 else B // 2))
+            # conv1: the CUs the conv2 blocks leave (one block per CU; past B=256 every block takes
+            # several images instead of the grid growing beyond the chip)
+            self.g1 = g1 or max(1, min(B, 256 - 4 * self.g2))
         else:
             self.g2 = g2 or max(1, min(B, B // 6))      # conv2 wgrad: 4 ci-quarter blocks x ~6 images per group
             self.g1 = g1 or max(1, min(B, B // 2))      # conv1 wgrad: 2 images per block

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--g1", type=int, default=None)
     ap.add_argument("--g2", type=int, default=None)
     ap.add_argument("--fc1-split", type=int, default=None)
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16")
     ap.add_argument("--wgrad-sweep", default="", help="merged weight-gradient launch at other (g1, g2) "
                     "splits, plus each body alone on g1 / 4*g2 workgroups")
     a = ap.parse_args()
@@ -47,7 +48,7 @@ def main():
     data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
     labels = torch.randint(0, 10, (50000,), dtype=torch.int32, generator=g)
     eng = FusedCifarEngine(a.batch, data, labels, device="cuda", g1=a.g1, g2=a.g2, fc1_split=a.fc1_split,
-                           lr=1e-4)
+                           lr=1e-4, dtype=a.dtype)
     eng.step()
     torch.cuda.synchronize()
     o, p = eng.ops, eng.pv
@@ -55,6 +56,9 @@ def main():
     res["conv1_fwd"] = timeit(lambda: o.conv1_fwd(eng.data, eng.bidx, None, 1, eng.cy, eng.cx, eng.w1f,
                                                   p["conv1_bias"], eng.p1, eng.am1, None, eng.xraw), a.iters)
     res["conv2_fwd"] = timeit(lambda: o.conv2_fwd(eng.p1, eng.w2f, p["conv2_bias"], eng.p2, eng.am2), a.iters)
+    if eng.fp8:
+        res["conv2_fwd_fp8"] = timeit(lambda: o.conv2_fwd_fp8(eng.p1, eng.w2f8, p["conv2_bias"], eng.amax_x, eng.scale_w,
+                                                              None, eng.p2, eng.am2), a.iters)
     res["conv12_fwd"] = timeit(lambda: o.conv12_fwd(eng.data, eng.bidx, None, 1, eng.cy, eng.cx,
                                                     eng.w1f, p["conv1_bias"], eng.p1, eng.am1, eng.w2f,
                                                     p["conv2_bias"], eng.p2, eng.am2, eng.xraw), a.iters)
@@ -100,7 +104,7 @@ def main():
                              and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad",
                                                                    "conv2_dgrad" if eng.fused_w1 else "conv2_dgrad_w1")
                              and k not in (("conv1_fwd", "conv2_fwd") if eng.fused_fwd else ("conv12_fwd",)))
-    cfg = dict(batch=a.batch, g1=eng.g1, g2=eng.g2, fc1_split=eng.fc1_split)
+    cfg = dict(batch=a.batch, g1=eng.g1, g2=eng.g2, fc1_split=eng.fc1_split, dtype=a.dtype)
     print(json.dumps({"config": cfg, "us": {k: round(v, 2) for k, v in res.items()}}), flush=True)
 
 
