@@ -346,8 +346,9 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
          bool staircase, const Tensor& ticket, const Tensor& loss_part, const Tensor& correct_part,
          const Tensor& stats, const c10::optional<Tensor>& w2f8, const c10::optional<Tensor>& amax_w,
          const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize, int64_t batch,
-         const c10::optional<Tensor>& bidx, const c10::optional<Tensor>& order) {
+         const c10::optional<Tensor>& bidx, const c10::optional<Tensor>& order, double warmup) {
   TORCH_CHECK(roles >= 0 && roles <= 2, "sgd roles must be 0..2");
+  TORCH_CHECK(warmup >= 0.0, "sgd: warmup must be >= 0");
   TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
   TORCH_CHECK(off.size() == 10, "off must have 10 entries");
   static const int64_t numel[10] = {4800, 64, 102400, 64, 884736, 384, 73728, 192, 1920, 10};
@@ -391,7 +392,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   a.w1f = w1f.data_ptr(); a.w2f = w2f.data_ptr(); a.w2d = w2d.data_ptr(); a.fc1n = fc1n.data_ptr();
   a.fc2t = fc2t.data_ptr(); a.fc2n = fc2n.data_ptr(); a.fc3t = fc3t.data_ptr(); a.fc3d = fc3d.data_ptr();
   a.step = step.data_ptr<int64_t>(); a.lr0 = (float)lr0; a.decay = (float)decay;
-  a.decay_steps = (float)decay_steps; a.staircase = staircase;
+  a.decay_steps = (float)decay_steps; a.staircase = staircase; a.warmup = (float)warmup;
   a.ticket = reinterpret_cast<unsigned int*>(ticket.data_ptr<int>());
   a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
   a.nhead = (int)loss_part.numel();
@@ -454,7 +455,7 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
-        "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None) -> ()");
+        "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

@@ -241,7 +241,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
             at::IntArrayRef mv_off, int64_t fcw_off, int64_t fcb_off, at::TensorList part, at::TensorList wf,
             at::TensorList wd, const Tensor& stat, const Tensor& red, const Tensor& fc_part, const Tensor& loss_img,
             const Tensor& correct_img, const Tensor& step, const Tensor& ticket, const Tensor& stats, int64_t mode,
-            double lr0, double decay, double decay_steps, bool staircase, double bn_momentum) {
+            double lr0, double decay, double decay_steps, bool staircase, double bn_momentum, double warmup) {
   constexpr int L = DMLC_RN_LAYERS;
   TORCH_CHECK(mode >= 0 && mode <= 3, "rn_sgd mode must be 0..3");
   TORCH_CHECK(conv_off.size() == L && gamma_off.size() == L && beta_off.size() == L && mm_off.size() == L &&
@@ -297,6 +297,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
   a.mode = (int)mode;
   a.step = step.data_ptr<int64_t>(); a.lr0 = (float)lr0; a.decay = (float)decay; a.decay_steps = (float)decay_steps;
   a.staircase = staircase ? 1 : 0;
+  a.warmup = (float)warmup;
   a.ticket = reinterpret_cast<unsigned int*>(ticket.data_ptr<int>());
   a.loss_img = loss_img.data_ptr<float>(); a.correct_img = correct_img.data_ptr<int>();
   a.stats = stats.data_ptr<float>(); a.stats_len = (int)stats.size(0);
@@ -327,7 +328,7 @@ TORCH_LIBRARY_FRAGMENT(dmlc, m) {
         "int[] gamma_off, int[] beta_off, int[] mm_off, int[] mv_off, int fcw_off, int fcb_off, Tensor[] part, "
         "Tensor(d!)[] wf, Tensor(e!)[] wd, Tensor stat, Tensor red, Tensor fc_part, Tensor loss_img, "
         "Tensor correct_img, Tensor(f!) step, Tensor(g!) ticket, Tensor(h!) stats, int mode, float lr0, "
-        "float decay, float decay_steps, bool staircase, float bn_momentum) -> ()");
+        "float decay, float decay_steps, bool staircase, float bn_momentum, float warmup=0.0) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

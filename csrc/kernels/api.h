@@ -166,6 +166,7 @@ struct DmlcSgdArgs {
   void* w1f; void* w2f; void* w2d; void* fc1n; void* fc2t; void* fc2n; void* fc3t; void* fc3d;
   // schedule
   int64_t* step; float lr0; float decay; float decay_steps; int staircase;
+  float warmup;             // linear LR warm-up over this many steps (0: none)
   unsigned int* ticket;     // zero-initialised arrival counter
   const float* loss_part; const int* correct_part; int nhead;
   float* stats; int stats_len;   // ring [stats_len][4] = {step, loss, accuracy, lr}

@@ -89,6 +89,7 @@ struct DmlcRnSgdArgs {
   int split[DMLC_RN_LAYERS + 1];       // slab split factor per conv layer + fc (set by the launcher)
   int mode;                  // 0 reduce+apply, 1 reduce->grad, 2 apply grad, 3 shadows only
   int64_t* step; float lr0, decay, decay_steps; int staircase;
+  float warmup;             // linear LR warm-up steps (0: none)
   unsigned int* ticket;
   const float* loss_img; const int* correct_img;
   float* stats; int stats_len;

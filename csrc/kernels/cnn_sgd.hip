@@ -42,8 +42,11 @@ __host__ __device__ inline int fc1_blocks(const DmlcSgdArgs& a) {
   return ((a.off[6] - a.off[4]) / 4 + 256 * FC_F4_PER_THREAD - 1) / (256 * FC_F4_PER_THREAD);
 }
 
+// staircase (or constant) decay, times a linear warm-up ramp (step + 1) / warmup over the first
+// `warmup` steps (large-batch recipe, BASELINE config 5)
 DEV float lr_of(const DmlcSgdArgs& a, int64_t step) {
-  return a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
+  const float lr = a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
+  return a.warmup > 0.f && (float)step < a.warmup ? lr * ((float)step + 1.f) / a.warmup : lr;
 }
 
 DEV float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }

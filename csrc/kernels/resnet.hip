@@ -779,7 +779,8 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
   __shared__ float4 lds[RT];
   __shared__ float lred[2][4];
   const int64_t step = *a.step;
-  const float lr = a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
+  const float lr0 = a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
+  const float lr = a.warmup > 0.f && (float)step < a.warmup ? lr0 * ((float)step + 1.f) / a.warmup : lr0;
   const int mode = a.mode;
   const bool reduce = mode <= 1, apply = mode == 0 || mode == 2;
   const int blk = blockIdx.x, tid = threadIdx.x;

@@ -59,6 +59,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--lr_decay", type=float, default=d.lr_decay)
     p.add_argument("--num_gens_to_wait", type=float, default=d.num_gens_to_wait)
     p.add_argument("--lr_schedule", choices=["staircase", "constant"], default=d.lr_schedule)
+    p.add_argument("--lr_scaling", choices=["none", "linear"], default=d.lr_scaling,
+                   help="linear: learning_rate * global_batch / lr_base_batch (large-batch recipe)")
+    p.add_argument("--lr_base_batch", type=int, default=d.lr_base_batch)
+    p.add_argument("--warmup_steps", type=int, default=d.warmup_steps, help="linear LR warm-up steps")
     p.add_argument("--output_every", type=int, default=d.output_every)
     p.add_argument("--eval_every", type=int, default=d.eval_every)
     p.add_argument("--eval_batches", type=int, default=d.eval_batches)

@@ -55,6 +55,11 @@ class TrainConfig:
     lr_decay: float = LR_DECAY
     num_gens_to_wait: float = NUM_GENS_TO_WAIT
     lr_schedule: str = "staircase"        # 'staircase' (D3 fixed) | 'constant' (reference as run)
+    # large-batch recipe (BASELINE config 5): lr = learning_rate * global_batch / lr_base_batch with
+    # 'linear' scaling, ramped linearly from lr / warmup_steps over the first warmup_steps steps
+    lr_scaling: str = "none"              # 'none' (reference) | 'linear'
+    lr_base_batch: int = BATCH_SIZE       # the batch learning_rate was tuned for (the reference's 128)
+    warmup_steps: int = 0
     output_every: int = OUTPUT_EVERY
     eval_every: int = EVAL_EVERY
     eval_batches: int = 0                 # 0 = full test set; 1 = reference fidelity (one batch)
@@ -85,3 +90,12 @@ class TrainConfig:
 
     def replace(self, **kw) -> "TrainConfig":
         return dataclasses.replace(self, **kw)
+
+
+def effective_lr(cfg: "TrainConfig", world_size: int) -> float:
+    """The base learning rate the engines run with: the reference's, or linearly scaled with the
+    global batch (cfg.lr_scaling == 'linear'; Goyal et al.'s large-minibatch rule, used together
+    with cfg.warmup_steps)."""
+    if cfg.lr_scaling == "linear":
+        return cfg.learning_rate * cfg.batch_size * max(1, world_size) / cfg.lr_base_batch
+    return cfg.learning_rate

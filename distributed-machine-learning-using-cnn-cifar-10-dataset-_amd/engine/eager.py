@@ -26,7 +26,7 @@ class EagerTrainer:
                  lr: float = C.LEARNING_RATE, lr_decay: float = C.LR_DECAY,
                  decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, relu_logits: bool = True,
                  crop: int = C.CROP_HEIGHT, seed: int = 0, flat_params: Optional[torch.Tensor] = None,
-                 augment: bool = False, graph: bool = False):
+                 augment: bool = False, graph: bool = False, warmup_steps: int = 0):
         self.device = torch.device(device)
         self.model = build_model(model, seed=seed, relu_logits=relu_logits, flat=flat_params).to(self.device)
         self.B = int(batch_size)
@@ -35,6 +35,7 @@ class EagerTrainer:
         self.world_size, self.rank, self.pg = world_size, rank, process_group
         self.dtype = dtype
         self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
+        self.warmup = int(warmup_steps)
         self.crop = crop
         self.off = (32 - crop) // 2
         self.seed = seed
@@ -57,9 +58,10 @@ class EagerTrainer:
 
     # ------------------------------------------------------------------------------------------
     def lr(self, step: int) -> float:
-        if not self.staircase:
-            return self.lr0
-        return self.lr0 * self.decay ** math.floor(step / self.decay_steps)
+        lr = self.lr0 * self.decay ** math.floor(step / self.decay_steps) if self.staircase else self.lr0
+        if step < self.warmup:                 # linear warm-up, as the fused SGD kernels (lr_of)
+            lr *= (step + 1) / self.warmup
+        return lr
 
     def epoch_permutation(self, epoch: int) -> torch.Tensor:
         return self.order.epoch_shard(epoch)

@@ -68,7 +68,7 @@ class FusedCifarEngine:
                  process_group=None, seed: int = 0, fc1_split: Optional[int] = None, g1: Optional[int] = None,
                  g2: Optional[int] = None, stats_len: int = 4096, comm_dtype: str = "fp32",
                  capture_comm: Optional[bool] = None, dtype: str = "bf16", allreduce: str = "auto",
-                 dp_schedule: str = "serial", dp_force: bool = False):
+                 dp_schedule: str = "serial", dp_force: bool = False, warmup_steps: int = 0):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -83,6 +83,7 @@ class FusedCifarEngine:
         # the collective path (e.g. a captured RCCL all-reduce) on a single GPU
         self.dp = world_size > 1 or dp_force
         self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
+        self.warmup = float(warmup_steps)      # linear LR warm-up (large-batch recipe), in the SGD kernel
         self.relu_logits = relu_logits
         self.cy, self.cx = crop_offset
         self.comm_dtype = comm_dtype
@@ -336,7 +337,7 @@ class FusedCifarEngine:
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                      self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
                                                                       if self.fp8 else (None, None, None)),
-                     roles, finalize, self.Bv, self.bidx, self.order_desc)
+                     roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist

@@ -90,7 +90,7 @@ class FusedResNetEngine:
                  rank: int = 0, process_group=None, seed: int = 0, groups: Optional[List[int]] = None,
                  stats_len: int = 4096, comm_dtype: str = "fp32", wgrad_branch: Optional[bool] = None,
                  allreduce: str = "auto", capture_comm: Optional[bool] = None, dp_force: bool = False,
-                 deterministic: Optional[bool] = None):
+                 deterministic: Optional[bool] = None, warmup_steps: int = 0):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -101,6 +101,7 @@ class FusedResNetEngine:
         self.B = B
         self.world_size, self.rank, self.pg = world_size, rank, process_group
         self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
+        self.warmup = float(warmup_steps)      # linear LR warm-up, in the SGD kernel
         self.seed, self.comm_dtype = seed, comm_dtype
         self.dp = world_size > 1 or dp_force     # dp_force: the all-reduce path at world_size 1 (tests)
         if capture_comm is None:                 # RCCL collectives inside the step graph (nccl only)
@@ -307,7 +308,7 @@ class FusedResNetEngine:
         self.ops.rn_sgd(self.master, self.grad, scale, self.state, self.conv_off, self.gamma_off, self.beta_off,
                         self.mm_off, self.mv_off, self.fcw_off, self.fcb_off, self.part, self.wf, self.wd, self.stat,
                         self.red, self.fc_part, self.loss_img, self.correct_img, self.step_t, self.ticket, self.stats,
-                        mode, self.lr0, self.decay, self.decay_steps, self.staircase, R.BN_MOMENTUM)
+                        mode, self.lr0, self.decay, self.decay_steps, self.staircase, R.BN_MOMENTUM, self.warmup)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist

@@ -49,7 +49,7 @@ class _FusedAdapter:
     def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, data, labels):
         from .fused import FusedCifarEngine
         self.eng = FusedCifarEngine(cfg.batch_size, data, labels, device=info.device, world_size=info.world_size,
-                                    rank=max(0, info.rank), seed=cfg.seed, lr=cfg.learning_rate,
+                                    rank=max(0, info.rank), seed=cfg.seed, lr=C.effective_lr(cfg, info.world_size), warmup_steps=cfg.warmup_steps,
                                     lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                     staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
                                     crop_offset=((32 - cfg.crop) // 2,) * 2, comm_dtype=cfg.comm_dtype,
@@ -132,7 +132,7 @@ class _FusedResNetAdapter(_FusedAdapter):
         from .fused_resnet import FusedResNetEngine
         from ..models import resnet as R
         self.eng = FusedResNetEngine(cfg.batch_size, data, labels, device=info.device, world_size=info.world_size,
-                                     rank=max(0, info.rank), seed=cfg.seed, lr=cfg.learning_rate,
+                                     rank=max(0, info.rank), seed=cfg.seed, lr=C.effective_lr(cfg, info.world_size), warmup_steps=cfg.warmup_steps,
                                      lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                      staircase=cfg.lr_schedule == "staircase", comm_dtype=cfg.comm_dtype,
                                      allreduce=cfg.allreduce)
@@ -167,7 +167,7 @@ class _EagerAdapter:
         from .eager import EagerTrainer
         self.tr = EagerTrainer(cfg.model, cfg.batch_size, data, labels, device=info.device,
                                world_size=info.world_size, rank=max(0, info.rank), dtype=cfg.dtype,
-                               lr=cfg.learning_rate, lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
+                               lr=C.effective_lr(cfg, info.world_size), warmup_steps=cfg.warmup_steps, lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
                                crop=cfg.crop, seed=cfg.seed, augment=cfg.augment)
         self.specs = self.tr.model.specs

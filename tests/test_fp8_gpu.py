@@ -63,3 +63,37 @@ def test_fp8_training_tracks_scales_and_reduces_loss():
     assert abs(float(eng.amax_w[s]) - amax) <= 1e-6 * max(1.0, amax)       # exact running amax
     assert abs(float(eng.scale_w[s]) * amax - 224.0) / 224.0 < 0.05        # 2x headroom scale
     assert losses[-1] < 0.9 * losses[0], losses
+
+
+def test_fp8_loss_curve_tracks_bf16_over_300_steps():
+    """BASELINE config 5 acceptance: 300 steps of the same run in fp8 (conv2 forward on the f8f6f4
+    MFMA) and in bf16 -- same weights, same batches (the generated order is shared) -- must give loss
+    curves within 5 % of each other on 25-step windows, and both must learn."""
+    from dmlc.data import synthetic
+    B, steps, win = 128, 300, 25
+    data, labels = synthetic(8192, seed=5, learnable=True)
+    curves = {}
+    for dt in ("bf16", "fp8"):
+        eng = FusedCifarEngine(B, data, labels, seed=6, lr=1e-4, relu_logits=False, staircase=False, dtype=dt)
+        eng.step()
+        eng.capture()
+        eng.run(steps - 1)
+        torch.cuda.synchronize()
+        curves[dt] = torch.tensor([eng.read_stats(k)["loss"] for k in range(1, steps + 1)]).view(-1, win).mean(1)
+    wb, wf = curves["bf16"], curves["fp8"]
+    assert torch.isfinite(wf).all() and wf[-1] < 0.5 * wf[0] and wb[-1] < 0.5 * wb[0], (wf.tolist(), wb.tolist())
+    dev = float(((wf - wb).abs() / wb).max())
+    assert dev < 0.05, (dev, wf.tolist(), wb.tolist())
+
+
+def test_lr_warmup_and_linear_scaling_on_device():
+    """The fused SGD kernel's learning rate (lr_of) with the large-batch recipe: a linear warm-up
+    over the first steps times the staircase decay, read back from the on-device stats ring."""
+    from dmlc.data import synthetic
+    data, labels = synthetic(256, seed=3)
+    eng = FusedCifarEngine(16, data, labels, seed=4, lr=0.4, lr_decay=0.5, decay_steps=3, warmup_steps=4)
+    for _ in range(8):
+        eng.step()
+    torch.cuda.synchronize()
+    want = [0.4 * 0.5 ** (s // 3) * (min(s + 1, 4) / 4) for s in range(8)]
+    assert [eng.read_stats(s)["lr"] for s in range(1, 9)] == pytest.approx(want, rel=1e-6)
