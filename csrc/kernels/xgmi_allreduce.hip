@@ -113,8 +113,14 @@ __global__ __launch_bounds__(XT) void k_xgmi_allreduce(XgmiArgs a) {
   peer_barrier<W>(a, 0, e);            // every rank's gradients are complete
 
   // reduce-scatter of this rank's slice + push of the sums to every rank
+  // Element i belongs to thread (i - off4) % stride in EVERY phase (pack, reduce/push, unpack): the
+  // barriers are per workgroup, so a workgroup may only touch peer elements that the same workgroup
+  // of the peer produced before its barrier signal.  (Walking the slice from `lo` instead hands
+  // element i to another workgroup than the one that packed / unpacks it: a race in the bf16 path.)
   const int64_t lo = a.off4 + a.n4 * a.rank / W, hi = a.off4 + a.n4 * (a.rank + 1) / W;
-  for (int64_t i = lo + t0; i < hi; i += stride) {
+  int64_t i0 = a.off4 + t0;
+  if (i0 < lo) i0 += (lo - i0 + stride - 1) / stride * stride;
+  for (int64_t i = i0; i < hi; i += stride) {
     float4 v[W];
 #pragma unroll
     for (int p = 0; p < W; ++p) v[p] = BF16 ? unpack_bf16x4(a.wires[p][i]) : a.bufs[p][i];
