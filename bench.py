@@ -96,8 +96,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--impl", choices=["auto", "fused", "eager"], default="auto",
-                    help="fused = hand-written HIP kernels + HIP graph (cifar_cnn); eager = PyTorch ops")
+    ap.add_argument("--impl", choices=["auto", "fused", "eager", "hipf32"], default="auto",
+                    help="fused = hand-written HIP kernels + HIP graph (cifar_cnn); eager = PyTorch ops; "
+                         "hipf32 = the fp32-accurate CNN on the fp32 MFMA HIP kernels (--dtype fp32)")
     ap.add_argument("--model", choices=["cifar_cnn", "resnet20"], default="cifar_cnn")
     ap.add_argument("--crop", type=int, default=None, help="input crop (default 24 for cifar_cnn, 32 for resnet20)")
     ap.add_argument("--no-graph", action="store_true")
@@ -115,7 +116,7 @@ def parse():
     ap.add_argument("--capture-comm", choices=["auto", "on", "off"], default="auto",
                     help="RCCL all-reduce inside the step HIP graph (auto: on over nccl)")
     ap.add_argument("--steps-per-graph", type=int, default=32, help="longest chain of steps per graph replay")
-    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+    ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
     ap.add_argument("--dataset-size", type=int, default=50000)
     return ap.parse_args()
@@ -150,9 +151,11 @@ def _capture_comm(args):
 
 def build_eager(args, info, data, labels):
     from dmlc.engine.eager import EagerTrainer
+    hipf32 = args.impl == "hipf32"
     tr = EagerTrainer(args.model, args.batch, data, labels, device=info.device, world_size=info.world_size,
-                      rank=info.rank, dtype="bf16", crop=args.crop, lr=0.01 if args.model == "resnet20" else 0.1,
-                      graph=args.eager_graph)
+                      rank=info.rank, dtype="fp32" if hipf32 or args.dtype == "fp32" else "bf16", crop=args.crop,
+                      lr=0.01 if args.model == "resnet20" else 0.1, graph=args.eager_graph or hipf32,
+                      backend="hip_f32" if hipf32 else "torch")
     return tr, tr.step, None
 
 
@@ -167,7 +170,14 @@ def main():
         D.shutdown(info)
         sys.exit(3)
     if args.impl == "auto":
-        args.impl = "fused" if args.model == "cifar_cnn" or args.dtype == "bf16" else "eager"
+        if args.dtype == "fp32":
+            args.impl = "hipf32" if args.model == "cifar_cnn" and info.device.type == "cuda" else "eager"
+        else:
+            args.impl = "fused" if args.model == "cifar_cnn" or args.dtype == "bf16" else "eager"
+    if args.impl == "hipf32":
+        if args.model != "cifar_cnn" or info.world_size != 1:
+            raise SystemExit("--impl hipf32 is the single-GPU fp32 reference-precision CNN path")
+        args.dtype = "fp32"
     if args.crop is None:
         args.crop = 24 if args.model == "cifar_cnn" else 32
     if args.impl == "fused" and args.model == "cifar_cnn" and args.crop != 24:
@@ -254,7 +264,8 @@ def main():
                 "seq_len": None,
                 "parallelism": f"dp{n}",
                 "impl": args.impl + ("+hipgraph" if (args.impl == "fused" and not args.no_graph)
-                                     or (args.impl == "eager" and args.eager_graph) else ""),
+                                     or (args.impl == "eager" and args.eager_graph) or args.impl == "hipf32"
+                                     else ""),
                 "comm_dtype": args.comm_dtype,
                 "comm": comm,
                 "graph_warmup_steps": graph_warm,

@@ -75,7 +75,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--download", type="bool", nargs="?", const=True, default=False)
     p.add_argument("--model", choices=["cifar_cnn", "resnet20"], default=d.model)
     p.add_argument("--dtype", choices=["fp32", "bf16", "fp8"], default=d.dtype)
-    p.add_argument("--impl", choices=["auto", "fused", "eager"], default=d.impl)
+    p.add_argument("--impl", choices=["auto", "fused", "eager", "hipf32"], default=d.impl)
     p.add_argument("--device", choices=["auto", "cpu", "cuda"], default=d.device)
     p.add_argument("--seed", type=int, default=d.seed)
     p.add_argument("--checkpoint_secs", type=float, default=d.checkpoint_secs)

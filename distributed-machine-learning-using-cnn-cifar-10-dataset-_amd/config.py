@@ -71,7 +71,7 @@ class TrainConfig:
     download: bool = False                # fetch the CIFAR-10 archive if absent (offline by default)
     model: str = "cifar_cnn"              # cifar_cnn | resnet20
     dtype: str = "bf16"                   # fp32 | bf16 | fp8
-    impl: str = "auto"                    # auto | fused (HIP kernels + hipGraph) | eager (torch ops)
+    impl: str = "auto"                    # auto | fused (HIP kernels + hipGraph) | eager (torch ops) | hipf32 (fp32 HIP)
     device: str = "auto"                  # auto | cpu | cuda
     seed: int = 0
     checkpoint_secs: float = CHECKPOINT_SECS

@@ -1,8 +1,9 @@
 """Eager (PyTorch-op) training engine.
 
-Used for (a) the CPU "plumbing" configuration (BASELINE config 1), (b) models without fused HIP
-kernels yet (ResNet-20), (c) the framework-default comparison line of the benchmark, and (d) as
-the numerics oracle for the fused engine.  Semantics follow the reference training step
+Used for (a) the CPU "plumbing" configuration (BASELINE config 1), (b) the fp32-accurate GPU mode
+(``backend='hip_f32'``: the model's matmuls/convs on the fp32 HIP kernels of ops/f32.py, driven
+step by step from here, optionally captured into one HIP graph), (c) the framework-default
+comparison line of the benchmark, and (d) the numerics oracle for the fused engines.  Semantics follow the reference training step
 (/root/reference/cifar10cnn.py:159-164, :230): sparse softmax cross-entropy (mean), plain SGD,
 staircase LR decay, global_step++.  Data parallelism is synchronous: the flat gradient is
 all-reduced in two buckets (fc first, then conv — SURVEY.md §2.D) and averaged.
@@ -26,9 +27,13 @@ class EagerTrainer:
                  lr: float = C.LEARNING_RATE, lr_decay: float = C.LR_DECAY,
                  decay_steps: float = C.NUM_GENS_TO_WAIT, staircase: bool = True, relu_logits: bool = True,
                  crop: int = C.CROP_HEIGHT, seed: int = 0, flat_params: Optional[torch.Tensor] = None,
-                 augment: bool = False, graph: bool = False, warmup_steps: int = 0):
+                 augment: bool = False, graph: bool = False, warmup_steps: int = 0, backend: str = "torch"):
         self.device = torch.device(device)
-        self.model = build_model(model, seed=seed, relu_logits=relu_logits, flat=flat_params).to(self.device)
+        if backend == "hip_f32" and (self.device.type != "cuda" or dtype != "fp32"):
+            raise ValueError("the hip_f32 backend is the fp32 GPU path (device cuda, dtype fp32)")
+        self.backend = backend
+        self.model = build_model(model, seed=seed, relu_logits=relu_logits, flat=flat_params,
+                                 backend=backend).to(self.device)
         self.B = int(batch_size)
         self.data = data.to(self.device)
         self.labels = labels.to(self.device).long()

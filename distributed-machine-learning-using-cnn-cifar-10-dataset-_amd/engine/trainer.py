@@ -163,13 +163,14 @@ class _FusedResNetAdapter(_FusedAdapter):
 class _EagerAdapter:
     kind = "eager"
 
-    def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, data, labels):
+    def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, data, labels, backend: str = "torch"):
         from .eager import EagerTrainer
         self.tr = EagerTrainer(cfg.model, cfg.batch_size, data, labels, device=info.device,
                                world_size=info.world_size, rank=max(0, info.rank), dtype=cfg.dtype,
                                lr=C.effective_lr(cfg, info.world_size), warmup_steps=cfg.warmup_steps, lr_decay=cfg.lr_decay, decay_steps=cfg.num_gens_to_wait,
                                staircase=cfg.lr_schedule == "staircase", relu_logits=cfg.relu_logits,
-                               crop=cfg.crop, seed=cfg.seed, augment=cfg.augment)
+                               crop=cfg.crop, seed=cfg.seed, augment=cfg.augment, backend=backend,
+                               graph=backend == "hip_f32" and cfg.graph and info.world_size == 1)
         self.specs = self.tr.model.specs
 
     def start(self, log=print):
@@ -231,6 +232,8 @@ def pick_impl(cfg: C.TrainConfig, device: torch.device) -> str:
     if (device.type == "cuda" and cfg.model == "cifar_cnn" and cfg.dtype in ("bf16", "fp8") and cfg.crop == 24
             and not cfg.augment):
         return "fused"                    # any batch size: masked tail rows (engine/fused.py)
+    if device.type == "cuda" and cfg.model == "cifar_cnn" and cfg.dtype == "fp32":
+        return "hipf32"                   # reference precision on the fp32 HIP kernels (ops/f32.py)
     if (device.type == "cuda" and cfg.model == "resnet20" and cfg.dtype == "bf16" and cfg.crop == 32
             and cfg.batch_size % 16 == 0 and not cfg.augment):
         return "fused"
@@ -263,7 +266,10 @@ class Session:
         self.test = (te_x, te_y)
         impl = pick_impl(cfg, info.device)
         fused = _FusedResNetAdapter if cfg.model == "resnet20" else _FusedAdapter
-        self.engine = (fused if impl == "fused" else _EagerAdapter)(cfg, info, tr_x, tr_y)
+        if impl == "fused":
+            self.engine = fused(cfg, info, tr_x, tr_y)
+        else:
+            self.engine = _EagerAdapter(cfg, info, tr_x, tr_y, backend="hip_f32" if impl == "hipf32" else "torch")
         self.impl = impl
         self.ckpt = None
         self.events = None

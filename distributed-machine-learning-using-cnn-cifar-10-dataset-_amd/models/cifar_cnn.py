@@ -148,8 +148,13 @@ class CifarCNN(nn.Module):
 
     specs = PARAM_SPECS
 
-    def __init__(self, flat: torch.Tensor | None = None, relu_logits: bool = True, seed: int = 0):
+    def __init__(self, flat: torch.Tensor | None = None, relu_logits: bool = True, seed: int = 0,
+                 backend: str = "torch"):
         super().__init__()
+        if backend not in ("torch", "hip_f32"):
+            raise ValueError(f"unknown CNN backend {backend!r}")
+        # 'hip_f32': every matmul/conv on the fp32 HIP kernels (ops/f32.py) -- reference precision
+        self.backend = backend
         if flat is None:
             g = torch.Generator().manual_seed(seed)
             flat = init_flat_params(g)
@@ -160,6 +165,9 @@ class CifarCNN(nn.Module):
         return views(self.flat)
 
     def forward(self, images_nhwc: torch.Tensor) -> torch.Tensor:
+        if self.backend == "hip_f32":
+            from ..ops.f32 import cnn_forward_f32
+            return cnn_forward_f32(images_nhwc, self.params(), self.relu_logits)
         return cnn_forward(images_nhwc, self.params(), self.relu_logits)
 
     def named_tf_variables(self) -> Dict[str, torch.Tensor]:
