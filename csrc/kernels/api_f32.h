@@ -11,8 +11,13 @@ extern "C" {
 // B stored [K,N] (ldb) or, with tb, B stored [N,K].  splits > 1: K is cut into `splits` chunks of
 // `kc` (multiple of 16) whose partial products go to ws[splits][M][N] and are summed in slice order
 // by a second kernel (deterministic).  ws may be null when splits == 1.
+// conv = 1 / 2: A is an NHWC activation and op(A) its implicit im2col matrix (no tb): geometry 1 =
+// [B][24][24][3], geometry 2 = [B][12][12][64], 5x5 taps, pad 2; rows = pixels (B*HW*HW), columns
+// (kh*5 + kw)*C + c, and column 25*C (if K or M reaches it) is the constant 1 (bias-gradient row).
+// With ta the product is im2col(A)^T op(B) (weight gradient); lda is unused.
 hipError_t dmlc_f32_gemm(const float* A, const float* B, const float* bias, float* C, float* ws, int M, int N,
-                         int K, int lda, int ldb, bool ta, bool tb, bool relu, int splits, int kc, hipStream_t s);
+                         int K, int lda, int ldb, bool ta, bool tb, bool relu, int splits, int kc, int conv,
+                         hipStream_t s);
 
 // im2col of a stride-1, zero-padded KHxKW convolution (TF 'SAME' for odd kernels: pad = k/2):
 // x NHWC [B,H,W,C] -> cols [B*H*W][KH*KW*C], column (kh*KW + kw)*C + c (the row order of an HWIO

@@ -13,8 +13,13 @@
 //  * deterministic split-K: slices write partial products, a second kernel sums them in slice
 //    order (+ bias, ReLU) -- the long-K weight gradients (K = B*H*W) get enough workgroups without
 //    atomics, so results are bitwise reproducible.
-//  * im2col / col2im (gather form, fixed tap order) for the stride-1 SAME 5x5 convolutions, and a
-//    two-pass column sum for the bias gradients.
+//  * implicit-GEMM convolutions (template CONV = the layer geometry): the A operand is the im2col
+//    matrix of an NHWC activation, gathered straight from it by the tile loader -- forward (cols W),
+//    weight gradient (cols^T dY, with an optional ones column whose output row is the bias
+//    gradient) and data gradient (im2col(dY) against the flipped, transposed weight) never
+//    materialise a column matrix;
+//  * explicit im2col / col2im (gather form, fixed tap order) for other geometries, and a two-pass
+//    column sum for the fc bias gradients.
 #include <algorithm>
 
 #include "common.h"
@@ -22,9 +27,65 @@
 
 namespace dmlc {
 
-constexpr int FT = 256, FBM = 64, FBN = 64, FBK = 16, FLD = 80;
+constexpr int FT = 256, FBM = 64, FBN = 64, FBK = 64, FLD = 80, FNE = FBK * 64 / FT;   // FNE: elements per thread per operand
 
 DEV f32x4 mfma_f32(float a, float b, const f32x4& c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// Implicit im2col geometry: x NHWC [B][HW][HW][CH], KSxKS taps, stride 1, zero padding KS/2;
+// column (kh*KS + kw)*CH + ci, plus (ones) a constant-1 column at index KS*KS*CH.
+template <int CONV> struct ConvGeom;
+template <> struct ConvGeom<1> { static constexpr int CH = 3, HW = 24, KS = 5; };    // conv1 input
+template <> struct ConvGeom<2> { static constexpr int CH = 64, HW = 12, KS = 5; };   // conv2 input / dY
+
+// Tile-loader state of the implicit im2col operand.  The loop-invariant half of every gathered
+// element is computed once per thread: with !TA the thread's 4 tile rows are fixed pixels
+// (b, y, x -> base offset), with TA its tile column is a fixed (tap, channel) -- so a k-step costs
+// one constant division (channel -> tap, or pixel -> y, x) and a bounds test per element.
+template <bool TA, int CONV>
+struct ConvA {
+  using Gm = ConvGeom<CONV>;
+  static constexpr int CH = Gm::CH, HW = Gm::HW, KS = Gm::KS, PAD = KS / 2, KC = KS * KS * CH;
+  int y[4], x[4], base[4];      // !TA: per tile row
+  int dy, dx, off;              // TA: the column's tap offsets
+  bool ones, colok;
+  MDEV void init(int M, int m0, int t) {
+    if constexpr (!TA) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gm = min(m0 + (t >> 4) + 16 * i, M - 1);
+        const int b = gm / (HW * HW), pp = gm - b * (HW * HW);
+        y[i] = pp / HW;
+        x[i] = pp - y[i] * HW;
+        base[i] = gm * CH;
+      }
+    } else {
+      const int col = m0 + (t & 63);
+      colok = col < M;
+      ones = col == KC;
+      const int c = min(col, KC - 1), tap = c / CH, ci = c - tap * CH, kh = tap / KS, kw = tap - kh * KS;
+      dy = kh - PAD;
+      dx = kw - PAD;
+      off = (dy * HW + dx) * CH + ci;
+    }
+  }
+  // element i of the thread's share of a k-step: op(A)(gm, gk); ok = inside the problem
+  MDEV float fetch(const float* X, int i, int gm, int gk, bool ok) const {
+    if constexpr (!TA) {                       // gk = im2col column of the fixed pixel row i
+      const int tap = gk / CH, ci = gk - tap * CH, kh = tap / KS, kw = tap - kh * KS;
+      const int iy = y[i] + kh - PAD, ix = x[i] + kw - PAD;
+      const bool in = ok && iy >= 0 && iy < HW && ix >= 0 && ix < HW;
+      const float v = X[in ? base[i] + ((kh - PAD) * HW + (kw - PAD)) * CH + ci : 0];
+      return in ? v : 0.f;
+    } else {                                   // gk = pixel of the fixed column (tap, channel)
+      (void)gm;
+      const int pp = gk % (HW * HW), yy = pp / HW, xx = pp - yy * HW;
+      const int iy = yy + dy, ix = xx + dx;
+      const bool in = ok && !ones && iy >= 0 && iy < HW && ix >= 0 && ix < HW;
+      const float v = X[in ? (int64_t)gk * CH + off : 0];
+      return ones ? (ok ? 1.f : 0.f) : (in ? v : 0.f);
+    }
+  }
+};
 
 struct F32GemmArgs {
   const float* A;
@@ -36,24 +97,39 @@ struct F32GemmArgs {
   bool relu;
 };
 
-// One K-step of operands in registers: thread t owns 4 elements of the 64x16 A tile and 4 of the
-// 16x64 B tile, mapped so that consecutive threads read consecutive addresses of the stored matrix.
-template <bool TA, bool TB>
+// One K-step of operands in registers: thread t owns FNE elements of the 64 x FBK A tile and FNE of
+// the FBK x 64 B tile, mapped so that consecutive threads read consecutive addresses of the stored
+// matrix (a k-contiguous operand: 16 k x 4 rows per thread-quad pattern; an m/n-contiguous one:
+// 64 consecutive m/n).  64 k per step: 256 MFMAs per workgroup between two global round trips.
+template <bool T>   // T: the 64-wide index is contiguous in memory
+DEV void tile_idx(int t, int i, int& mn, int& k) {
+  if (T) { mn = t & 63; k = (t >> 6) + 4 * i; }
+  else { mn = (t >> 4) + 16 * (i & 3); k = (t & 15) + 16 * (i >> 2); }
+}
+
+template <bool TA, bool TB, int CONV>
 struct F32Tile {
-  float a[4], b[4];
+  float a[FNE], b[FNE];
+  ConvA<TA, CONV == 0 ? 1 : CONV> cv;
   MDEV void load(const F32GemmArgs& p, int m0, int n0, int k0, int kend, int t) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = TA ? (t & 63) : (t >> 4) + 16 * i, k = TA ? (t >> 6) + 4 * i : (t & 15);
+    for (int i = 0; i < FNE; ++i) {
+      int m, k;
+      tile_idx<TA>(t, i, m, k);
       const int gm = m0 + m, gk = k0 + k;
       const bool ok = gm < p.M && gk < kend;
-      const int64_t off = TA ? (int64_t)gk * p.lda + gm : (int64_t)gm * p.lda + gk;
-      const float v = p.A[ok ? off : 0];
-      a[i] = ok ? v : 0.f;
+      if constexpr (CONV != 0) {                // op(A) = im2col(x) (pixel, column) or its transpose
+        a[i] = cv.fetch(p.A, i & 3, gm, gk, ok);
+      } else {
+        const int64_t off = TA ? (int64_t)gk * p.lda + gm : (int64_t)gm * p.lda + gk;
+        const float v = p.A[ok ? off : 0];
+        a[i] = ok ? v : 0.f;
+      }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = TB ? (t >> 4) + 16 * i : (t & 63), k = TB ? (t & 15) : (t >> 6) + 4 * i;
+    for (int i = 0; i < FNE; ++i) {
+      int n, k;
+      tile_idx<!TB>(t, i, n, k);
       const int gn = n0 + n, gk = k0 + k;
       const bool ok = gn < p.N && gk < kend;
       const int64_t off = TB ? (int64_t)gn * p.ldb + gk : (int64_t)gk * p.ldb + gn;
@@ -63,19 +139,21 @@ struct F32Tile {
   }
   MDEV void store(float* As, float* Bs, int t) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = TA ? (t & 63) : (t >> 4) + 16 * i, k = TA ? (t >> 6) + 4 * i : (t & 15);
+    for (int i = 0; i < FNE; ++i) {
+      int m, k;
+      tile_idx<TA>(t, i, m, k);
       As[k * FLD + m] = a[i];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = TB ? (t >> 4) + 16 * i : (t & 63), k = TB ? (t & 15) : (t >> 6) + 4 * i;
+    for (int i = 0; i < FNE; ++i) {
+      int n, k;
+      tile_idx<!TB>(t, i, n, k);
       Bs[k * FLD + n] = b[i];
     }
   }
 };
 
-template <bool TA, bool TB>
+template <bool TA, bool TB, int CONV>
 __global__ __launch_bounds__(FT) void k_gemm_f32(F32GemmArgs p) {
   __shared__ float As[FBK * FLD], Bs[FBK * FLD];
   const int t = threadIdx.x, lane = t & 63, w = wave_id();
@@ -87,14 +165,15 @@ __global__ __launch_bounds__(FT) void k_gemm_f32(F32GemmArgs p) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = zero4();
-  F32Tile<TA, TB> tile;
+  F32Tile<TA, TB, CONV> tile;
+  if constexpr (CONV != 0) tile.cv.init(p.M, m0, t);
   tile.load(p, m0, n0, kbeg, kend, t);
   for (int k0 = kbeg; k0 < kend; k0 += FBK) {
     tile.store(As, Bs, t);
     __syncthreads();
     if (k0 + FBK < kend) tile.load(p, m0, n0, k0 + FBK, kend, t);   // next step under the MFMAs
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
+    for (int kk = 0; kk < FBK / 4; ++kk) {
       const float* ar = As + (4 * kk + q) * FLD + wm + r;
       const float* br = Bs + (4 * kk + q) * FLD + wn + r;
       const float a0 = ar[0], a1 = ar[16], b0 = br[0], b1 = br[16];
@@ -198,15 +277,23 @@ using namespace dmlc;
 extern "C" {
 
 hipError_t dmlc_f32_gemm(const float* A, const float* B, const float* bias, float* C, float* ws, int M, int N,
-                         int K, int lda, int ldb, bool ta, bool tb, bool relu, int splits, int kc, hipStream_t s) {
+                         int K, int lda, int ldb, bool ta, bool tb, bool relu, int splits, int kc, int conv,
+                         hipStream_t s) {
   if (M <= 0 || N <= 0 || K <= 0 || splits < 1 || kc % FBK || (int64_t)splits * kc < K || (splits > 1 && !ws))
     return hipErrorInvalidValue;
+  if (conv < 0 || conv > 2 || (conv && tb)) return hipErrorInvalidValue;
   F32GemmArgs p{A, B, bias, C, ws, M, N, K, lda, ldb, splits, kc, relu};
   const dim3 grid((M + FBM - 1) / FBM, (N + FBN - 1) / FBN, splits);
-  if (ta && tb) hipLaunchKernelGGL((k_gemm_f32<true, true>), grid, dim3(FT), 0, s, p);
-  else if (ta) hipLaunchKernelGGL((k_gemm_f32<true, false>), grid, dim3(FT), 0, s, p);
-  else if (tb) hipLaunchKernelGGL((k_gemm_f32<false, true>), grid, dim3(FT), 0, s, p);
-  else hipLaunchKernelGGL((k_gemm_f32<false, false>), grid, dim3(FT), 0, s, p);
+  if (conv == 1) {
+    if (ta) hipLaunchKernelGGL((k_gemm_f32<true, false, 1>), grid, dim3(FT), 0, s, p);
+    else hipLaunchKernelGGL((k_gemm_f32<false, false, 1>), grid, dim3(FT), 0, s, p);
+  } else if (conv == 2) {
+    if (ta) hipLaunchKernelGGL((k_gemm_f32<true, false, 2>), grid, dim3(FT), 0, s, p);
+    else hipLaunchKernelGGL((k_gemm_f32<false, false, 2>), grid, dim3(FT), 0, s, p);
+  } else if (ta && tb) hipLaunchKernelGGL((k_gemm_f32<true, true, 0>), grid, dim3(FT), 0, s, p);
+  else if (ta) hipLaunchKernelGGL((k_gemm_f32<true, false, 0>), grid, dim3(FT), 0, s, p);
+  else if (tb) hipLaunchKernelGGL((k_gemm_f32<false, true, 0>), grid, dim3(FT), 0, s, p);
+  else hipLaunchKernelGGL((k_gemm_f32<false, false, 0>), grid, dim3(FT), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || splits == 1) return e;
   const int64_t mn = (int64_t)M * N;

@@ -166,8 +166,8 @@ class CifarCNN(nn.Module):
 
     def forward(self, images_nhwc: torch.Tensor) -> torch.Tensor:
         if self.backend == "hip_f32":
-            from ..ops.f32 import cnn_forward_f32
-            return cnn_forward_f32(images_nhwc, self.params(), self.relu_logits)
+            from ..ops.f32 import cnn_forward_f32, flat_views
+            return cnn_forward_f32(images_nhwc, flat_views(self.flat, self.specs), self.relu_logits)
         return cnn_forward(images_nhwc, self.params(), self.relu_logits)
 
     def named_tf_variables(self) -> Dict[str, torch.Tensor]:

@@ -61,6 +61,39 @@ def test_im2col_col2im_are_adjoint_and_match_conv():
     assert abs(lhs - rhs) / abs(rhs) < 1e-5
 
 
+@pytest.mark.parametrize("H,C,CO", [(24, 3, 64), (12, 64, 64)])
+def test_implicit_conv_gemm_matches_explicit_im2col(H, C, CO):
+    ops = _ops()
+    B = 5
+    g = torch.Generator(device="cuda").manual_seed(H)
+    x = torch.randn(B, H, H, C, device="cuda", generator=g)
+    w = torch.randn(25 * C, CO, device="cuda", generator=g) * 0.05
+    dy = torch.randn(B * H * H, CO, device="cuda", generator=g)
+    cols = ops.f32_im2col(x, 5, 5, 2).double()
+    y = ops.f32_conv_gemm(x, w, None, False, False)
+    assert _rel(y, cols @ w.double()) < 2e-6
+    gwb = ops.f32_conv_gemm(x, dy, None, True, True)          # [25C + 1, CO]: weights + bias row
+    assert gwb.shape == (25 * C + 1, CO)
+    assert _rel(gwb[:25 * C], cols.t() @ dy.double()) < 2e-6
+    assert _rel(gwb[25 * C], dy.double().sum(0)) < 2e-6
+    assert torch.equal(gwb, ops.f32_conv_gemm(x, dy, None, True, True))
+
+
+def test_implicit_conv_autograd_matches_explicit_path():
+    from dmlc.ops import f32 as F32
+    g = torch.Generator(device="cuda").manual_seed(1)
+    x = torch.randn(4, 12, 12, 64, device="cuda", generator=g, requires_grad=True)
+    w = (torch.randn(5, 5, 64, 64, device="cuda", generator=g) * 0.05).requires_grad_()
+    b = torch.randn(64, device="cuda", generator=g, requires_grad=True)
+    outs = []
+    for implicit in (True, False):
+        y = F32.conv_same(x, w, b, implicit=implicit)
+        gx, gw, gb = torch.autograd.grad((y * y).sum(), (x, w, b))
+        outs.append((y.detach(), gx, gw, gb))
+    for a, e in zip(outs[0], outs[1]):
+        assert _rel(a, e) < 1e-5
+
+
 def test_colsum_is_fixed_order_and_exact_enough():
     ops = _ops()
     for M_, N_ in [(147456, 64), (256, 384), (5, 10), (1000, 1)]:
