@@ -211,6 +211,15 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
   float* red = reinterpret_cast<float*>(smem + F::XB);          // [4][2][64]
   float* cf = red + 4 * 2 * 64;                                  // [2][64] BN scale / shift of layer l-1
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15;
+  // timing build only (tools/rn_ktiming.py): phases of the stage-1 16->16 forward, kernel id 0
+  constexpr bool TS = CIN == 16 && COUT == 16 && S == 1;
+  if (TS) DMLC_STAMP(0, 0);
+  // weight fragments first (independent of everything): their latency overlaps the prologue's
+  const int ct = w % F::CT, pt0 = w / F::CT;
+  const bf16* W = reinterpret_cast<const bf16*>(a.w) + (16 * ct + li) * KP + 8 * g;
+  bf16x8 wa[F::KS];
+#pragma unroll
+  for (int ks = 0; ks < F::KS; ++ks) wa[ks] = glb_b128(W + 32 * ks);
 
   // ---- prologue: padded input image (stem: dataset gather; else BN-apply of layer l-1) ----
   if constexpr (CIN == 3) {
@@ -230,13 +239,6 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
   } else {
     constexpr int C8 = CIN / 8;
     const int c8 = tid % C8;                  // fixed channel chunk of this thread (RT % C8 == 0)
-    if (tid < CIN) {                          // BN_{l-1} coefficients, once per block
-      float mean, rstd;
-      bn_mean_rstd(a.stat_prev, tid, a.inv_n_prev, mean, rstd);
-      const float sc = a.gamma_prev[tid] * rstd;
-      cf[tid] = sc;
-      cf[64 + tid] = a.beta_prev[tid] - mean * sc;
-    }
     const uint4* zp = reinterpret_cast<const uint4*>(a.z_prev) + (size_t)b * HIN * HIN * C8;
     const uint4* ss = reinterpret_cast<const uint4*>(a.sc_src);
     uint4 zv[F::IT], sv[F::IT];
@@ -255,6 +257,15 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
         const uint4 v = ss[q];
         sv[i] = lowc ? v : make_uint4(0, 0, 0, 0);
       }
+    }
+    // BN_{l-1} coefficients, once per block: the statistics reads go out behind the image loads
+    // (computed first, they added a dependent memory round trip to the prologue)
+    if (tid < CIN) {
+      float mean, rstd;
+      bn_mean_rstd(a.stat_prev, tid, a.inv_n_prev, mean, rstd);
+      const float sc = a.gamma_prev[tid] * rstd;
+      cf[tid] = sc;
+      cf[64 + tid] = a.beta_prev[tid] - mean * sc;
     }
     lds_barrier();
     float sc[8], sh[8];
@@ -282,13 +293,9 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
       }
     }
   }
-  // weight fragments of this wave's c_out tile
-  const int ct = w % F::CT, pt0 = w / F::CT;
-  const bf16* W = reinterpret_cast<const bf16*>(a.w) + (16 * ct + li) * KP + 8 * g;
-  bf16x8 wa[F::KS];
-#pragma unroll
-  for (int ks = 0; ks < F::KS; ++ks) wa[ks] = glb_b128(W + 32 * ks);
+  if (TS) DMLC_STAMP(0, 1);                       // 1: input image staged (BN-apply done)
   __syncthreads();
+  if (TS) DMLC_STAMP(0, 2);                       // 2: weights in registers, barrier passed
 
   // ---- implicit GEMM: C[co][px] = sum_k W[co][k] X[px][k] ----
   f32x4 acc[F::NPT];
@@ -308,6 +315,7 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
       acc[i] = mfma16(wa[ks], bx, acc[i]);
     }
   }
+  if (TS) DMLC_STAMP(0, 3);                       // 3: MFMAs issued
   // ---- epilogue: z (bf16) + BN partial sums ----
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   bf16* zo = reinterpret_cast<bf16*>(a.z) + (size_t)b * HOUT * HOUT * COUT;
@@ -318,7 +326,9 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s1[r] += acc[i][r]; s2[r] += acc[i][r] * acc[i][r]; }
   }
+  if (TS) DMLC_STAMP(0, 4);                       // 4: z stored, partial sums ready
   reduce_flush<F::CT, COUT>(s1, s2, red, a.stat, w, g, li, tid, a.stat_det, a.B);
+  if (TS) DMLC_STAMP(0, 5);                       // 5: statistics flushed (end)
 }
 
 // ================================ dgrad ========================================================
@@ -343,6 +353,8 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
   float* red = reinterpret_cast<float*>(smem + D::GB);           // [4][2][64]
   float* cf = red + 4 * 2 * 64;                                   // [5][64]: A, Bc, Cc (layer l); mean, rstd (l-1)
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15;
+  constexpr bool TS = CIN == 16 && COUT == 16 && S == 1;   // timing build: stage-1 dgrad, kernel id 1
+  if (TS) DMLC_STAMP(1, 0);
 
   if (tid < COUT) {
     float A, Bc, Cc;
@@ -402,6 +414,36 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
 #pragma unroll
   for (int ks = 0; ks < D::KS; ++ks) wa[ks] = glb_b128(Wd + 32 * ks);
   __syncthreads();
+  if (TS) DMLC_STAMP(1, 1);                       // 1: g_z staged, weights in registers
+
+  // Epilogue operands of layer l-1 (activation for the ReLU mask, z for x-hat, the shortcut's g_y),
+  // 4 pixel tiles per chunk, software-pipelined: chunk 0 is issued here, under the MFMAs, and chunk
+  // c+1 before chunk c's stores.  (Loaded inside the store loop, every tile paid a full memory
+  // latency -- the stores may alias the loads -- 11 of the kernel's 22 us at 16 tiles per wave.)
+  struct EpiIn { uint2 a, z, s; };
+  constexpr int EC = D::NPT < 4 ? D::NPT : 4;
+  const int c0 = 16 * ct + 4 * g;
+  const bf16* ap = reinterpret_cast<const bf16*>(a.a_prev) + (size_t)b * HIN * HIN * CIN;
+  const bf16* zpp = reinterpret_cast<const bf16*>(a.z_prev) + (size_t)b * HIN * HIN * CIN;
+  auto epi_load = [&](int i, EpiIn& e) {
+    const int px = 16 * (pt0 + D::WPC * i) + li;
+    const int iy = px / HIN, ix = px - (px / HIN) * HIN;
+    e.a = *reinterpret_cast<const uint2*>(ap + px * CIN + c0);
+    e.z = *reinterpret_cast<const uint2*>(zpp + px * CIN + c0);
+    e.s = make_uint2(0u, 0u);
+    if (a.sc_mode == 1) {
+      e.s = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.gy_sc) + ((size_t)b * HIN * HIN + px) * CIN + c0);
+    } else if (a.sc_mode == 2) {
+      const bool even = !(iy & 1) && !(ix & 1);
+      const int HB = HIN / 2;
+      const size_t q = ((size_t)b * HB * HB + (even ? (iy / 2) * HB + ix / 2 : 0)) * (2 * CIN) + c0;
+      const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.gy_sc) + q);
+      e.s = even ? v : make_uint2(0u, 0u);
+    }
+  };
+  EpiIn cur[EC];
+#pragma unroll
+  for (int j = 0; j < EC; ++j) epi_load(j, cur[j]);
 
   // ---- C[ci][px_in] = sum_{tap', co} Wd[ci][tap'*COUT + co] G[(iy+kh')*HPD + ix + kw'][co] ----
   f32x4 acc[D::NPT];
@@ -422,45 +464,45 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
     }
   }
 
+  if (TS) DMLC_STAMP(1, 2);                       // 2: MFMAs issued
   // ---- epilogue: g_a_{l-1} (+ shortcut) -> g_y_{l-1} + its BN reductions ----
-  const int c0 = 16 * ct + 4 * g;
   float mean[4], rstd[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) { mean[r] = cf[192 + c0 + r]; rstd[r] = cf[256 + c0 + r]; }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-  const bf16* ap = reinterpret_cast<const bf16*>(a.a_prev) + (size_t)b * HIN * HIN * CIN;
-  const bf16* zpp = reinterpret_cast<const bf16*>(a.z_prev) + (size_t)b * HIN * HIN * CIN;
   bf16* gyo = reinterpret_cast<bf16*>(a.gy_prev) + (size_t)b * HIN * HIN * CIN;
 #pragma unroll
-  for (int i = 0; i < D::NPT; ++i) {
-    const int px = 16 * (pt0 + D::WPC * i) + li;
-    const int iy = px / HIN, ix = px - (px / HIN) * HIN;
-    const uint2 av = *reinterpret_cast<const uint2*>(ap + px * CIN + c0);
-    const uint2 zv = *reinterpret_cast<const uint2*>(zpp + px * CIN + c0);
-    float sc4[4] = {0.f, 0.f, 0.f, 0.f};
-    if (a.sc_mode == 1) {
-      const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.gy_sc) +
-                                                     ((size_t)b * HIN * HIN + px) * CIN + c0);
-      sc4[0] = bf16_lo(v.x); sc4[1] = bf16_hi(v.x); sc4[2] = bf16_lo(v.y); sc4[3] = bf16_hi(v.y);
-    } else if (a.sc_mode == 2) {
-      const bool even = !(iy & 1) && !(ix & 1);
-      const int HB = HIN / 2;
-      const size_t q = ((size_t)b * HB * HB + (even ? (iy / 2) * HB + ix / 2 : 0)) * (2 * CIN) + c0;
-      const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.gy_sc) + q);
-      if (even) { sc4[0] = bf16_lo(v.x); sc4[1] = bf16_hi(v.x); sc4[2] = bf16_lo(v.y); sc4[3] = bf16_hi(v.y); }
-    }
-    const float av4[4] = {bf16_lo(av.x), bf16_hi(av.x), bf16_lo(av.y), bf16_hi(av.y)};
-    const float zv4[4] = {bf16_lo(zv.x), bf16_hi(zv.x), bf16_lo(zv.y), bf16_hi(zv.y)};
-    float gy[4];
+  for (int c = 0; c < D::NPT; c += EC) {
+    EpiIn nxt[EC];
+    if (c + EC < D::NPT) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      gy[r] = av4[r] > 0.f ? acc[i][r] + sc4[r] : 0.f;
-      s1[r] += gy[r];
-      s2[r] += gy[r] * (zv4[r] - mean[r]) * rstd[r];
+      for (int j = 0; j < EC; ++j) epi_load(c + EC + j, nxt[j]);
     }
-    *reinterpret_cast<bf16x4*>(gyo + px * CIN + c0) = pack4(gy[0], gy[1], gy[2], gy[3]);
+#pragma unroll
+    for (int j = 0; j < EC; ++j) {
+      const int i = c + j;
+      const int px = 16 * (pt0 + D::WPC * i) + li;
+      const uint2 av = cur[j].a, zv = cur[j].z, sv = cur[j].s;
+      const float sc4[4] = {bf16_lo(sv.x), bf16_hi(sv.x), bf16_lo(sv.y), bf16_hi(sv.y)};
+      const float av4[4] = {bf16_lo(av.x), bf16_hi(av.x), bf16_lo(av.y), bf16_hi(av.y)};
+      const float zv4[4] = {bf16_lo(zv.x), bf16_hi(zv.x), bf16_lo(zv.y), bf16_hi(zv.y)};
+      float gy[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gy[r] = av4[r] > 0.f ? acc[i][r] + sc4[r] : 0.f;
+        s1[r] += gy[r];
+        s2[r] += gy[r] * (zv4[r] - mean[r]) * rstd[r];
+      }
+      *reinterpret_cast<bf16x4*>(gyo + px * CIN + c0) = pack4(gy[0], gy[1], gy[2], gy[3]);
+    }
+    if (c + EC < D::NPT) {
+#pragma unroll
+      for (int j = 0; j < EC; ++j) cur[j] = nxt[j];
+    }
   }
+  if (TS) DMLC_STAMP(1, 3);                       // 3: g_y stored, partial sums ready
   reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid, a.red_det, a.B);
+  if (TS) DMLC_STAMP(1, 4);                       // 4: reductions flushed (end)
 }
 
 // ================================ wgrad ========================================================
@@ -499,6 +541,8 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
   float* cf = reinterpret_cast<float*>(gz + NB * G::GE);          // [3][64]
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int b0 = grp * a.B / a.G, b1 = (grp + 1) * a.B / a.G;
+  constexpr bool TS = CIN == 16 && COUT == 16 && S == 1;   // timing build: stage-1 wgrad, kernel id 2
+  if (TS) DMLC_STAMP(2, 0);
 
   if (tid < COUT) {
     float A, Bc, Cc;
@@ -580,6 +624,7 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
       }
     }
     __syncthreads();
+    if (TS && bb == b0) DMLC_STAMP(2, 1);         // 1: first staging step in LDS
     // ---- MFMA over the staged images' pixels ----
     for (int im = 0; im < nb; ++im) {
       const bf16* xi = xs + im * G::XE;
@@ -608,6 +653,7 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
       }
     }
   }
+  if (TS) DMLC_STAMP(2, 2);                       // 2: all MFMAs issued
   // slab rows k = 16m + 4g + i, cols co = 16n + li
   float* out = a.part + (size_t)grp * KP * COUT;
 #pragma unroll
@@ -620,6 +666,7 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
         for (int i = 0; i < 4; ++i) out[(16 * m + 4 * g + i) * COUT + 16 * n + li] = acc[j][n][i];
     }
   }
+  if (TS) DMLC_STAMP(2, 3);                       // 3: slab written (end)
 }
 
 template <int CIN, int COUT, int HIN, int S>
