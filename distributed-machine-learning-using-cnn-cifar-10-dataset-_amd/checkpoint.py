@@ -11,8 +11,11 @@ the latest checkpoint on start-up.  This module reproduces that on-disk contract
 
 Keys: the 10 ``model_definition/...`` variables in TF layouts (HWIO conv kernels, [in,out] fc
 weights, ``full_weight_1`` rows in NHWC flatten order), ``global_step`` (int64 scalar) and
-``Variable`` (int32 scalar = the reference's ``generation_num``, :216).  The ``.meta`` MetaGraphDef
-is TF-graph specific and is not written (documented deviation).
+``Variable`` (int32 scalar = the reference's ``generation_num``, :216).
+
+With ``graph_info`` the manager also writes what the TF1 hooks write beside the checkpoints:
+``<log_dir>/graph.pbtxt`` (once) and ``model.ckpt-N.meta`` (a MetaGraphDef per checkpoint, removed
+with it): the reference model as a TF1 graph with a V2 saver (utils/metagraph.py).
 """
 from __future__ import annotations
 
@@ -123,8 +126,10 @@ class CheckpointManager:
     """Chief-side saver: TF1 CheckpointSaverHook semantics (save at start, every ``secs`` seconds and
     at the end; keep the newest ``max_to_keep``)."""
 
-    def __init__(self, log_dir: str, max_to_keep: int = 5, secs: float = 600.0):
+    def __init__(self, log_dir: str, max_to_keep: int = 5, secs: float = 600.0, graph_info: Optional[dict] = None):
         self.log_dir = os.path.abspath(log_dir)
+        self.graph_info = graph_info       # model / batch / crop / relu_logits for graph.pbtxt + .meta
+        self._meta = None
         self.max_to_keep = max_to_keep
         self.secs = secs
         self.last_save = None
@@ -137,6 +142,12 @@ class CheckpointManager:
     def save(self, step: int, tensors: Dict[str, torch.Tensor]) -> str:
         prefix = os.path.join(self.log_dir, f"{PREFIX}-{int(step)}")
         write_bundle(prefix, tensors)
+        if self.graph_info is not None:
+            from .utils import metagraph as MG
+            if self._meta is None:            # the variables never change: build once
+                self._meta = MG.build_meta_graph(tensors, max_to_keep=self.max_to_keep, **self.graph_info)
+                MG.write_graph_pbtxt(self.log_dir, self._meta)
+            MG.write_meta(prefix, self._meta)
         self.kept = [p for p in self.kept if p != prefix] + [prefix]
         while self.max_to_keep and len(self.kept) > self.max_to_keep:
             old = self.kept.pop(0)

@@ -277,7 +277,9 @@ class Session:
         self.tracer = Tracer(cfg.trace, cfg.log_dir, cfg.trace_steps, max(0, info.rank))
         if self.chief and cfg.log_dir:
             if cfg.save_checkpoints:
-                self.ckpt = CK.CheckpointManager(cfg.log_dir, cfg.max_to_keep, cfg.checkpoint_secs)
+                self.ckpt = CK.CheckpointManager(
+                    cfg.log_dir, cfg.max_to_keep, cfg.checkpoint_secs,
+                    graph_info=dict(model=cfg.model, batch=cfg.batch_size, crop=cfg.crop, relu_logits=cfg.relu_logits))
             self.events = EventsWriter(cfg.log_dir)
             self.metrics = MetricsLog(cfg.metrics_file or os.path.join(cfg.log_dir, "metrics.jsonl"))
 
