@@ -626,30 +626,54 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
     __syncthreads();
     if (TS && bb == b0) DMLC_STAMP(2, 1);         // 1: first staging step in LDS
     // ---- MFMA over the staged images' pixels ----
+    // Software-pipelined: the next k-step's fragments (ds_read_b64_tr_b16) are read under this
+    // k-step's MFMAs -- with the reads in line, every k-step waited one LDS latency (the phase took
+    // 7 us for one 32x32x16 image, tools/rn_ktiming.py).  The wave's m-tiles are loop-invariant.
+    int moff[G::MJ], mci[G::MJ];
+    bool mok[G::MJ];
+#pragma unroll
+    for (int j = 0; j < G::MJ; ++j) {
+      const int m = mc * G::MCH + w + 4 * j;
+      mok[j] = w + 4 * j < G::MCH && m < G::MT;          // wave-uniform
+      int tap, ci0;
+      if (CINP >= 16) { tap = (16 * m) / CINP; ci0 = (16 * m) % CINP + 4 * p; }
+      else { tap = 2 * m + (p >> 1); ci0 = 4 * (p & 1); }
+      tap = min(tap, 8);
+      const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+      moff[j] = kh * HP + kw;
+      mci[j] = ci0;
+    }
     for (int im = 0; im < nb; ++im) {
       const bf16* xi = xs + im * G::XE;
       const bf16* gi = gz + im * G::GE;
-      for (int s = 0; s < G::KSTEPS; ++s) {
+      auto frags = [&](int s, bf16x8 (&bf)[NT], bf16x8 (&af)[G::MJ]) {
         const int rA = 32 * s + 8 * g + q, rB = rA + 4;
-        bf16x8 bf[NT];
 #pragma unroll
         for (int n = 0; n < NT; ++n) bf[n] = tr_frag(gi + rA * GLD + 16 * n + 4 * p, gi + rB * GLD + 16 * n + 4 * p);
         const int oyA = rA / HOUT, oxA = rA - oyA * HOUT, oyB = rB / HOUT, oxB = rB - oyB * HOUT;
         const int pA = (oyA * S) * HP + oxA * S, pB = (oyB * S) * HP + oxB * S;
 #pragma unroll
-        for (int j = 0; j < G::MJ; ++j) {
-          const int m = mc * G::MCH + w + 4 * j;
-          if (w + 4 * j < G::MCH && m < G::MT) {
-            int tap, ci0;
-            if (CINP >= 16) { tap = (16 * m) / CINP; ci0 = (16 * m) % CINP + 4 * p; }
-            else { tap = 2 * m + (p >> 1); ci0 = 4 * (p & 1); }
-            tap = min(tap, 8);
-            const int kh = tap / 3, kw = tap - 3 * (tap / 3), off = kh * HP + kw;
-            const bf16x8 af = tr_frag(xi + (pA + off) * CINP + ci0, xi + (pB + off) * CINP + ci0);
+        for (int j = 0; j < G::MJ; ++j)
+          if (mok[j]) af[j] = tr_frag(xi + (pA + moff[j]) * CINP + mci[j], xi + (pB + moff[j]) * CINP + mci[j]);
+      };
+      bf16x8 bf[NT], af[G::MJ];
+      frags(0, bf, af);
+      for (int s = 0; s < G::KSTEPS; ++s) {
+        bf16x8 bn[NT], an[G::MJ];
+        wait_lds();                                  // step s's fragments have landed
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 < G::KSTEPS) frags(s + 1, bn, an);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int n = 0; n < NT; ++n) acc[j][n] = mfma16(af, bf[n], acc[j][n]);
+        for (int j = 0; j < G::MJ; ++j)
+          if (mok[j]) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) acc[j][n] = mfma16(af[j], bf[n], acc[j][n]);
           }
-        }
+#pragma unroll
+        for (int n = 0; n < NT; ++n) bf[n] = bn[n];
+#pragma unroll
+        for (int j = 0; j < G::MJ; ++j) af[j] = an[j];
       }
     }
   }
@@ -682,7 +706,7 @@ __global__ __launch_bounds__(RT) void k_rn_wgrad(DmlcRnWgradArgs a) {
 // launch, so the BN-reduction slots are unchanged), the rest the wgrad body (group, m-chunk).  One
 // launch per layer instead of two, with no stream fork/join in the step graph.
 template <int CIN, int COUT, int HIN, int S>
-__global__ __launch_bounds__(RT) void k_rn_bwd(DmlcRnDgradArgs d, DmlcRnWgradArgs w) {
+__global__ __launch_bounds__(RT, 2) void k_rn_bwd(DmlcRnDgradArgs d, DmlcRnWgradArgs w) {
   if ((int)blockIdx.x < d.B) {
     rn_dgrad_body<CIN, COUT, HIN, S>(d);
   } else {
