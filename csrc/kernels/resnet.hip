@@ -102,21 +102,26 @@ DEV void det_flush(float t1, float t2, double* dst, float* det, int nblk, int ti
   }
   __syncthreads();
   if (!flag[0]) return;
-  // the group's rows: 8 loads in flight per thread (independent relaxed atomics), summed in block
-  // order; 2 threads per statistic each take every other row, combined in fixed order through LDS
-  __shared__ double part2[2][128];
-  const int e = tid & 127, h = tid >> 7;              // statistic, half of the group's rows
+  // the group's rows: T = 256 / (2C) threads per statistic (8 / 4 / 2 for 16 / 32 / 64 channels),
+  // thread h of a statistic sums rows h, h+T, ... in order, 8 loads in flight; the T partials are
+  // combined in fixed order through LDS.  At B = 256 (32 rows per group) that is ONE memory round
+  // trip for the 16- and 32-channel layers (two threads per statistic took two).
+  constexpr int NSTAT = 2 * C, T = 256 / NSTAT;
+  static_assert(256 % NSTAT == 0 && RT == 256, "det_flush: statistics must tile the 256 threads");
+  __shared__ double partT[256];
+  const int st = tid / T, h = tid - st * T;
+  const int e = st < C ? st : 64 + (st - C);          // row position of the statistic
   const int rows = (nblk - slot + NSLOT - 1) / NSLOT;
-  // device-coherent (sc1) loads, 8 in flight per thread: issued as one asm block (the compiler puts a
-  // vmcnt(0) behind every atomic load), rows past the group clamped to row `slot` and weighted 0
+  // device-coherent (sc1) loads issued as one asm block (the compiler puts a vmcnt(0) behind every
+  // atomic load), rows past the group clamped to row 0 of the slot and weighted 0
   double s = 0.0;
-  if (tid < 256 && (e & 63) < C) {
-    for (int r0 = h; r0 < rows; r0 += 16) {
+  if (tid < 256) {
+    for (int r0 = h; r0 < rows; r0 += 8 * T) {
       const float* p[8];
       float v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int r = r0 + 2 * u < rows ? r0 + 2 * u : 0;
+        const int r = r0 + T * u < rows ? r0 + T * u : 0;
         p[u] = det + (size_t)(slot + NSLOT * r) * 128 + e;
       }
       asm volatile(
@@ -133,12 +138,17 @@ DEV void det_flush(float t1, float t2, double* dst, float* det, int nblk, int ti
           : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
           : "memory");
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += r0 + 2 * u < rows ? (double)v[u] : 0.0;
+      for (int u = 0; u < 8; ++u) s += r0 + T * u < rows ? (double)v[u] : 0.0;
     }
+    partT[tid] = s;
   }
-  if (tid < 256) part2[h][e] = s;
   __syncthreads();
-  if (tid < 128 && (e & 63) < C) dst[slot * 128 + e] = part2[0][e] + part2[1][e];
+  if (tid < NSTAT) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < T; ++k) acc += partT[tid * T + k];
+    dst[slot * 128 + (tid < C ? tid : 64 + tid - C)] = acc;
+  }
 }
 
 // block-level channel reduction of per-lane partials (lanes with equal li share a channel group) and
