@@ -241,8 +241,11 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
             at::IntArrayRef mv_off, int64_t fcw_off, int64_t fcb_off, at::TensorList part, at::TensorList wf,
             at::TensorList wd, const Tensor& stat, const Tensor& red, const Tensor& fc_part, const Tensor& loss_img,
             const Tensor& correct_img, const Tensor& step, const Tensor& ticket, const Tensor& stats, int64_t mode,
-            double lr0, double decay, double decay_steps, bool staircase, double bn_momentum, double warmup) {
+            double lr0, double decay, double decay_steps, bool staircase, double bn_momentum, double warmup,
+            int64_t layer_lo, int64_t layer_hi, bool tail) {
   constexpr int L = DMLC_RN_LAYERS;
+  TORCH_CHECK(layer_lo >= 0 && layer_lo <= layer_hi && layer_hi <= L, "rn_sgd: bad layer range");
+  TORCH_CHECK(tail || mode == 0, "rn_sgd: a partial (tail=False) launch is mode 0 only");
   TORCH_CHECK(mode >= 0 && mode <= 3, "rn_sgd mode must be 0..3");
   TORCH_CHECK(conv_off.size() == L && gamma_off.size() == L && beta_off.size() == L && mm_off.size() == L &&
                   mv_off.size() == L, "rn_sgd: 19 offsets per table");
@@ -295,6 +298,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
   a.state = state.data_ptr<float>(); a.bn_momentum = (float)bn_momentum;
   a.fcw_off = (int)fcw_off; a.fcb_off = (int)fcb_off; a.fc_part = fc_part.data_ptr<float>(); a.B = (int)B;
   a.mode = (int)mode;
+  a.layer_lo = (int)layer_lo; a.layer_hi = (int)layer_hi; a.tail = tail ? 1 : 0;
   a.step = step.data_ptr<int64_t>(); a.lr0 = (float)lr0; a.decay = (float)decay; a.decay_steps = (float)decay_steps;
   a.staircase = staircase ? 1 : 0;
   a.warmup = (float)warmup;
@@ -328,7 +332,8 @@ TORCH_LIBRARY_FRAGMENT(dmlc, m) {
         "int[] gamma_off, int[] beta_off, int[] mm_off, int[] mv_off, int fcw_off, int fcb_off, Tensor[] part, "
         "Tensor(d!)[] wf, Tensor(e!)[] wd, Tensor stat, Tensor red, Tensor fc_part, Tensor loss_img, "
         "Tensor correct_img, Tensor(f!) step, Tensor(g!) ticket, Tensor(h!) stats, int mode, float lr0, "
-        "float decay, float decay_steps, bool staircase, float bn_momentum, float warmup=0.0) -> ()");
+        "float decay, float decay_steps, bool staircase, float bn_momentum, float warmup=0.0, int layer_lo=0, "
+        "int layer_hi=19, bool tail=True) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

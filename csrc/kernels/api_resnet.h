@@ -88,6 +88,10 @@ struct DmlcRnSgdArgs {
   int blk_start[DMLC_RN_LAYERS + 3];   // block ranges (set by the launcher): conv layers, fc, BN layers
   int split[DMLC_RN_LAYERS + 1];       // slab split factor per conv layer + fc (set by the launcher)
   int mode;                  // 0 reduce+apply, 1 reduce->grad, 2 apply grad, 3 shadows only
+  // conv layers [layer_lo, layer_hi) only; tail = also the fc / BN parameters, the BN running
+  // statistics and the step publication (a partial launch of the conv layers whose weight gradients
+  // are complete can run on a graph branch beside the rest of the backward)
+  int layer_lo, layer_hi, tail;
   int64_t* step; float lr0, decay, decay_steps; int staircase;
   float warmup;             // linear LR warm-up steps (0: none)
   unsigned int* ticket;

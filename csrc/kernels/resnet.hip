@@ -921,7 +921,7 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
         }
       }
     }
-  } else if (mode != 3) {                        // BN layer L: gamma/beta + running statistics
+  } else if (mode != 3 && a.tail) {               // BN layer L: gamma/beta + running statistics
     const int L = blk - a.blk_start[NL + 1];
     const int c = tid;
     if (c < a.cout[L]) {
@@ -962,7 +962,7 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
       }
     }
   }
-  if (!apply) return;
+  if (!apply || !a.tail) return;                 // a partial (layer-range) launch publishes nothing
   __syncthreads();
   if (tid == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1092,19 +1092,22 @@ static int split_for(int n) {                 // slabs per thread <= 8
 }
 
 hipError_t dmlc_rn_sgd(DmlcRnSgdArgs* a, hipStream_t s) {
+  if (a->layer_lo < 0 || a->layer_hi > DMLC_RN_LAYERS || a->layer_lo > a->layer_hi) return hipErrorInvalidValue;
+  if (!a->tail && (a->mode == 1 || a->mode == 2 || a->mode == 3)) return hipErrorInvalidValue;   // partial: mode 0
   int blocks = 0;
-  for (int l = 0; l < DMLC_RN_LAYERS; ++l) {
+  for (int l = 0; l < DMLC_RN_LAYERS; ++l) {      // layers outside the range get no blocks
     a->split[l] = split_for(a->G[l]);
     a->blk_start[l] = blocks;
     const int O = RT / a->split[l];
-    blocks += (9 * a->cin[l] * a->cout[l] / 4 + O - 1) / O;
+    if (l >= a->layer_lo && l < a->layer_hi) blocks += (9 * a->cin[l] * a->cout[l] / 4 + O - 1) / O;
   }
   a->split[DMLC_RN_LAYERS] = split_for(a->B);
   a->blk_start[DMLC_RN_LAYERS] = blocks;                     // fc
-  blocks += (164 + RT / a->split[DMLC_RN_LAYERS] - 1) / (RT / a->split[DMLC_RN_LAYERS]);
+  if (a->tail) blocks += (164 + RT / a->split[DMLC_RN_LAYERS] - 1) / (RT / a->split[DMLC_RN_LAYERS]);
   a->blk_start[DMLC_RN_LAYERS + 1] = blocks;                 // BN, one block per layer
-  blocks += DMLC_RN_LAYERS;
+  if (a->tail) blocks += DMLC_RN_LAYERS;
   a->blk_start[DMLC_RN_LAYERS + 2] = blocks;
+  if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rn_sgd, dim3(blocks), dim3(RT), 0, s, *a);
   return hipGetLastError();
 }

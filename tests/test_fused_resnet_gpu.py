@@ -240,3 +240,27 @@ def test_merged_backward_launch_matches_separate_launches(monkeypatch):
     assert _rel(g_m, g_s) < 1e-4, _rel(g_m, g_s)
     for lm, ls in zip(merged.part, split.part):
         assert _rel(lm, ls) < 1e-3
+
+
+def test_branch_sgd_split_equals_single_sgd_launch(monkeypatch):
+    """The layer-range SGD launches on a graph branch (stage 3 after its last backward launch, stage
+    2 after its) + the tail SGD give bitwise the same parameters, BN state and step as one SGD
+    launch, eagerly and under graph replay."""
+    B = 32
+    data, labels = _data(8 * B, seed=21)
+    monkeypatch.setenv("DMLC_RN_SGD_SPLIT", "1")
+    split = FusedResNetEngine(B, data, labels, seed=5, lr=0.01)
+    assert split.sgd_split
+    monkeypatch.setenv("DMLC_RN_SGD_SPLIT", "0")
+    one = FusedResNetEngine(B, data, labels, seed=5, lr=0.01)
+    assert not one.sgd_split
+    for e in (split, one):
+        for _ in range(3):
+            e.step()
+        e.capture()
+        for _ in range(4):
+            e.step()
+    torch.cuda.synchronize()
+    assert split.global_step() == one.global_step() == 7
+    assert torch.equal(split.master, one.master)
+    assert torch.equal(split.state, one.state)
