@@ -150,7 +150,9 @@ class _FlatViews(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *grads):
         parts, pos = [], 0
-        ref = next(g for g in grads if g is not None)
+        ref = next((g for g in grads if g is not None), None)
+        if ref is None:
+            return None, None
         for s, g in zip(ctx.specs, grads):
             if s.offset > pos:
                 parts.append(ref.new_zeros(s.offset - pos))
