@@ -115,6 +115,8 @@ def parse():
                          "the timed region) and keep the faster")
     ap.add_argument("--capture-comm", choices=["auto", "on", "off"], default="auto",
                     help="RCCL all-reduce inside the step HIP graph (auto: on over nccl)")
+    ap.add_argument("--rccl-channels", type=int, default=0,
+                    help="NCCL_MIN_NCHANNELS for RCCL over the 7 xGMI links (0 = RCCL's topology choice)")
     ap.add_argument("--steps-per-graph", type=int, default=32, help="longest chain of steps per graph replay")
     ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
@@ -161,7 +163,7 @@ def build_eager(args, info, data, labels):
 
 def main():
     args = parse()
-    info = D.init(D.env_info(), device="auto")
+    info = D.init(D.env_info(), device="auto", rccl_channels=args.rccl_channels)
     import torch.distributed as dist
     seen = dist.get_world_size() if dist.is_initialized() else 1
     if seen != args.gpus or info.world_size != args.gpus:
@@ -237,6 +239,8 @@ def main():
     comm = dict(getattr(eng, "comm_info", None) or {})
     comm.update(backend=info.backend if seen > 1 else "none", world_size_seen=seen,
                 device_count=torch.cuda.device_count() if info.device.type == "cuda" else 0, device=str(info.device))
+    if info.backend == "nccl" and seen > 1:
+        comm["rccl_env"] = D.rccl_env()
 
     n = info.world_size
     ms = elapsed * 1000.0 / args.steps

@@ -45,7 +45,7 @@ void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   a.amax = nullptr;
   a.xraw = xraw_ptr(xraw, B);
   if (amax.has_value()) {
-    check_numel(*amax, "amax", at::kFloat, 2);
+    check_numel(*amax, "amax", at::kFloat, B);
     a.amax = amax->data_ptr<float>();
   }
   CHECK_HIP(dmlc_conv1_fwd(&a, stream_of(out)));
@@ -57,7 +57,7 @@ void conv2_fwd_fp8(const Tensor& in, const Tensor& w8, const Tensor& b2, const T
   check(in, "in", at::kBFloat16, {B, 12, 12, 64});
   check(w8, "w8", at::kByte, {64, 1600});
   check_numel(b2, "b2", at::kFloat, 64);
-  check_numel(amax_x, "amax_x", at::kFloat, 2);
+  check_numel(amax_x, "amax_x", at::kFloat, B);
   check_numel(scale_w, "scale_w", at::kFloat, 2);
   check(out, "out", at::kBFloat16, {B, 6, 6, 64});
   check(am, "am", at::kByte, {B, 6, 6, 64});
@@ -136,6 +136,22 @@ void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const 
   a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
   a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B;
   CHECK_HIP(dmlc_conv2_dgrad(&a, stream_of(dp2)));
+}
+
+void conv2_dgrad_fp8(const Tensor& dp2, const Tensor& am2, const Tensor& w2d8, const Tensor& scale_w, const Tensor& dp1,
+                     const Tensor& dy2) {
+  const int64_t B = dp2.size(0);
+  check(dp2, "dp2", at::kBFloat16, {B, 6, 6, 64});
+  check(am2, "am2", at::kByte, {B, 6, 6, 64});
+  check(w2d8, "w2d8", at::kByte, {64, 1600});
+  check_numel(scale_w, "scale_w", at::kFloat, 2);
+  check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
+  c10::DeviceGuard guard(dp2.device());
+  DmlcConv2DgradFp8Args a;
+  a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.w8 = w2d8.data_ptr<uint8_t>();
+  a.scale_w = scale_w.data_ptr<float>(); a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B;
+  CHECK_HIP(dmlc_conv2_dgrad_fp8(&a, stream_of(dp2)));
 }
 
 void conv2_dgrad_w1(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const c10::optional<Tensor>& dp1,
@@ -397,14 +413,17 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
   a.nhead = (int)loss_part.numel();
   a.stats = stats.data_ptr<float>(); a.stats_len = (int)stats.size(0);
-  a.w2f8 = nullptr; a.amax_w = nullptr; a.scale_w = nullptr;
+  a.w2f8 = nullptr; a.w2d8 = nullptr; a.amax_w = nullptr; a.scale_w = nullptr;
   a.roles = (int)roles; a.finalize = finalize ? 1 : 0;
   if (w2f8.has_value()) {
     TORCH_CHECK(amax_w.has_value() && scale_w.has_value(), "fp8 shadow needs amax_w and scale_w");
-    check(*w2f8, "w2f8", at::kByte, {64, 1600});
+    // [64][1600] = the forward shadow only; [2][64][1600] = forward + the fp8 dgrad's flipped copy
+    if (w2f8->dim() == 3) check(*w2f8, "w2f8", at::kByte, {2, 64, 1600});
+    else check(*w2f8, "w2f8", at::kByte, {64, 1600});
     check_numel(*amax_w, "amax_w", at::kFloat, 2);
     check_numel(*scale_w, "scale_w", at::kFloat, 2);
     a.w2f8 = w2f8->data_ptr<uint8_t>(); a.amax_w = amax_w->data_ptr<float>(); a.scale_w = scale_w->data_ptr<float>();
+    if (w2f8->dim() == 3) a.w2d8 = a.w2f8 + 64 * 1600;
   }
   a.bidx = nullptr; a.bidx_n = 0;
   memset(&a.next, 0, sizeof(a.next));
@@ -437,6 +456,7 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(a!) p1, Tensor(b!) am1, Tensor w2f, Tensor b2, Tensor(c!) p2, Tensor(d!) am2, "
         "Tensor(e!)? xraw=None) -> ()");
   m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
+  m.def("conv2_dgrad_fp8(Tensor dp2, Tensor am2, Tensor w2d8, Tensor scale_w, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv2_dgrad_w1(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!)? dp1, Tensor(b!) dy2, Tensor am1, Tensor xraw, "
         "int cy, int cx, Tensor(c!) part1, Tensor(d!) partb1) -> ()");
   m.def("conv1_wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
@@ -465,6 +485,7 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("conv2_fwd_fp8", &conv2_fwd_fp8);
   m.impl("fp8_roundtrip", &fp8_roundtrip);
   m.impl("conv2_dgrad", &conv2_dgrad);
+  m.impl("conv2_dgrad_fp8", &conv2_dgrad_fp8);
   m.impl("conv2_dgrad_w1", &conv2_dgrad_w1);
   m.impl("conv1_wgrad", &conv1_wgrad);
   m.impl("conv2_wgrad", &conv2_wgrad);

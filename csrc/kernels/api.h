@@ -40,8 +40,8 @@ struct DmlcConv1FwdArgs {
   const float* bias;        // [64]
   void* out;                // bf16 [B][12][12][64]
   uint8_t* am;              // [B][12][12][64] argmax (0..8) in the pool window, 255 = no gradient
-  float* amax;              // nullable: fp8 path, float[2] running max of the pooled output, slot
-                            //   (step & 1) accumulated (atomic max), slot (step+1) & 1 zeroed
+  float* amax;              // nullable: fp8 path, float[B] per-image max of the pooled output (plain
+                            //   stores, no atomics; the fp8 conv2 forward reduces them)
   uint8_t* xraw;            // nullable: copy of each row's raw uint8 image [B][3072] for the wgrad
 };
 
@@ -56,17 +56,30 @@ struct DmlcConv2FwdArgs {
 };
 
 // conv2 forward on fp8 (OCP e4m3fn) MFMA operands, per-tensor scales (BASELINE config 5).
-// x8 = sat(x * 448 / amax_x[step&1]), w8 = w2f8 (quantised by the SGD kernel with scale_w[step&1]);
+// x8 = sat(x * 448 / max_b amax_x[b]), w8 = w2f8 (quantised by the SGD kernel with scale_w[step&1]);
 // out = relu(acc / (sx * sw) + b), then the same TF-SAME pool as the bf16 path.
 struct DmlcConv2FwdFp8Args {
   const void* in;           // bf16 [B][12][12][64]
   const uint8_t* w8;        // fp8 [64 co][1600]
   const float* bias;        // [64]
-  const float* amax_x;      // float[2] (conv1 pool output amax, slot step & 1)
+  const float* amax_x;      // float[B] (conv1 pool output max per image, this batch)
   const float* scale_w;     // float[2] (weight quantisation scale, slot step & 1)
   const int64_t* counter;   // device global_step (nullable: slot 0)
   void* out;                // bf16 [B][6][6][64]
   uint8_t* am;              // [B][6][6][64]
+  int B;
+};
+
+// conv2 input gradient on fp8 MFMA operands (BASELINE config 5 backward): w8 = the flipped, ci-major
+// W2 (w2d layout) quantised with scale_w (the SGD kernel writes it next to w2f8, both scale slots
+// hold the current scale); dY2 quantised per image in-kernel.  Outputs as DmlcConv2DgradArgs.
+struct DmlcConv2DgradFp8Args {
+  const void* dp2;          // bf16 [B][6][6][64]
+  const uint8_t* am2;       // [B][6][6][64]
+  const uint8_t* w8;        // fp8 [64 ci][1600]  (k' = (kh'*5+kw')*64 + co, W[4-kh'][4-kw'][ci][co] * sw)
+  const float* scale_w;     // float[2]
+  void* dp1;                // bf16 [B][12][12][64]
+  void* dy2;                // bf16 [B][144][64]
   int B;
 };
 
@@ -175,6 +188,7 @@ struct DmlcSgdArgs {
   // (2x headroom over the previous weights' amax), store sw to scale_w[(step+1)&1] and the new amax
   // to amax_w[(step+1)&1]; the last arriver zeroes amax_w[step&1].  Mode 3 uses/stores slot step&1.
   uint8_t* w2f8; float* amax_w; float* scale_w;
+  uint8_t* w2d8;            // nullable: fp8 [64 ci][1600] flipped shadow for the fp8 conv2 dgrad
   // block roles launched: 0 all, 1 conv rows + conv biases only, 2 fc only (data-parallel split of
   // the apply around the bucketed all-reduce); only launches with finalize = 1 bump global_step /
   // publish stats (their last arriver).
@@ -193,6 +207,7 @@ hipError_t dmlc_conv2_fwd(const DmlcConv2FwdArgs* a, hipStream_t s);
 // conv1 + pool1 + conv2 + pool2 of one image per workgroup in one launch (bf16; a1->amax must be null)
 hipError_t dmlc_conv12_fwd(const DmlcConv1FwdArgs* a1, const DmlcConv2FwdArgs* a2, hipStream_t s);
 hipError_t dmlc_conv2_fwd_fp8(const DmlcConv2FwdFp8Args* a, hipStream_t s);
+hipError_t dmlc_conv2_dgrad_fp8(const DmlcConv2DgradFp8Args* a, hipStream_t s);
 hipError_t dmlc_fp8_roundtrip(const float* x, float* y, int n, float scale, hipStream_t s);
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s);
 // conv2 dgrad + the conv1 weight gradient of each image (one slab per image: w1->g1 == B, xraw set)

@@ -129,14 +129,21 @@ __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 2);
   uint32_t vmax = 0;
   pool_emit<24>(cout, reinterpret_cast<bf16*>(a.out) + (size_t)b * 9216, a.am + (size_t)b * 9216, tid, &vmax);
-  if (a.amax) {                                // fp8 path: running max of the pooled activations
-    const int slot = a.src.counter ? (int)(*a.src.counter & 1) : 0;
+  if (a.amax) {                                // fp8 path: this image's max of the pooled activations
+    // one plain store per image (amax[b]); the fp8 conv2 forward reduces the B maxima itself.  (One
+    // same-address atomic per wave serialised at the L2: 8192 of them cost 70 us at B=1024.)
+    float* red = reinterpret_cast<float*>(smem + (C1_XIN + C1_OUT) * 2);
     uint32_t m = vmax;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-    if ((tid & 63) == 0 && m)                  // bf16 bits -> fp32 bits preserve order for x >= 0
-      atomicMax(reinterpret_cast<unsigned int*>(a.amax) + slot, m << 16);
-    if (b == 0 && tid == 0) a.amax[slot ^ 1] = 0.f;
+    if ((tid & 63) == 0) red[w] = __uint_as_float(m << 16);   // bf16 bits -> fp32 (pooled >= 0)
+    __syncthreads();
+    if (tid == 0) {
+      float v = red[0];
+#pragma unroll
+      for (int i = 1; i < NT / 64; ++i) v = fmaxf(v, red[i]);
+      a.amax[b] = v;
+    }
   }
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 3);
 }
@@ -515,40 +522,25 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
 
 using namespace dmlc;
 
-namespace {
-// Kernels above 64 KiB of dynamic LDS must opt in once (gfx950 has 160 KiB per CU).
-void allow_lds(const void* f, size_t bytes, bool& done) {
-  if (!done) {
-    (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    done = true;
-  }
-}
-bool g_c1 = false, g_c2 = false, g_dg = false;
-}  // namespace
 
 extern "C" {
 
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s) {
-  const size_t lds = (C1_XIN + C1_OUT) * 2;
-  allow_lds(reinterpret_cast<const void*>(&k_conv1_fwd), lds, g_c1);
+  const size_t lds = (C1_XIN + C1_OUT) * 2 + 64;        // + the fp8 path's 8 wave maxima
+  DMLC_LDS_OPTIN(&k_conv1_fwd, lds);
   hipLaunchKernelGGL(k_conv1_fwd, dim3(a->B), dim3(NT), lds, s, *a);
   return hipGetLastError();
 }
 
 hipError_t dmlc_conv2_fwd(const DmlcConv2FwdArgs* a, hipStream_t s) {
   const size_t lds = (C2_XIN + C2_OUT) * 2 + WS_BYTES;
-  allow_lds(reinterpret_cast<const void*>(&k_conv2_fwd), lds, g_c2);
+  DMLC_LDS_OPTIN(&k_conv2_fwd, lds);
   hipLaunchKernelGGL(k_conv2_fwd, dim3(a->B), dim3(NT), lds, s, *a);
   return hipGetLastError();
 }
 
 hipError_t dmlc_conv12_fwd(const DmlcConv1FwdArgs* a1, const DmlcConv2FwdArgs* a2, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv12_fwd), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)C12_LDS);
-    attr = true;
-  }
+  DMLC_LDS_OPTIN(&k_conv12_fwd, C12_LDS);
   if (a1->B != a2->B || a1->amax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_conv12_fwd, dim3(a1->B), dim3(NT), C12_LDS, s, *a1, *a2);
   return hipGetLastError();
@@ -569,7 +561,7 @@ hipError_t dmlc_conv2_dgrad_w1(const DmlcConv2DgradArgs* a, const DmlcConv1Wgrad
 
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s) {
   const size_t lds = (C2_XIN + C2_OUT) * 2 + 2304 * 3 + WS_BYTES;
-  allow_lds(reinterpret_cast<const void*>(&k_conv2_dgrad), lds, g_dg);
+  DMLC_LDS_OPTIN(&k_conv2_dgrad, lds);
   hipLaunchKernelGGL(k_conv2_dgrad, dim3(a->B), dim3(NT), lds, s, *a);
   return hipGetLastError();
 }

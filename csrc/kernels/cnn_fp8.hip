@@ -12,9 +12,13 @@
 //     padded pixel) XOR-swizzled by padded-row parity every B fragment read is conflict-free; weight
 //     rows (1792 B) XOR their 16-B units by (row & 1 | ((row >> 1) & 3) << 2): A reads conflict-free.
 // Scaling is per tensor and delayed (graph-capturable, no host sync):
-//   activations: sx = 448 / amax(p1), amax accumulated by conv1_fwd's pool epilogue this step;
+//   activations: sx = 448 / amax(p1) of THIS batch: conv1_fwd's pool epilogue stores one maximum per
+//                image, every block here reduces the B of them (4 KB at B=1024) behind its weight loads;
 //   weights:     w2f8 = sat(W2 * sw) written by the SGD kernel together with sw (cnn_sgd.hip).
-// Backward stays bf16 (dgrad/wgrad read the bf16 p1 and the bf16 W2 shadows).
+// conv2 input gradient (k_conv2_dgrad_fp8): the same weight-stationary core on the flipped, ci-major
+// weights (w2d8, quantised by the SGD kernel with the same scale as w2f8) and the pool2/ReLU-backward
+// gradient dY2 quantised per IMAGE with sy = 448 / amax(dY2 of that image), reduced in-block from the
+// values the block just produced.  The weight gradients stay bf16 (they read the bf16 p1 and dY2).
 #include "conv_common.h"
 
 namespace dmlc {
@@ -24,7 +28,8 @@ typedef int fp8x32 __attribute__((ext_vector_type(8)));   // 32 packed e4m3 valu
 constexpr int X8_BYTES = 256 * 64;            // [16x16 padded pixels][64 ch] fp8
 constexpr int W8_LD = 1792;                   // weight row stride (bytes): 26 taps x 64 used
 constexpr int W8_BYTES = 64 * W8_LD;
-constexpr size_t FP8_LDS = X8_BYTES + W8_BYTES + 144 * 64 * 2;
+constexpr size_t FP8_RED = X8_BYTES + W8_BYTES + 144 * 64 * 2;   // 8 wave maxima
+constexpr size_t FP8_LDS = FP8_RED + 64;
 static_assert(FP8_LDS <= 160 * 1024, "fp8 conv2 LDS");
 
 DEV int x8_addr(int P, int u) { return P * 64 + ((u ^ ((P >> 4) & 1)) << 4); }
@@ -37,6 +42,26 @@ DEV fp8x32 lds_fp8x32(const uint8_t* lo, const uint8_t* hi) {
   const uint4 a = *reinterpret_cast<const uint4*>(lo), b = *reinterpret_cast<const uint4*>(hi);
   const fp8x32 r = {(int)a.x, (int)a.y, (int)a.z, (int)a.w, (int)b.x, (int)b.y, (int)b.z, (int)b.w};
   return r;
+}
+
+// All of an fp8 [64 rows][1600] weight matrix -> LDS: 64 rows x 104 units of 16 B (units 100..103 =
+// the zero tap), 13 per thread in two rounds of up to 7 loads in flight.
+DEV void stage_w8(const uint8_t* __restrict__ src, uint8_t* w8, int tid) {
+#pragma unroll 1
+  for (int i0 = 0; i0 < 13; i0 += 7) {
+    uint4 wv[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int e = min(tid + (i0 + i) * NT, 6655), row = e / 104, U = e - row * 104;
+      wv[i] = load_sel(reinterpret_cast<const uint4*>(src + row * 1600 + U * 16), reinterpret_cast<const uint4*>(src),
+                       U < 100);
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int e = tid + (i0 + i) * NT, row = e / 104, U = e - row * 104;
+      if (e < 6656) *reinterpret_cast<uint4*>(w8 + w8_addr(row, U)) = U < 100 ? wv[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
 }
 
 // MFMAs of one image: wave (cp, pg) owns c_out tiles 2cp, 2cp+1 x pixel tiles pg, pg+4, pg+8 (< 9).
@@ -88,25 +113,21 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd_fp8(DmlcConv2FwdFp8Args a) 
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15, cp = w & 1, pg = w >> 1;
   const int slot = a.counter ? (int)(*a.counter & 1) : 0;
-  const float sx = 448.f / fmaxf(a.amax_x[slot], 1e-20f), sw = a.scale_w[slot];
-  const float inv = 1.f / (sx * sw);
+  const float sw = a.scale_w[slot];
+  float mx = 0.f;                              // the batch's activation amax from the per-image maxima
+  for (int i = tid; i < a.B; i += NT) mx = fmaxf(mx, a.amax_x[i]);
 
-  // weights -> LDS once: 64 rows x 104 units of 16 B (units 100..103 = the zero tap), 13 per thread
-#pragma unroll 1
-  for (int i0 = 0; i0 < 13; i0 += 7) {          // two rounds of up to 7 loads in flight per thread
-    uint4 wv[7];
+  stage_w8(a.w8, w8, tid);                     // weights -> LDS once
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int e = min(tid + (i0 + i) * NT, 6655), row = e / 104, U = e - row * 104;
-      wv[i] = load_sel(reinterpret_cast<const uint4*>(a.w8 + row * 1600 + U * 16), reinterpret_cast<const uint4*>(a.w8),
-                       U < 100);
-    }
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float* red = reinterpret_cast<float*>(smem + FP8_RED);
+  if (lane == 0) red[w] = mx;
+  __syncthreads();
+  mx = red[0];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int e = tid + (i0 + i) * NT, row = e / 104, U = e - row * 104;
-      if (e < 6656) *reinterpret_cast<uint4*>(w8 + w8_addr(row, U)) = U < 100 ? wv[i] : make_uint4(0u, 0u, 0u, 0u);
-    }
-  }
+  for (int i = 1; i < NT / 64; ++i) mx = fmaxf(mx, red[i]);
+  const float sx = 448.f / fmaxf(mx, 1e-20f);
+  const float inv = 1.f / (sx * sw);
   float b4[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -160,6 +181,98 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd_fp8(DmlcConv2FwdFp8Args a) 
   }
 }
 
+// conv2 input gradient on fp8: per image, pool2/ReLU backward (2x2 ownership, 288 tasks = one per
+// thread) -> dY2 (bf16 to global, for the weight gradient) and, in registers, its block amax -> e4m3
+// with sy = 448 / amax into the padded swizzled input grid -> the fp8 core against w2d8 -> dp1 =
+// acc / (sy * sw) in bf16.  The next image's dp2 / argmax are prefetched into registers under the
+// current image's MFMAs.  LDS: x8 16 KB | w8 112 KB | dp2 4.5 KB | argmax 2.25 KB | 8 wave maxima.
+constexpr size_t DG8_DP2 = X8_BYTES + W8_BYTES, DG8_AM2 = DG8_DP2 + 2304 * 2, DG8_RED = DG8_AM2 + 2304;
+constexpr size_t DG8_LDS = DG8_RED + 64;
+static_assert(DG8_LDS <= 160 * 1024, "fp8 conv2 dgrad LDS");
+
+__global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_fp8(DmlcConv2DgradFp8Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint8_t* x8 = reinterpret_cast<uint8_t*>(smem);
+  uint8_t* w8 = x8 + X8_BYTES;
+  bf16* dp2 = reinterpret_cast<bf16*>(smem + DG8_DP2);
+  uint8_t* am2 = reinterpret_cast<uint8_t*>(smem + DG8_AM2);
+  float* red = reinterpret_cast<float*>(smem + DG8_RED);
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int g = lane >> 4, li = lane & 15, cp = w & 1, pg = w >> 1;
+  const float sw = a.scale_w[0];
+  const int G = gridDim.x;
+
+  Prefetch16<288, NT> pd;
+  Prefetch16<144, NT> pa;
+  pd.load(reinterpret_cast<const bf16*>(a.dp2) + (size_t)blockIdx.x * 2304, tid);
+  pa.load(a.am2 + (size_t)blockIdx.x * 2304, tid);
+  stage_w8(a.w8, w8, tid);
+  for (int s = tid; s < 1024; s += NT) {        // halo of the padded 16x16 grid: zero once
+    const int P = s >> 2, r = P >> 4, col = P & 15;
+    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<uint4*>(x8 + x8_addr(P, s & 3)) = make_uint4(0u, 0u, 0u, 0u);
+  }
+  for (int b = blockIdx.x; b < a.B; b += G) {
+    __syncthreads();                             // the previous image's core / pool reads are done
+    pd.store(dp2, tid);
+    pa.store(am2, tid);
+    if (b + G < a.B) {                           // next image's operands in flight under this one
+      pd.load(reinterpret_cast<const bf16*>(a.dp2) + (size_t)(b + G) * 2304, tid);
+      pa.load(a.am2 + (size_t)(b + G) * 2304, tid);
+    }
+    __syncthreads();
+    float o[4][8];
+    float m = 0.f;
+    const int win = tid >> 3, c = tid & 7, py = win / 6, px = win - py * 6;
+    if (tid < 288) {
+      pool_bwd_2x2<6>(dp2, am2, py, px, c, o);
+      bf16* dy2 = reinterpret_cast<bf16*>(a.dy2) + (size_t)b * 9216;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
+        *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8) = to_bf16x8(o[k]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(o[k][j]));
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if (lane == 0) red[w] = m;
+    __syncthreads();
+    float amax = red[0];
+#pragma unroll
+    for (int i = 1; i < NT / 64; ++i) amax = fmaxf(amax, red[i]);
+    const float sy = amax > 0.f ? 448.f / amax : 1.f;
+    if (tid < 288) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int P = (2 * py + (k >> 1) + 2) * 16 + 2 * px + (k & 1) + 2;
+        const uint32_t lo = pk_fp8x4(o[k][0] * sy, o[k][1] * sy, o[k][2] * sy, o[k][3] * sy);
+        const uint32_t hi = pk_fp8x4(o[k][4] * sy, o[k][5] * sy, o[k][6] * sy, o[k][7] * sy);
+        *reinterpret_cast<uint2*>(x8 + x8_addr(P, c >> 1) + (c & 1) * 8) = make_uint2(lo, hi);
+      }
+    }
+    __syncthreads();
+    const float inv = 1.f / (sy * sw);
+    bf16* dp1 = reinterpret_cast<bf16*>(a.dp1) + (size_t)b * 9216;
+    auto epi = [&](int ct, int T, f32x4 acc) {
+      const int ty = T / 3, tx = T - ty * 3;
+      const int p = (4 * ty + (li >> 2)) * 12 + 4 * tx + (li & 3);
+      *reinterpret_cast<bf16x4*>(dp1 + p * 64 + 16 * ct + 4 * g) = pack4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+    };
+    if (pg == 0) {
+      f32x4 acc[2][3];
+      conv2_core_fp8<3>(x8, w8, acc, pg, cp, g, li);
+#pragma unroll
+      for (int t = 0; t < 3; ++t) { epi(2 * cp, pg + 4 * t, acc[0][t]); epi(2 * cp + 1, pg + 4 * t, acc[1][t]); }
+    } else {
+      f32x4 acc[2][2];
+      conv2_core_fp8<2>(x8, w8, acc, pg, cp, g, li);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) { epi(2 * cp, pg + 4 * t, acc[0][t]); epi(2 * cp + 1, pg + 4 * t, acc[1][t]); }
+    }
+  }
+}
+
 // quantise -> dequantise through the hardware converter (numerics test of the fp8 format: OCP e4m3fn)
 __global__ void k_fp8_roundtrip(const float* x, float* y, int n, float scale) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -172,19 +285,17 @@ __global__ void k_fp8_roundtrip(const float* x, float* y, int n, float scale) {
 
 using namespace dmlc;
 
-namespace {
-bool g_fp8 = false;
-}
-
 extern "C" {
 
 hipError_t dmlc_conv2_fwd_fp8(const DmlcConv2FwdFp8Args* a, hipStream_t s) {
-  if (!g_fp8) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv2_fwd_fp8),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)FP8_LDS);
-    g_fp8 = true;
-  }
+  DMLC_LDS_OPTIN(&k_conv2_fwd_fp8, FP8_LDS);
   hipLaunchKernelGGL(k_conv2_fwd_fp8, dim3(a->B < 256 ? a->B : 256), dim3(NT), FP8_LDS, s, *a);
+  return hipGetLastError();
+}
+
+hipError_t dmlc_conv2_dgrad_fp8(const DmlcConv2DgradFp8Args* a, hipStream_t s) {
+  DMLC_LDS_OPTIN(&k_conv2_dgrad_fp8, DG8_LDS);
+  hipLaunchKernelGGL(k_conv2_dgrad_fp8, dim3(a->B < 256 ? a->B : 256), dim3(NT), DG8_LDS, s, *a);
   return hipGetLastError();
 }
 

@@ -191,12 +191,7 @@ extern "C" hipError_t dmlc_gemm_grouped(DmlcGemmGroup* G, hipStream_t s) {
   }
   G->nblocks = blocks;
   if (blocks == 0) return hipSuccess;
-  static bool lds_set = false;
-  if (!lds_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_grouped),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)GEMM_LDS);
-    lds_set = true;
-  }
+  DMLC_LDS_OPTIN(&k_gemm_grouped, GEMM_LDS);
   hipLaunchKernelGGL(k_gemm_grouped, dim3(blocks), dim3(256), GEMM_LDS, s, *G);
   return hipGetLastError();
 }

@@ -254,12 +254,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
 
 template <int RB>
 hipError_t launch_head(const DmlcHeadArgs* a, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_head<RB>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              HeadLds<RB>::BYTES);
-    attr = true;
-  }
+  DMLC_LDS_OPTIN(&k_head<RB>, HeadLds<RB>::BYTES);
   hipLaunchKernelGGL(k_head<RB>, dim3(a->B / RB), dim3(HT), HeadLds<RB>::BYTES, s, *a);
   return hipGetLastError();
 }

@@ -78,8 +78,9 @@ DEV float4 split_sum(const float* __restrict__ p, size_t stride, int n, float4* 
   return t;
 }
 
-DEV float4 sgd4(float* m, float4 g, float lr, float scale, bool apply) {
-  float4 w = *reinterpret_cast<float4*>(m);
+// w: the master value, loaded by the caller BEFORE the slab reduction so that its memory latency
+// overlaps the slab loads instead of adding a second dependent round trip
+DEV float4 sgd4(float* m, float4 w, float4 g, float lr, float scale, bool apply) {
   if (apply) {
     const float f = lr * scale;
     w.x -= f * g.x; w.y -= f * g.y; w.z -= f * g.z; w.w -= f * g.w;
@@ -93,12 +94,13 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   const int idx = threadIdx.x % T, r = idx >> 4, co = (idx & 15) * 4;
   const int krow = blk * C2_ROWS + r;                 // (kh*5+kw)*64 + ci
   const size_t e = (size_t)krow * 64 + co;
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f), w0 = g;
+  if (a.mode != 1 && threadIdx.x < T) w0 = *reinterpret_cast<const float4*>(a.master + a.off[2] + e);
   if (a.mode == 0 || a.mode == 1) g = split_sum<C2_SPLIT>(a.part2 + e, 1600 * 64, a.g2, lds);
   if (threadIdx.x >= T) return;
   if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[2] + e);
   if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[2] + e) = g; return; }
-  const float4 w = sgd4(a.master + a.off[2] + e, g, lr, a.grad_scale, a.mode != 3);
+  const float4 w = sgd4(a.master + a.off[2] + e, w0, g, lr, a.grad_scale, a.mode != 3);
   const int ci = krow & 63, khw = krow >> 6;
   if (a.w2f8) {                                       // fp8 shadow for the fp8 conv2 forward
     const int64_t step = *a.step;
@@ -108,7 +110,11 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
     uint8_t* w8 = a.w2f8 + krow;
     w8[(co + 0) * 1600] = (uint8_t)q; w8[(co + 1) * 1600] = (uint8_t)(q >> 8);
     w8[(co + 2) * 1600] = (uint8_t)(q >> 16); w8[(co + 3) * 1600] = (uint8_t)(q >> 24);
-    if (threadIdx.x == 0) a.scale_w[nxt] = sw;       // identical value from every block
+    // the fp8 dgrad's flipped ci-major copy: the same 4 bytes, contiguous in co
+    if (a.w2d8) *reinterpret_cast<uint32_t*>(a.w2d8 + (size_t)ci * 1600 + (24 - khw) * 64 + co) = q;
+    // identical value from every block, into BOTH slots: the training forward runs without a step
+    // counter (slot 0) and must dequantise with the scale this launch quantised w2f8 with
+    if (threadIdx.x == 0) { a.scale_w[0] = sw; a.scale_w[1] = sw; }
     if (a.mode != 3) {
       float m = fmaxf(fmaxf(fabsf(w.x), fabsf(w.y)), fmaxf(fabsf(w.z), fabsf(w.w)));
 #pragma unroll
@@ -131,13 +137,14 @@ DEV void conv1_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   const int row = blk >> 1, co = (blk & 1) * 32 + (threadIdx.x % T) * 4;   // HWIO row = (kh*5+kw)*3 + ci
   const int ci = row % 3, khw = row / 3, kh = khw / 5, kw = khw - kh * 5;
   const size_t e = (size_t)row * 64 + co;
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f), w0 = g;
+  if (a.mode != 1 && threadIdx.x < T) w0 = *reinterpret_cast<const float4*>(a.master + a.off[0] + e);
   if (a.mode == 0 || a.mode == 1)                     // slab row k'' = kh*16 + kw*3 + ci
     g = split_sum<C1_SPLIT, C1_LOADS>(a.part1 + (size_t)(kh * 16 + kw * 3 + ci) * 64 + co, 80 * 64, a.g1, lds);
   if (threadIdx.x >= T) return;
   if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[0] + e);
   if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[0] + e) = g; return; }
-  const float4 w = sgd4(a.master + a.off[0] + e, g, lr, a.grad_scale, a.mode != 3);
+  const float4 w = sgd4(a.master + a.off[0] + e, w0, g, lr, a.grad_scale, a.mode != 3);
   const int k = kh * 32 + kw * 4 + ci;                // forward shadow layout w1f[co][160]
   bf16* w1f = reinterpret_cast<bf16*>(a.w1f);
   w1f[(co + 0) * 160 + k] = (bf16)w.x;
@@ -150,14 +157,15 @@ DEV void conv1_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
 DEV void conv_bias(const DmlcSgdArgs& a, int which, float lr, float4* lds) {
   const int c = (threadIdx.x % 16) * 4;
   const int seg = which == 0 ? 1 : 3;
-  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f), w0 = g;
+  if (a.mode != 1 && threadIdx.x < 16) w0 = *reinterpret_cast<const float4*>(a.master + a.off[seg] + c);
   if (a.mode == 0 || a.mode == 1)
     g = split_sum<16>((which == 0 ? a.partb1 : a.partb2) + c, 64, which == 0 ? a.g1 : a.g2, lds);
   if (threadIdx.x >= 16) return;
   float* gp = a.grad + a.off[seg] + c;
   if (a.mode == 1) { *reinterpret_cast<float4*>(gp) = g; return; }
   if (a.mode == 2) g = *reinterpret_cast<const float4*>(gp);
-  sgd4(a.master + a.off[seg] + c, g, lr, a.grad_scale, a.mode != 3);
+  sgd4(a.master + a.off[seg] + c, w0, g, lr, a.grad_scale, a.mode != 3);
 }
 
 DEV void fc1_block(const DmlcSgdArgs& a, int blk, float lr) {

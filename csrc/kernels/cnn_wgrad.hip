@@ -264,18 +264,10 @@ static_assert(W1T == W2T, "k_wgrad runs both bodies with one block size");
 
 using namespace dmlc;
 
-namespace {
-bool g_w1 = false;
-}
-
 extern "C" {
 
 hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s) {
-  if (!g_w1) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv1_wgrad),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)W1_LDS);
-    g_w1 = true;
-  }
+  DMLC_LDS_OPTIN(&k_conv1_wgrad, W1_LDS);
   hipLaunchKernelGGL(k_conv1_wgrad, dim3(a->g1), dim3(W1T), W1_LDS, s, *a);
   return hipGetLastError();
 }
@@ -286,12 +278,7 @@ hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s) {
 }
 
 hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)WG_LDS);
-    attr = true;
-  }
+  DMLC_LDS_OPTIN(&k_wgrad, WG_LDS);
   const int blocks = a->w1.g1 + 4 * a->w2.g2;
   hipLaunchKernelGGL(k_wgrad, dim3(blocks), dim3(W1T), WG_LDS, s, *a);
   return hipGetLastError();

@@ -168,6 +168,22 @@ DEV int swz128(int pix, int chunk) { return pix * 64 + ((chunk ^ (pix & 7)) << 3
 // with the plain (pix & 7) key (modelled per lane group, tools/lds_banks.py).
 DEV int swzpad(int pix, int chunk) { return pix * 64 + ((chunk ^ ((pix + 4 * (pix >> 4)) & 7)) << 3); }
 
+// Kernels above 64 KiB of dynamic LDS opt in once per kernel (gfx950: 160 KiB per CU).  The
+// attribute's status is returned to the launcher, so a refused opt-in reports itself instead of
+// surfacing later as a generic launch failure; it is retried on the next launch until it succeeds.
+inline hipError_t lds_optin(const void* f, size_t bytes, bool& done) {
+  if (done) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  done = e == hipSuccess;
+  return e;
+}
+#define DMLC_LDS_OPTIN(fn, bytes)                                                                   \
+  do {                                                                                              \
+    static bool optin_done_ = false;                                                                \
+    const hipError_t optin_e_ = ::dmlc::lds_optin(reinterpret_cast<const void*>(fn), (bytes), optin_done_); \
+    if (optin_e_ != hipSuccess) return optin_e_;                                                    \
+  } while (0)
+
 }  // namespace dmlc
 
 // ---- diagnostic phase timing (build with DMLC_TIMING=1: separate library, never the default) ----

@@ -983,10 +983,6 @@ using namespace dmlc::rn;
 
 namespace {
 
-template <class KFn>
-void set_lds(KFn* f, size_t bytes) {
-  if (bytes > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-}
 
 // the ResNet-20 layer shapes (CIN, COUT, HIN, S)
 #define DMLC_RN_SHAPES(X) \
@@ -1000,8 +996,7 @@ void set_lds(KFn* f, size_t bytes) {
 template <int CI, int CO, int H, int ST>
 hipError_t launch_fwd(const DmlcRnFwdArgs& a, hipStream_t s) {
   using F = Fwd<CI, CO, H, ST>;
-  static bool once = false;
-  if (!once) { set_lds(&k_rn_fwd<CI, CO, H, ST>, F::LDS); once = true; }
+  DMLC_LDS_OPTIN((&k_rn_fwd<CI, CO, H, ST>), F::LDS);
   hipLaunchKernelGGL((k_rn_fwd<CI, CO, H, ST>), dim3(a.B), dim3(RT), F::LDS, s, a);
   return hipGetLastError();
 }
@@ -1012,8 +1007,7 @@ hipError_t launch_dgrad(const DmlcRnDgradArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;             // the stem has no input gradient
   } else {
     using D = Dg<CI, CO, H, ST>;
-    static bool once = false;
-    if (!once) { set_lds(&k_rn_dgrad<CI, CO, H, ST>, D::LDS); once = true; }
+    DMLC_LDS_OPTIN((&k_rn_dgrad<CI, CO, H, ST>), D::LDS);
     hipLaunchKernelGGL((k_rn_dgrad<CI, CO, H, ST>), dim3(a.B), dim3(RT), D::LDS, s, a);
     return hipGetLastError();
   }
@@ -1027,8 +1021,7 @@ hipError_t launch_bwd(const DmlcRnDgradArgs& d, const DmlcRnWgradArgs& w, hipStr
     using D = Dg<CI, CO, H, ST>;
     using G = Wg<CI, CO, H, ST>;
     constexpr size_t lds = D::LDS > G::LDS ? D::LDS : G::LDS;
-    static bool once = false;
-    if (!once) { set_lds(&k_rn_bwd<CI, CO, H, ST>, lds); once = true; }
+    DMLC_LDS_OPTIN((&k_rn_bwd<CI, CO, H, ST>), lds);
     hipLaunchKernelGGL((k_rn_bwd<CI, CO, H, ST>), dim3(d.B + w.G * G::MC), dim3(RT), lds, s, d, w);
     return hipGetLastError();
   }
@@ -1037,8 +1030,7 @@ hipError_t launch_bwd(const DmlcRnDgradArgs& d, const DmlcRnWgradArgs& w, hipStr
 template <int CI, int CO, int H, int ST>
 hipError_t launch_wgrad(const DmlcRnWgradArgs& a, hipStream_t s) {
   using G = Wg<CI, CO, H, ST>;
-  static bool once = false;
-  if (!once) { set_lds(&k_rn_wgrad<CI, CO, H, ST>, G::LDS); once = true; }
+  DMLC_LDS_OPTIN((&k_rn_wgrad<CI, CO, H, ST>), G::LDS);
   hipLaunchKernelGGL((k_rn_wgrad<CI, CO, H, ST>), dim3(a.G, G::MC), dim3(RT), G::LDS, s, a);
   return hipGetLastError();
 }

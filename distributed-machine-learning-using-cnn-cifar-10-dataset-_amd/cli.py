@@ -93,6 +93,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--steps_per_graph", type=int, default=d.steps_per_graph,
                    help="longest chain of training steps captured into one HIP graph")
     p.add_argument("--pg_timeout_s", type=float, default=d.pg_timeout_s)
+    p.add_argument("--rccl_channels", type=int, default=d.rccl_channels,
+                   help="RCCL channels (rings over different xGMI link permutations); 0 = RCCL's choice")
     p.add_argument("--graph", type="bool", default=d.graph)
     p.add_argument("--trace", choices=["", "roctx", "torch"], default=d.trace)
     p.add_argument("--trace_steps", type=int, default=d.trace_steps)

@@ -82,6 +82,7 @@ class TrainConfig:
     allreduce: str = "auto"               # gradient all-reduce: auto | rccl | xgmi (parallel/xgmi.py)
     dp_schedule: str = "auto"             # N>1 fused step: auto (measured at start) | serial | overlap
     steps_per_graph: int = 8              # longest chain of training steps per HIP graph replay
+    rccl_channels: int = 0                # >0: NCCL_MIN_NCHANNELS for RCCL over the 7 xGMI links (§5.8)
     pg_timeout_s: float = 300.0           # process-group timeout (fail-fast on a dead rank)
     graph: bool = True                    # capture the fused step into a HIP graph
     trace: str = ""                       # '' | 'roctx' (phase ranges for rocprofv3 --marker-trace)

@@ -138,11 +138,14 @@ class FusedCifarEngine:
         self.w1f, self.w2f, self.w2d = z(64, 160), z(64, 1600), z(64, 1600)
         self.fc1n, self.fc2t, self.fc2n = z(2304, 384), z(192, 384), z(384, 192)
         self.fc3t, self.fc3d = z(16, 192), z(192, 32)
-        # fp8 conv2 forward (BASELINE config 5): e4m3 weight shadow + delayed per-tensor scales
+        # fp8 conv2 forward + input gradient (BASELINE config 5): e4m3 weight shadows [0] forward
+        # (co-major) and [1] the dgrad's flipped ci-major copy, delayed per-tensor weight scale;
+        # DMLC_FP8_DGRAD=0 keeps the conv2 input gradient in bf16
         self.fp8 = dtype == "fp8"
+        self.fp8_dgrad = self.fp8 and os.environ.get("DMLC_FP8_DGRAD", "1") != "0"
         if self.fp8:
-            self.w2f8 = z(64, 1600, dt=torch.uint8)
-            self.amax_x = z(2, dt=torch.float32)
+            self.w2f8 = z(2, 64, 1600, dt=torch.uint8)
+            self.amax_x = z(B, dt=torch.float32)      # per-image activation maxima (conv1 -> conv2)
             self.amax_w = z(2, dt=torch.float32)
             self.scale_w = z(2, dt=torch.float32)
 
@@ -292,7 +295,7 @@ class FusedCifarEngine:
             o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
                         self.am1, self.amax_x if self.fp8 else None, self.xraw if train else None)
         if self.fp8:
-            o.conv2_fwd_fp8(self.p1, self.w2f8, p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
+            o.conv2_fwd_fp8(self.p1, self.w2f8[0], p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
         elif not self.fused_fwd:
             o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
         f = self._fc1_fwd
@@ -316,7 +319,10 @@ class FusedCifarEngine:
                     self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw,
                     False)
             return
-        o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
+        if self.fp8_dgrad:
+            o.conv2_dgrad_fp8(self.dp2, self.am2, self.w2f8[1], self.scale_w, self.dp1, self.dy2)
+        else:
+            o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         if self.merged_wgrad:
             o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
                     self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw)

@@ -406,7 +406,7 @@ def main(argv=None) -> int:
         return 0                          # unknown --job_name: the reference silently did nothing
     if role.kind == "ps":
         return D.serve_ps(role, log=lambda m: print(m, flush=True))
-    info = D.init(D.role_info(role), device=cfg.device, timeout_s=cfg.pg_timeout_s)
+    info = D.init(D.role_info(role), device=cfg.device, timeout_s=cfg.pg_timeout_s, rccl_channels=cfg.rccl_channels)
     try:
         sess = Session(cfg, info, log=lambda m: print(m, flush=True))
         res = sess.run()

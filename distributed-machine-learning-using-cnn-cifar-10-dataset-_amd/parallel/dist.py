@@ -70,13 +70,37 @@ def pick_device(local_rank: int, want: str = "auto") -> torch.device:
     return d
 
 
+RCCL_ENV_KEYS = ("NCCL_MIN_NCHANNELS", "NCCL_MAX_NCHANNELS", "NCCL_ALGO", "NCCL_PROTO", "RCCL_MSCCL_ENABLE",
+                 "NCCL_P2P_LEVEL")
+
+
+def rccl_env(channels: int = 0) -> dict:
+    """RCCL channel layout for the 7 point-to-point xGMI links of an MI355X node.
+
+    One ring drives one egress link per GPU, so an all-reduce over a single ring is bound by ONE of
+    the seven ~153 GB/s links.  ``channels`` > 0 asks RCCL for at least that many channels (rings laid
+    over different link permutations; 7 or a multiple of it covers every link) via NCCL_MIN_NCHANNELS,
+    raising NCCL_MAX_NCHANNELS to match.  The variables are read when the communicator is created, so
+    this runs before ``init_process_group``.  Values already in the environment win (per-job tuning
+    from the shell); 0 leaves RCCL's own topology-based choice.  Returns the RCCL/NCCL variables in
+    effect, which bench.py reports next to the measured all-reduce choice."""
+    if channels > 0:
+        os.environ.setdefault("NCCL_MIN_NCHANNELS", str(channels))
+        mx = os.environ.get("NCCL_MAX_NCHANNELS")
+        if mx is None or int(mx) < int(os.environ["NCCL_MIN_NCHANNELS"]):
+            os.environ["NCCL_MAX_NCHANNELS"] = os.environ["NCCL_MIN_NCHANNELS"]
+    return {k: os.environ[k] for k in RCCL_ENV_KEYS if k in os.environ}
+
+
 def init(info: Optional[DistInfo] = None, device: str = "auto", timeout_s: float = 300.0,
-         backend: Optional[str] = None) -> DistInfo:
+         backend: Optional[str] = None, rccl_channels: int = 0) -> DistInfo:
     """Initialise the default process group (if world_size > 1) and bind this rank's device."""
     info = info or env_info()
     info.device = pick_device(info.local_rank, device)
     # DMLC_DIST_BACKEND=gloo: rehearse a multi-rank GPU job on one GPU (RCCL refuses two ranks per GPU)
     info.backend = backend or os.environ.get("DMLC_DIST_BACKEND") or ("nccl" if info.device.type == "cuda" else "gloo")
+    if info.backend == "nccl":
+        rccl_env(rccl_channels)
     if info.world_size > 1 and not dist.is_initialized():
         timeout = datetime.timedelta(seconds=timeout_s)
         kw = {}

@@ -217,3 +217,18 @@ def test_bench_rejects_world_size_mismatch():
                           "--batch", "8", "--steps", "1", "--warmup", "1", "--dataset-size", "64"],
                          env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 3, (out.returncode, out.stderr[-2000:])
+
+
+def test_rccl_channel_env(monkeypatch):
+    """--rccl_channels sets NCCL_MIN_NCHANNELS (and a matching max) before the communicator exists;
+    values already in the environment win; 0 leaves RCCL's own choice."""
+    from dmlc.parallel import dist as D
+    for k in D.RCCL_ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    assert D.rccl_env(0) == {}
+    assert D.rccl_env(14) == {"NCCL_MIN_NCHANNELS": "14", "NCCL_MAX_NCHANNELS": "14"}
+    monkeypatch.setenv("NCCL_MIN_NCHANNELS", "28")
+    monkeypatch.setenv("NCCL_MAX_NCHANNELS", "16")
+    assert D.rccl_env(7) == {"NCCL_MIN_NCHANNELS": "28", "NCCL_MAX_NCHANNELS": "28"}
+    from dmlc import cli
+    assert cli.parse(["--rccl_channels=7"])[0].rccl_channels == 7

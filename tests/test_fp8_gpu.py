@@ -1,5 +1,8 @@
-"""fp8 (OCP e4m3fn) conv2 forward path (BASELINE config 5): converter format, forward numerics vs the
-fp32 PyTorch reference, delayed-scaling bookkeeping and training."""
+"""fp8 (OCP e4m3fn) conv2 forward + input-gradient path (BASELINE config 5): converter format, forward
+and dgrad numerics vs the fp32 PyTorch reference, delayed-scaling bookkeeping and training."""
+import json
+import os
+
 import pytest
 import torch
 
@@ -43,6 +46,45 @@ def test_fp8_forward_matches_reference():
     rel = float((got - ref).norm() / ref.norm())
     assert rel < 8e-2, rel
     assert float(eng.scale_w[eng.host_step & 1]) > 0
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm())
+
+
+@pytest.mark.parametrize("B", [64, 320])
+def test_fp8_dgrad_matches_reference(B):
+    """The fp8 conv2 input gradient (k_conv2_dgrad_fp8: per-image dY2 scale, e4m3 flipped weights,
+    weight-stationary blocks looping over images for B > 256) against fp32 PyTorch fed with the
+    kernel's own bf16 dY2 and the fp32 master W2; the bf16 kernel on the same inputs sets the scale of
+    the comparison, and the conv1 weight gradient downstream must keep its direction."""
+    data, labels = _synthetic(1024, seed=4)
+    eng = FusedCifarEngine(B, data, labels, seed=2, dtype="fp8")
+    assert eng.fp8_dgrad
+    g8 = eng.compute_gradients().clone()
+    torch.cuda.synchronize()
+    dy = eng.dy2.float().view(B, 12, 12, 64).permute(0, 3, 1, 2)
+    w = M.views(eng.flat_params().cuda())["conv2_kernel"].float()                # HWIO
+    ref = torch.nn.grad.conv2d_input((B, 64, 12, 12), w.permute(3, 2, 0, 1).contiguous(), dy, padding=2)
+    ref = ref.permute(0, 2, 3, 1)
+    rel8 = _rel(eng.dp1, ref)
+    dp1b, dy2b = torch.empty_like(eng.dp1), torch.empty_like(eng.dy2)
+    eng.ops.conv2_dgrad(eng.dp2, eng.am2, eng.w2d, dp1b, dy2b)
+    torch.cuda.synchronize()
+    assert torch.equal(dy2b, eng.dy2)                  # the same pool2 / ReLU backward, bit for bit
+    relb = _rel(dp1b, ref)
+    per_img = ((eng.dp1.float() - ref).flatten(1).norm(dim=1) / ref.flatten(1).norm(dim=1).clamp_min(1e-30))
+    eng.fp8_dgrad = False
+    gb = eng.compute_gradients().clone()
+    c1 = slice(M.PARAM_SPECS[0].offset, M.PARAM_SPECS[0].offset + M.PARAM_SPECS[0].numel)
+    cos = float(torch.nn.functional.cosine_similarity(g8[c1], gb[c1], dim=0))
+    out = {"B": B, "rel_fp8": rel8, "rel_bf16": relb, "per_image_rel_max": float(per_img.max()), "conv1_grad_cos": cos}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/fp8_dgrad_numerics_b{B}.json", "w") as f:
+        json.dump(out, f)
+    assert rel8 < 6e-2 and float(per_img.max()) < 1e-1, out
+    assert relb < 1e-2, out
+    assert cos > 0.995, out
 
 
 def test_fp8_training_tracks_scales_and_reduces_loss():

@@ -57,7 +57,7 @@ def main():
                                                   p["conv1_bias"], eng.p1, eng.am1, None, eng.xraw), a.iters)
     res["conv2_fwd"] = timeit(lambda: o.conv2_fwd(eng.p1, eng.w2f, p["conv2_bias"], eng.p2, eng.am2), a.iters)
     if eng.fp8:
-        res["conv2_fwd_fp8"] = timeit(lambda: o.conv2_fwd_fp8(eng.p1, eng.w2f8, p["conv2_bias"], eng.amax_x, eng.scale_w,
+        res["conv2_fwd_fp8"] = timeit(lambda: o.conv2_fwd_fp8(eng.p1, eng.w2f8[0], p["conv2_bias"], eng.amax_x, eng.scale_w,
                                                               None, eng.p2, eng.am2), a.iters)
     res["conv12_fwd"] = timeit(lambda: o.conv12_fwd(eng.data, eng.bidx, None, 1, eng.cy, eng.cx,
                                                     eng.w1f, p["conv1_bias"], eng.p1, eng.am1, eng.w2f,
@@ -71,6 +71,9 @@ def main():
                                         eng.loss_part, eng.correct_part, None), a.iters)
     res["fc_bwd_gemm"] = timeit(eng._fc_backward, a.iters)
     res["conv2_dgrad"] = timeit(lambda: o.conv2_dgrad(eng.dp2, eng.am2, eng.w2d, eng.dp1, eng.dy2), a.iters)
+    if eng.fp8:
+        res["conv2_dgrad_fp8"] = timeit(lambda: o.conv2_dgrad_fp8(eng.dp2, eng.am2, eng.w2f8[1], eng.scale_w, eng.dp1,
+                                                                  eng.dy2), a.iters)
     if eng.fused_w1:
         res["conv2_dgrad_w1"] = timeit(lambda: o.conv2_dgrad_w1(eng.dp2, eng.am2, eng.w2d, None, eng.dy2, eng.am1,
                                                                 eng.xraw, eng.cy, eng.cx, eng.part1, eng.partb1),
