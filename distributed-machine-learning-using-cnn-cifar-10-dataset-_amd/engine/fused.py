@@ -492,7 +492,18 @@ class FusedCifarEngine:
                 self.chains[k] = self._capture_one(lambda k=k: [self._eager_step() for _ in range(k)], pool)
                 k *= 2
         self.chains[1] = self.graphs[0] if self.single_graph else None
+        self._pool = pool
         torch.cuda.synchronize(self.device)
+
+    def add_chain(self, k: int) -> bool:
+        """Also capture a chain of exactly ``k`` steps, so :meth:`run` (k) is ONE graph replay (a
+        short timed region otherwise pays one graph-launch boundary per power-of-two piece)."""
+        k = int(k)
+        if not self.single_graph or not self.graphs or k < 2 or self.chains.get(k) is not None:
+            return False
+        self.chains[k] = self._capture_one(lambda: [self._eager_step() for _ in range(k)], self._pool)
+        torch.cuda.synchronize(self.device)
+        return True
 
     def _capture_one(self, fn, pool):
         g = torch.cuda.CUDAGraph()
