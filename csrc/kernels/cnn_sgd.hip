@@ -285,12 +285,27 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
   // would hold the ticket until every store of the block had been acknowledged.
   lds_barrier();
   if (threadIdx.x < 64) {                              // wave 0: ticket, then (last) the stats
+    // the head's per-workgroup partials (an earlier launch), loaded by EVERY block's wave 0 together
+    // with its ticket: the last arriver then has them in registers instead of paying one more memory
+    // round trip on the launch's critical path (802 x 512 B of L2 reads, nothing)
+    // (branch-free, clamped: no wait between these loads and the ticket atomic, which then share
+    // one memory latency; partials beyond 256 -- per-GPU batch > 1024 -- are summed by the last only)
+    float lv[4];
+    int cv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = threadIdx.x + 64 * u, qc = q < a.nhead ? q : 0;
+      lv[u] = a.loss_part[qc];
+      cv[u] = a.correct_part[qc];
+    }
     int last = 0;
     if (threadIdx.x == 0) last = last_arrival(a.ticket, blockIdx.x, gridDim.x) ? 1 : 0;
     if (__shfl(last, 0)) {
-      // the head's per-workgroup partials, summed by the whole wave (all loads in flight at once)
       float loss = 0.f, corr = 0.f;
-      for (int q = threadIdx.x; q < a.nhead; q += 64) { loss += a.loss_part[q]; corr += (float)a.correct_part[q]; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (threadIdx.x + 64 * u < a.nhead) { loss += lv[u]; corr += (float)cv[u]; }
+      for (int q = threadIdx.x + 256; q < a.nhead; q += 64) { loss += a.loss_part[q]; corr += (float)a.correct_part[q]; }
       loss = wave_sum(loss);
       corr = wave_sum(corr);
       if (threadIdx.x == 0) {
