@@ -76,8 +76,11 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
   bf16* sA = reinterpret_cast<bf16*>(smem);             // [2][TILE_ELEMS]
   bf16* sB = sA + 2 * TILE_ELEMS;                        // [2][TILE_ELEMS]
   const int blk = blockIdx.x;
+  // problem lookup: every block_start compared at once (independent scalar loads, one latency; a
+  // search loop paid one dependent kernarg load per problem before the last problem's blocks began)
   int pi = 0;
-  while (pi + 1 < G.nprob && blk >= G.p[pi + 1].block_start) ++pi;
+#pragma unroll
+  for (int i = 1; i < DMLC_MAX_GEMM; ++i) pi += (i < G.nprob && blk >= G.p[i].block_start) ? 1 : 0;
   const DmlcGemmProblem P = G.p[pi];
   const int local = blk - P.block_start;
   DMLC_STAMP(DMLC_TK_GEMM, 0);

@@ -866,8 +866,11 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
   const bool reduce = mode <= 1, apply = mode == 0 || mode == 2;
   const int blk = blockIdx.x, tid = threadIdx.x;
   constexpr int NL = DMLC_RN_LAYERS;
+  // block role: every range start compared at once (21 independent kernarg loads, one latency; the
+  // search loop paid one dependent scalar load per range -- ~20 in a row for the BN blocks)
   int l = 0;
-  while (l < NL + 1 && blk >= a.blk_start[l + 1]) ++l;
+#pragma unroll
+  for (int i = 1; i <= NL + 1; ++i) l += blk >= a.blk_start[i] ? 1 : 0;
   if (l < NL) {                                  // conv layer l
     const int S = a.split[l], O = RT / S;
     const int cin = a.cin[l], cout = a.cout[l], cinp = cin < 8 ? 8 : cin;
