@@ -117,6 +117,8 @@ def parse():
                     help="RCCL all-reduce inside the step HIP graph (auto: on over nccl)")
     ap.add_argument("--rccl-channels", type=int, default=0,
                     help="NCCL_MIN_NCHANNELS for RCCL over the 7 xGMI links (0 = RCCL's topology choice)")
+    ap.add_argument("--settle-steps", type=int, default=256,
+                    help="untimed replayed steps (graph rehearsal included) before the timed region")
     ap.add_argument("--steps-per-graph", type=int, default=32, help="longest chain of steps per graph replay")
     ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
@@ -203,7 +205,8 @@ def main():
         if args.dp_schedule == "auto" and hasattr(eng, "tune_schedule") and info.world_size > 1:
             eng.tune_schedule(iters=max(10, args.warmup), steps_per_graph=args.steps_per_graph)
         # a short timed region replays as ONE graph of exactly --steps steps
-        if args.steps <= 2 * args.steps_per_graph and hasattr(eng, "add_chain"):
+        if (args.steps <= 2 * args.steps_per_graph and hasattr(eng, "add_chain")
+                and os.environ.get("DMLC_BENCH_EXACT_CHAIN", "1") != "0"):
             eng.add_chain(args.steps)
         # replay every captured chain once (first launches of a graph pay its upload): untimed
         # training steps on top of the W warm-up steps, reported as graph_warmup_steps
@@ -214,6 +217,12 @@ def main():
         if args.steps <= 64:
             eng.run(args.steps)
             graph_warm += args.steps
+        # ... and keep the GPU at sustained load for --settle-steps replayed steps in all (clocks /
+        # power settle over ~10-20 ms: 20-step runs measured 2.98-3.02 M after ~110 untimed steps,
+        # 3.05 M after ~300).  Untimed, counted in graph_warmup_steps.
+        if args.settle_steps > graph_warm and hasattr(eng, "run"):
+            eng.run(args.settle_steps - graph_warm)
+            graph_warm = args.settle_steps
     # run(n): n complete steps, as chained graph replays (fused engines) or n step() calls
     run = getattr(eng, "run", None) if capture is not None else None
     if run is None:

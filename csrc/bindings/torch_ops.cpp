@@ -420,7 +420,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
     // [64][1600] = the forward shadow only; [2][64][1600] = forward + the fp8 dgrad's flipped copy
     if (w2f8->dim() == 3) check(*w2f8, "w2f8", at::kByte, {2, 64, 1600});
     else check(*w2f8, "w2f8", at::kByte, {64, 1600});
-    check_numel(*amax_w, "amax_w", at::kFloat, 2);
+    check_numel(*amax_w, "amax_w", at::kFloat, 2 * 400);   // [2 slots][400 conv2-row blocks]
     check_numel(*scale_w, "scale_w", at::kFloat, 2);
     a.w2f8 = w2f8->data_ptr<uint8_t>(); a.amax_w = amax_w->data_ptr<float>(); a.scale_w = scale_w->data_ptr<float>();
     if (w2f8->dim() == 3) a.w2d8 = a.w2f8 + 64 * 1600;

@@ -184,9 +184,10 @@ struct DmlcSgdArgs {
   const float* loss_part; const int* correct_part; int nhead;
   float* stats; int stats_len;   // ring [stats_len][4] = {step, loss, accuracy, lr}
   int nblocks;
-  // fp8 conv2 shadow (nullable).  Modes 0/2 quantise the updated W2 with sw = 224 / amax_w[step&1]
-  // (2x headroom over the previous weights' amax), store sw to scale_w[(step+1)&1] and the new amax
-  // to amax_w[(step+1)&1]; the last arriver zeroes amax_w[step&1].  Mode 3 uses/stores slot step&1.
+  // fp8 conv2 shadow (nullable).  amax_w = float[2][400]: slot s holds one maximum per conv2-row
+  // block.  Modes 0/2 quantise the updated W2 with sw = 224 / max(amax_w[step&1][*]) (2x headroom
+  // over the previous weights' amax), store sw to both scale_w slots and each block's new maximum to
+  // amax_w[(step+1)&1][block] (plain stores).  Mode 3 uses slot step&1 (set by the host).
   uint8_t* w2f8; float* amax_w; float* scale_w;
   uint8_t* w2d8;            // nullable: fp8 [64 ci][1600] flipped shadow for the fp8 conv2 dgrad
   // block roles launched: 0 all, 1 conv rows + conv biases only, 2 fc only (data-parallel split of

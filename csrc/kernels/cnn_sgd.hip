@@ -96,6 +96,17 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   const size_t e = (size_t)krow * 64 + co;
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f), w0 = g;
   if (a.mode != 1 && threadIdx.x < T) w0 = *reinterpret_cast<const float4*>(a.master + a.off[2] + e);
+  // fp8: the previous weights' amax = max of the C2_BLOCKS per-block maxima the last launch stored
+  // (plain stores, no same-address atomics), loaded by wave 0 beside the slab loads
+  float am[(C2_BLOCKS + 63) / 64];
+  if (a.w2f8 && a.mode != 1 && threadIdx.x < T) {
+    const float* src = a.amax_w + (size_t)(*a.step & 1) * C2_BLOCKS;
+#pragma unroll
+    for (int u = 0; u < (C2_BLOCKS + 63) / 64; ++u) {
+      const int i = threadIdx.x + 64 * u;
+      am[u] = src[i < C2_BLOCKS ? i : 0];
+    }
+  }
   if (a.mode == 0 || a.mode == 1) g = split_sum<C2_SPLIT>(a.part2 + e, 1600 * 64, a.g2, lds);
   if (threadIdx.x >= T) return;
   if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[2] + e);
@@ -105,7 +116,12 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   if (a.w2f8) {                                       // fp8 shadow for the fp8 conv2 forward
     const int64_t step = *a.step;
     const int cur = (int)(step & 1), nxt = a.mode == 3 ? cur : cur ^ 1;
-    const float sw = 224.f / fmaxf(a.amax_w[cur], 1e-20f);
+    float amax = am[0];
+#pragma unroll
+    for (int u = 1; u < (C2_BLOCKS + 63) / 64; ++u) amax = fmaxf(amax, am[u]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    const float sw = 224.f / fmaxf(amax, 1e-20f);
     const uint32_t q = pk_fp8x4(w.x * sw, w.y * sw, w.z * sw, w.w * sw);
     uint8_t* w8 = a.w2f8 + krow;
     w8[(co + 0) * 1600] = (uint8_t)q; w8[(co + 1) * 1600] = (uint8_t)(q >> 8);
@@ -119,7 +135,7 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
       float m = fmaxf(fmaxf(fabsf(w.x), fabsf(w.y)), fmaxf(fabsf(w.z), fabsf(w.w)));
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-      if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned int*>(a.amax_w) + nxt, __float_as_uint(m));
+      if (threadIdx.x == 0) a.amax_w[(size_t)nxt * C2_BLOCKS + blk] = m;
     }
   }
   // w2d[ci][((4-kh)*5 + (4-kw))*64 + co] : contiguous in co
@@ -315,7 +331,6 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
         st[2] = corr / (float)a.B;
         st[3] = lr;
         *a.step = step + 1;
-        if (a.w2f8) a.amax_w[step & 1] = 0.f;         // every block has read it; next step's target
       }
     }
   }

@@ -146,7 +146,7 @@ class FusedCifarEngine:
         if self.fp8:
             self.w2f8 = z(2, 64, 1600, dt=torch.uint8)
             self.amax_x = z(B, dt=torch.float32)      # per-image activation maxima (conv1 -> conv2)
-            self.amax_w = z(2, dt=torch.float32)
+            self.amax_w = z(2, 400, dt=torch.float32)  # [slot][SGD conv2-row block] weight maxima
             self.scale_w = z(2, dt=torch.float32)
 
         # --- activations / workspaces -------------------------------------------------------

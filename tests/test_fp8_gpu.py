@@ -102,7 +102,7 @@ def test_fp8_training_tracks_scales_and_reduces_loss():
     s = eng.host_step & 1
     w2 = M.views(eng.flat_params())["conv2_kernel"]
     amax = float(w2.abs().max())
-    assert abs(float(eng.amax_w[s]) - amax) <= 1e-6 * max(1.0, amax)       # exact running amax
+    assert abs(float(eng.amax_w[s].max()) - amax) <= 1e-6 * max(1.0, amax)  # exact amax (block maxima)
     assert abs(float(eng.scale_w[s]) * amax - 224.0) / 224.0 < 0.05        # 2x headroom scale
     assert losses[-1] < 0.9 * losses[0], losses
 
