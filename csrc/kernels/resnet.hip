@@ -731,8 +731,20 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   __shared__ float pool_part[4][64];
   __shared__ float pooled[64], dlog[16], gpool[64], cf[2][64];
   __shared__ float redl[2][4][64];
+  __shared__ float fcw_s[650];                  // fc weight [64][10] + bias [10]
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int c = lane;                           // thread -> channel c, pixels w, w+4, ... (16 each)
+  // every small operand of the later phases is loaded at entry, beside the activations: the fc
+  // weights / bias into LDS, gamma / beta into registers (each was one more exposed memory latency
+  // on the serial chain pool -> logits -> dlogits -> pooled gradient)
+  float fv[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int e = tid + i * RT;                 // clamped addresses: every load in bounds
+    const float wv = a.fcw[e < 640 ? e : 0], bv = a.fcb[e >= 640 && e < 650 ? e - 640 : 0];
+    fv[i] = e < 640 ? wv : (e < 650 ? bv : 0.f);
+  }
+  const float gam = a.gamma[c], bet = a.beta[c];
   if (tid < 64) {
     float mean, rstd;
     bn_mean_rstd(a.stat, tid, a.inv_n, mean, rstd);
@@ -749,9 +761,14 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   }
   int label = 0;
   if (tid == 0) label = a.labels[batch_index(a.src, a.B, b)];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int e = tid + i * RT;
+    if (e < 650) fcw_s[e] = fv[i];
+  }
   __syncthreads();
   const float mean = cf[0][c], rstd = cf[1][c];
-  const float sc = a.gamma[c] * rstd, sh = a.beta[c] - mean * sc;
+  const float sc = gam * rstd, sh = bet - mean * sc;
   float av[16];
   float s = 0.f;
 #pragma unroll
@@ -766,8 +783,8 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   if (tid < 64) {                               // wave 0: logits / softmax / dlogits
     float lg = 0.f;
     if (lane < 10) {
-      lg = a.fcb[lane];
-      for (int k = 0; k < 64; ++k) lg += pooled[k] * a.fcw[k * 10 + lane];
+      lg = fcw_s[640 + lane];
+      for (int k = 0; k < 64; ++k) lg += pooled[k] * fcw_s[k * 10 + lane];
     }
     const float lgm = lane < 10 ? lg : -INFINITY;
     float m = lgm;
@@ -793,7 +810,7 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   if (tid < 64) {
     float gp = 0.f;
 #pragma unroll
-    for (int n = 0; n < 10; ++n) gp += a.fcw[tid * 10 + n] * dlog[n];
+    for (int n = 0; n < 10; ++n) gp += fcw_s[tid * 10 + n] * dlog[n];
     gpool[tid] = gp * (1.f / 64.f);
     float* fp = a.fc_part + (size_t)b * 656;
 #pragma unroll
@@ -927,33 +944,52 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
   } else if (mode != 3 && a.tail) {               // BN layer L: gamma/beta + running statistics
     const int L = blk - a.blk_start[NL + 1];
     const int c = tid;
-    if (c < a.cout[L]) {
-      const size_t og = (size_t)a.gamma_off[L] + c, ob = (size_t)a.beta_off[L] + c;
-      double r1, r2;
-      slot_sums(a.red + (size_t)L * NSLOT * 128, c, r1, r2);
+    // every load of this block first (gradient and statistics slots, master gamma / beta, running
+    // statistics, layer 0: the per-image loss / accuracy), then the arithmetic and the stores: the
+    // chain of dependent round trips made these 19 blocks the launch's tail
+    const bool act = c < a.cout[L];
+    const int cc = act ? c : 0;
+    const size_t og = (size_t)a.gamma_off[L] + cc, ob = (size_t)a.beta_off[L] + cc;
+    const double* rp = a.red + (size_t)L * NSLOT * 128;
+    const double* sp = a.stat + (size_t)L * NSLOT * 128;
+    double ra[NSLOT], rb[NSLOT], sa[NSLOT], sb[NSLOT];
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) {
+      ra[k] = rp[k * 128 + cc]; rb[k] = rp[k * 128 + 64 + cc];
+      sa[k] = sp[k * 128 + cc]; sb[k] = sp[k * 128 + 64 + cc];
+    }
+    float* mm = a.state + a.mm_off[L] + cc;
+    float* mv = a.state + a.mv_off[L] + cc;
+    // (a.grad exists only in the data-parallel modes 1/2; the running statistics are only updated
+    // by the applying modes)
+    float mg = 0.f, mb = 0.f, gg = 0.f, gb = 0.f, mmv = 0.f, mvv = 0.f;
+    if (mode != 1) { mg = a.master[og]; mb = a.master[ob]; mmv = *mm; mvv = *mv; }
+    if (mode == 2) { gg = a.grad[og]; gb = a.grad[ob]; }
+    float lsv = 0.f, csv = 0.f;
+    if (L == 0 && apply)
+      for (int q = tid; q < a.B; q += RT) { lsv += a.loss_img[q]; csv += (float)a.correct_img[q]; }
+    if (act) {
+      double r1 = 0.0, r2 = 0.0, s1 = 0.0, s2 = 0.0;    // same fixed slot order as slot_sums
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) { r1 += ra[k]; r2 += rb[k]; s1 += sa[k]; s2 += sb[k]; }
       if (mode == 1) {
         a.grad[og] = (float)r2;
         a.grad[ob] = (float)r1;
       } else {
-        a.master[og] -= lr * (mode == 2 ? a.grad[og] * a.grad_scale : (float)r2);
-        a.master[ob] -= lr * (mode == 2 ? a.grad[ob] * a.grad_scale : (float)r1);
-        double s1, s2;
-        slot_sums(a.stat + (size_t)L * NSLOT * 128, c, s1, s2);
+        a.master[og] = mg - lr * (mode == 2 ? gg * a.grad_scale : (float)r2);
+        a.master[ob] = mb - lr * (mode == 2 ? gb * a.grad_scale : (float)r1);
         const double inv = (double)a.inv_n[L];
         const double mean = s1 * inv;
         double var = s2 * inv - mean * mean;
         var = var > 0.0 ? var : 0.0;
         const double nn = 1.0 / inv;
         const float m = a.bn_momentum;
-        float* mm = a.state + a.mm_off[L] + c;
-        float* mv = a.state + a.mv_off[L] + c;
-        *mm = (1.f - m) * *mm + m * (float)mean;
-        *mv = (1.f - m) * *mv + m * (float)(var * nn / (nn - 1.0));
+        *mm = (1.f - m) * mmv + m * (float)mean;
+        *mv = (1.f - m) * mvv + m * (float)(var * nn / (nn - 1.0));
       }
     }
     if (L == 0 && apply) {                       // batch loss / accuracy -> stats ring (fields 1, 2)
-      float ls = 0.f, cs = 0.f;
-      for (int q = tid; q < a.B; q += RT) { ls += a.loss_img[q]; cs += (float)a.correct_img[q]; }
+      float ls = lsv, cs = csv;
       ls = wave_sum(ls);
       cs = wave_sum(cs);
       if ((tid & 63) == 0) { lred[0][tid >> 6] = ls; lred[1][tid >> 6] = cs; }
