@@ -93,15 +93,16 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     float4 acc = *reinterpret_cast<const float4*>(a.b1 + n);
     const float* hp = a.h1part + (size_t)(r0 + r) * 384 + n;
     const size_t sstride = (size_t)a.B * 384;
-    int sp = 0;
-    for (; sp + 4 <= a.nsplit; sp += 4) {
-      float4 v[4];
+    // up to 9 split-K partials (every fc1_split the engine picks) loaded at once, branch-free
+    // (clamped to partial 0, zeroed after): one memory latency, not one per group of four
+    constexpr int SP = 9;
+    float4 v[SP];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const float4*>(hp + (sp + k) * sstride);
+    for (int k = 0; k < SP; ++k) v[k] = *reinterpret_cast<const float4*>(hp + (k < a.nsplit ? k : 0) * sstride);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
-    }
-    for (; sp < a.nsplit; ++sp) {
+    for (int k = 0; k < SP; ++k)
+      if (k < a.nsplit) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
+    for (int sp = SP; sp < a.nsplit; ++sp) {
       const float4 v = *reinterpret_cast<const float4*>(hp + sp * sstride);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
