@@ -18,14 +18,27 @@
 namespace dmlc {
 
 constexpr int KC = 128;                     // K chunk staged per phase (4 MFMA k-steps)
-constexpr int KC_LD = KC + 8;               // k-major tile row stride (bf16): 272-B rows, b128 reads conflict-free
-constexpr int MC_LD = 72;                   // m-major tile row stride (bf16): 144-B rows, tr reads conflict-free
+// LDS images, modelled with the gfx950 lane groups (MI355X_MICROARCH.md §LDS; tools/lds_banks.py):
+//  * k-major [64 rows][128 k]: 288-B rows (a row is 8 banks further on), so the 16 lanes of every
+//    ds_read_b128 group land on 64 distinct banks (272-B rows: 2-way, 8 cycles instead of 4);
+//  * m-major [128 k rows][64 cols]: unpadded 128-B rows with the 16-B chunk index XORed by row bits 1
+//    and 3 (mswz): the 8 rows {q, 8+q} a ds_read_b64_tr_b16 half-wave touches then cover all 64
+//    banks exactly once (any plain row pad: 2-way, 4 cycles instead of 2); the 16-B stores of a row
+//    stay one contiguous permuted row (conflict-free).
+constexpr int KC_LD = KC + 16;              // k-major tile row stride (bf16)
+constexpr int MC_LD = 64;                   // m-major tile row stride (bf16), swizzled by mswz
 constexpr int TILE_ELEMS = 64 * KC_LD > KC * MC_LD ? 64 * KC_LD : KC * MC_LD;
 constexpr int PIECES = 64 * KC / 8 / 256;   // 16-byte pieces per thread per operand per chunk (4)
 constexpr size_t GEMM_LDS = (size_t)2 * 2 * TILE_ELEMS * 2;
 
 // One operand's share of a 64-row x KC-deep chunk, held in registers between the global load and the
 // LDS store (so the next chunk's loads are in flight while the current chunk is multiplied).
+// element offset of (row, col) in the swizzled m-major image (col: multiple of 4)
+DEV int mswz(int row, int col) {
+  const int f = 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+  return row * MC_LD + (((col >> 3) ^ f) << 3) + (col & 7);
+}
+
 struct Chunk {
   uint4 v[PIECES];
   MDEV void load(const bf16* __restrict__ X, int ld, int kmajor, int R, int K, int r0, int k0, int tid) {
@@ -43,7 +56,7 @@ struct Chunk {
 #pragma unroll
     for (int i = 0; i < PIECES; ++i) {
       const int c = tid + i * 256;
-      const int off = kmajor ? (c >> 4) * KC_LD + 8 * (c & 15) : (c >> 3) * MC_LD + 8 * (c & 7);
+      const int off = kmajor ? (c >> 4) * KC_LD + 8 * (c & 15) : mswz(c >> 3, 8 * (c & 7));
       *reinterpret_cast<uint4*>(sm + off) = v[i];
     }
   }
@@ -52,7 +65,7 @@ struct Chunk {
 DEV bf16x8 frag(const bf16* sm, int kmajor, int rr0, int kk, int g, int li) {
   if (kmajor) return lds_b128(sm + (rr0 + li) * KC_LD + kk * 32 + 8 * g);
   const int q = li >> 2, p = li & 3;
-  return tr_frag(sm + (kk * 32 + 8 * g + q) * MC_LD + rr0 + 4 * p, sm + (kk * 32 + 8 * g + 4 + q) * MC_LD + rr0 + 4 * p);
+  return tr_frag(sm + mswz(kk * 32 + 8 * g + q, rr0 + 4 * p), sm + mswz(kk * 32 + 8 * g + 4 + q, rr0 + 4 * p));
 }
 
 DEV void colsum_block(const DmlcGemmProblem& P, int local, float* red) {

@@ -21,10 +21,20 @@
 namespace dmlc {
 
 constexpr int HT = 1024;     // 16 waves
-constexpr int W2_LD = 392;   // fc2 weights in LDS, [192 n][384 k] rows of 784 B (b128 row reads conflict-free)
+// fc2 weights in LDS, [192 n][384 k]: unpadded 768-B rows with the 16-B chunk index XORed by
+// w2h(row) = 2 (row & 3) + 8 ((row >> 3) & 1).  Modelled with the gfx950 lane groups
+// (tools/lds_banks.py): the ds_read_b128 row fragments (16 rows x one chunk per lane group) and the
+// ds_read_b64_tr_b16 column fragments (rows {q, 8+q} x two chunks per half-wave) both hit 64
+// distinct banks, and the staging stores stay conflict-free; 784-B padded rows were 2-way on both
+// reads (8 / 4 LDS cycles instead of 4 / 2).
+constexpr int W2_LD = 384;
 constexpr int H1_LD = 392;   // 784-B rows: 16-B aligned, rows land on distinct bank slots
 constexpr int H2_LD = 200;   // 400-B rows
 constexpr int DL_LD = 40;    // 80-B rows (k padded to 32 with zeros)
+
+DEV int w2swz(int row, int col) {
+  return row * W2_LD + (((col >> 3) ^ (2 * (row & 3) + 8 * ((row >> 3) & 1))) << 3) + (col & 7);
+}
 
 template <int RB>
 struct HeadLds {             // byte offsets into the dynamic LDS; RB real rows + one zero row
@@ -114,7 +124,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
       const int c = tid + i * HT, n2 = c / 48, k8 = c - n2 * 48;
-      *reinterpret_cast<uint4*>(w2s + n2 * W2_LD + k8 * 8) = wv[i];
+      *reinterpret_cast<uint4*>(w2s + w2swz(n2, k8 * 8)) = wv[i];
     }
     if (act) {
       const bf16x4 o = pack4(fmaxf(acc.x, 0.f), fmaxf(acc.y, 0.f), fmaxf(acc.z, 0.f), fmaxf(acc.w, 0.f));
@@ -127,9 +137,9 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
   // (b) h2 = relu(h1 W2 + b2): C[n][r] = sum_k W2t[n][k] h1[r][k], waves 0..11 = n tiles
   if (w < 12) {
     f32x4 acc = zero4();
-    const bf16* wa = w2s + (16 * w + li) * W2_LD + 8 * g;
 #pragma unroll
-    for (int ks = 0; ks < 12; ++ks) acc = mfma16(lds_b128(wa + ks * 32), lds_b128(h1s + rr * H1_LD + ks * 32 + 8 * g), acc);
+    for (int ks = 0; ks < 12; ++ks)
+      acc = mfma16(lds_b128(w2s + w2swz(16 * w + li, 8 * g + 32 * ks)), lds_b128(h1s + rr * H1_LD + ks * 32 + 8 * g), acc);
     const int n = 16 * w + 4 * g;
     const bf16x4 o = pack4(fmaxf(acc[0] + b2v.x, 0.f), fmaxf(acc[1] + b2v.y, 0.f),
                            fmaxf(acc[2] + b2v.z, 0.f), fmaxf(acc[3] + b2v.w, 0.f));
@@ -221,8 +231,7 @@ __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
     f32x4 acc = zero4();
 #pragma unroll
     for (int ks = 0; ks < 6; ++ks) {
-      const bf16x8 af = tr_frag(w2s + (32 * ks + 8 * g + q) * W2_LD + k0 + 4 * p,
-                                w2s + (32 * ks + 8 * g + 4 + q) * W2_LD + k0 + 4 * p);
+      const bf16x8 af = tr_frag(w2s + w2swz(32 * ks + 8 * g + q, k0 + 4 * p), w2s + w2swz(32 * ks + 8 * g + 4 + q, k0 + 4 * p));
       acc = mfma16(af, lds_b128(dh2s + rr * H2_LD + ks * 32 + 8 * g), acc);
     }
     const int n = k0 + 4 * g;

@@ -50,3 +50,56 @@ def conv2_A():
                     res.append(cycles(addr))
     return sum(res) / len(res)
 print("B old", conv2_B(swz_old), "B new", conv2_B(swz_new), "A", conv2_A())
+
+# --- grouped GEMM (cnn_gemm.hip) and head (cnn_head.hip) operand images ---------------------------
+G64 = [list(range(0, 32)), list(range(32, 64))]      # ds_read_b64 / ds_read_b64_tr_b16 lane groups
+
+
+def cycles_g(addr, groups, ndw):
+    tot = 0
+    for grp in groups:
+        banks = {}
+        for l in grp:
+            for d in range(ndw):
+                dw = addr[l] // 4 + d
+                banks.setdefault(dw % 64, set()).add(dw)
+        tot += max(len(v) for v in banks.values())
+    return tot
+
+
+def gemm_kmajor(ld):            # lds_b128(sm + (rr0 + li) * KC_LD + kk * 32 + 8 g): ideal 4
+    r = [cycles_g([2 * ((rr0 + (l & 15)) * ld + kk * 32 + 8 * (l >> 4)) for l in range(64)], G128, 4)
+         for kk in range(4) for rr0 in (0, 16, 32, 48)]
+    return sum(r) / len(r)
+
+
+def mswz(row, col, ld=64):      # cnn_gemm.hip mswz
+    f = 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1))
+    return row * ld + (((col >> 3) ^ f) << 3) + (col & 7)
+
+
+def gemm_mmajor(off):           # tr_frag rows kk*32 + 8g + hh + q, cols rr0 + 4p: ideal 2
+    r = []
+    for kk in range(4):
+        for rr0 in (0, 16, 32, 48):
+            for hh in (0, 4):
+                r.append(cycles_g([2 * off(kk * 32 + 8 * (l >> 4) + hh + ((l & 15) >> 2), rr0 + 4 * (l & 3))
+                                   for l in range(64)], G64, 2))
+    return sum(r) / len(r)
+
+
+def w2swz(row, col, ld=384):    # cnn_head.hip w2swz
+    return row * ld + (((col >> 3) ^ (2 * (row & 3) + 8 * ((row >> 3) & 1))) << 3) + (col & 7)
+
+
+def head_reads(off):            # (b) b128 row fragments, ideal 4; (f) tr column fragments, ideal 2
+    rb = [cycles_g([2 * off(16 * w + (l & 15), 8 * (l >> 4) + 32 * ks) for l in range(64)], G128, 4)
+          for w in range(12) for ks in range(12)]
+    rt = [cycles_g([2 * off(32 * ks + 8 * (l >> 4) + hh + ((l & 15) >> 2), 16 * w + 4 * (l & 3)) for l in range(64)],
+                   G64, 2) for w in range(24) for ks in range(6) for hh in (0, 4)]
+    return sum(rb) / len(rb), sum(rt) / len(rt)
+
+
+print("gemm k-major b128: KC_LD 136 ->", gemm_kmajor(136), " KC_LD 144 ->", gemm_kmajor(144))
+print("gemm m-major tr: MC_LD 72 ->", gemm_mmajor(lambda r, c: r * 72 + c), " swizzled 64 ->", gemm_mmajor(mswz))
+print("head fc2 (b128, tr): W2_LD 392 ->", head_reads(lambda r, c: r * 392 + c), " swizzled 384 ->", head_reads(w2swz))
