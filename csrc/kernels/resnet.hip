@@ -567,6 +567,15 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[j][n] = zero4();
 
+  // stem: the dataset rows of the block's images, once per image (thread i -> image b0 + i), published
+  // by the first loop barrier.  Evaluated per staged element, the generated-order index (a keyed
+  // Feistel, ~150 instructions) ran XIT times per thread per image batch.
+  [[maybe_unused]] int* srow = nullptr;
+  if constexpr (CIN == 3) {
+    __shared__ int srow_s[RT];
+    srow = srow_s;
+    if (b1 - b0 <= RT && tid < b1 - b0) srow_s[tid] = batch_index(a.src, a.B, b0 + tid);
+  }
   for (int bb = b0; bb < b1; bb += NB) {
     const int nb = min(NB, b1 - bb);
     __syncthreads();
@@ -577,7 +586,8 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
       for (int i = 0; i < G::XIT; ++i) {
         const int e = min(tid + i * RT, NB * G::XCH - 1);
         const int im = min(e / G::XCH, nb - 1), e1 = e - (e / G::XCH) * G::XCH;
-        const uint8_t* img = a.data + (size_t)batch_index(a.src, a.B, bb + im) * 3072;
+        const int row = b1 - b0 <= RT ? srow[bb - b0 + im] : batch_index(a.src, a.B, bb + im);
+        const uint8_t* img = a.data + (size_t)row * 3072;
         const int iy = e1 / HP - G::PADB, ix = e1 % HP - G::PADB;
         px3[i] = load_px_u8(img, a.cy, a.cx, iy, ix, iy >= 0 && iy < HIN && ix >= 0 && ix < HIN);
       }
