@@ -247,9 +247,15 @@ class FusedCifarEngine:
     # ------------------------------------------------------------------------------------------
     @staticmethod
     def _pick_fc1_split(B: int) -> int:
-        # aim for ~192 workgroups: (B/64) * 6 tiles * split
+        # the largest split in (9, 6, 4, 3, 2) whose (B/64) * 6 tiles * split workgroups stay <= 450;
+        # 9 makes each K slice 256 = two 128-deep chunks.  Whole-step sweeps (tools/sweep_fc.py,
+        # profiles/r2_v26_fc1_split_sweep.jsonl): B=256 9 -> 82.2 vs 8 -> 83.0 us, B=512 9 best,
+        # B=1024 4 -> 208.7 vs 2 -> 211.5 / 9 -> 211.7 us
         tiles = max(1, math.ceil(B / 64)) * 6
-        return int(max(1, min(9, round(192 / tiles))))
+        for s in (9, 6, 4, 3, 2):
+            if tiles * s <= 450:
+                return s
+        return 1
 
     def refresh_shadows(self):
         if self.fp8:    # exact amax of the current W2 for the shadow quantisation at this step
