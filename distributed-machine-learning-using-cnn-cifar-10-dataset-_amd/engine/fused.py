@@ -46,8 +46,14 @@ def _ops():
 
 
 SEG_OFF = [s.offset for s in M.PARAM_SPECS]
-# batch rows per head workgroup (2 or 4; DMLC_HEAD_ROWS overrides it for A/B runs)
-HEAD_ROWS = int(os.environ.get("DMLC_HEAD_ROWS", "4"))
+# batch rows per head workgroup (2 or 4; DMLC_HEAD_ROWS overrides it for A/B runs).  Default: 2 up
+# to B=256 (more workgroups on the otherwise idle chip: 82.6-83.1 vs 83.1-83.5 us per step at B=256,
+# profiles/r2_v26_head_rows_groups_sweep.txt), 4 above (every workgroup streams all of fc2's weights).
+HEAD_ROWS_ENV = os.environ.get("DMLC_HEAD_ROWS")
+
+
+def head_rows(B: int) -> int:
+    return int(HEAD_ROWS_ENV) if HEAD_ROWS_ENV else (2 if B <= 256 else 4)
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
 SEG = {M.short(s.name): s for s in M.PARAM_SPECS}
@@ -196,9 +202,9 @@ class FusedCifarEngine:
         self.dp1, self.dy2 = z(B, 12, 12, 64), z(B, 144, 64)
         self.part2, self.partb2 = z(self.g2, 1600, 64, dt=torch.float32), z(self.g2, 64, dt=torch.float32)
         self.part1, self.partb1 = z(self.g1, 80, 64, dt=torch.float32), z(self.g1, 64, dt=torch.float32)
-        # head: HEAD_ROWS batch rows per workgroup (B / HEAD_ROWS workgroups share the fc2 weight reads)
-        self.loss_part = z(B // HEAD_ROWS, dt=torch.float32)
-        self.correct_part = z(B // HEAD_ROWS, dt=torch.int32)
+        # head: head_rows(B) batch rows per workgroup (B / rows workgroups share the fc2 weight reads)
+        self.loss_part = z(B // head_rows(B), dt=torch.float32)
+        self.correct_part = z(B // head_rows(B), dt=torch.int32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ticket = torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)   # two-level arrival counters
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)

@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import dmlc  # noqa: E402,F401
-from dmlc.engine.fused import FusedCifarEngine  # noqa: E402
+from dmlc.engine.fused import FusedCifarEngine, head_rows  # noqa: E402
 
 
 def main():
@@ -31,7 +31,7 @@ def main():
             eng.run(400)
             torch.cuda.synchronize()
             best = min(best, (time.perf_counter() - t0) / 400)
-        print(json.dumps({"B": B, "head_rows": int(os.environ.get("DMLC_HEAD_ROWS", "4")), "fc1_split": sp,
+        print(json.dumps({"B": B, "head_rows": head_rows(B), "fc1_split": sp,
                           "us_per_step": round(best * 1e6, 2)}), flush=True)
         del eng
 
