@@ -48,7 +48,8 @@ def _ops():
 SEG_OFF = [s.offset for s in M.PARAM_SPECS]
 # batch rows per head workgroup (2 or 4; DMLC_HEAD_ROWS overrides it for A/B runs).  Default: 2 up
 # to B=256 (more workgroups on the otherwise idle chip: 82.6-83.1 vs 83.1-83.5 us per step at B=256,
-# profiles/r2_v26_head_rows_groups_sweep.txt), 4 above (every workgroup streams all of fc2's weights).
+# profiles/r2_v26_head_rows_groups_sweep.txt; same-session bench.py A/B at 400 steps 3.14-3.16 M vs
+# 3.12-3.15 M, profiles/r2_v27_head_rows_ab_b256.txt), 4 above (each workgroup streams all of fc2).
 HEAD_ROWS_ENV = os.environ.get("DMLC_HEAD_ROWS")
 
 
