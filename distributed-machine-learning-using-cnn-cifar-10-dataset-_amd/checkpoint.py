@@ -143,16 +143,18 @@ class CheckpointManager:
         prefix = os.path.join(self.log_dir, f"{PREFIX}-{int(step)}")
         write_bundle(prefix, tensors)
         if self.graph_info is not None:
+            # metagraph imports google.protobuf lazily (inside its builders), so a missing protobuf
+            # runtime surfaces from build/write, not from the module import: all of it is guarded,
+            # and the bundle + state file written around it keep the checkpoint usable
             try:
                 from .utils import metagraph as MG
-            except ImportError as e:          # protobuf runtime missing: checkpoints stay usable
-                print(f"[dmlc] graph.pbtxt / .meta not written ({e})", flush=True)
-                self.graph_info = None
-            else:
                 if self._meta is None:        # the variables never change: build once
                     self._meta = MG.build_meta_graph(tensors, max_to_keep=self.max_to_keep, **self.graph_info)
                     MG.write_graph_pbtxt(self.log_dir, self._meta)
                 MG.write_meta(prefix, self._meta)
+            except ImportError as e:          # protobuf runtime missing
+                print(f"[dmlc] graph.pbtxt / .meta not written ({e})", flush=True)
+                self.graph_info, self._meta = None, None
         self.kept = [p for p in self.kept if p != prefix] + [prefix]
         while self.max_to_keep and len(self.kept) > self.max_to_keep:
             old = self.kept.pop(0)

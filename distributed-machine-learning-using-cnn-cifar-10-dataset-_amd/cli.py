@@ -93,6 +93,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--steps_per_graph", type=int, default=d.steps_per_graph,
                    help="longest chain of training steps captured into one HIP graph")
     p.add_argument("--pg_timeout_s", type=float, default=d.pg_timeout_s)
+    p.add_argument("--heartbeat_s", type=float, default=d.heartbeat_s)
+    p.add_argument("--heartbeat_timeout_s", type=float, default=d.heartbeat_timeout_s,
+                   help="a peer silent this long makes the survivors exit 75 (0: off)")
+    p.add_argument("--check_replicas", type="bool", default=d.check_replicas,
+                   help="compare a parameter checksum across ranks at every output point")
     p.add_argument("--rccl_channels", type=int, default=d.rccl_channels,
                    help="RCCL channels (rings over different xGMI link permutations); 0 = RCCL's choice")
     p.add_argument("--graph", type="bool", default=d.graph)

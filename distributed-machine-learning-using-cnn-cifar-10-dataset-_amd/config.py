@@ -81,9 +81,12 @@ class TrainConfig:
     comm_dtype: str = "fp32"              # gradient all-reduce dtype: fp32 | bf16
     allreduce: str = "auto"               # gradient all-reduce: auto | rccl | xgmi (parallel/xgmi.py)
     dp_schedule: str = "auto"             # N>1 fused step: auto (measured at start) | serial | overlap
-    steps_per_graph: int = 8              # longest chain of training steps per HIP graph replay
+    steps_per_graph: int = 32             # longest chain of training steps per HIP graph replay (= bench.py)
     rccl_channels: int = 0                # >0: NCCL_MIN_NCHANNELS for RCCL over the 7 xGMI links (§5.8)
     pg_timeout_s: float = 300.0           # process-group timeout (fail-fast on a dead rank)
+    heartbeat_s: float = 1.0              # liveness beat interval (parallel/health.py); N>1 only
+    heartbeat_timeout_s: float = 20.0     # a peer silent this long -> exit 75 (0 disables the heartbeat)
+    check_replicas: bool = True           # compare a parameter checksum across ranks every output_every
     graph: bool = True                    # capture the fused step into a HIP graph
     trace: str = ""                       # '' | 'roctx' (phase ranges for rocprofv3 --marker-trace)
                                           #    | 'torch' (torch.profiler chrome trace in log_dir)

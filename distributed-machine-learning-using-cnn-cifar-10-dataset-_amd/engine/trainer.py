@@ -30,11 +30,12 @@ import torch
 from .. import checkpoint as CK
 from .. import config as C
 from ..parallel import dist as D
+from ..parallel import health as H
 from ..utils.events import EventsWriter, MetricsLog
 from ..utils.trace import Tracer
 
 
-EXIT_COMM_FAILURE = 75      # a peer stopped participating / no device progress: the launcher restarts
+EXIT_COMM_FAILURE = H.EXIT_COMM_FAILURE   # a peer stopped participating / no device progress / replicas diverged
 
 
 class CommFailure(RuntimeError):
@@ -122,6 +123,12 @@ class _FusedAdapter:
 
     def sync(self):
         torch.cuda.synchronize(self.eng.device)
+
+    def param_checksum(self) -> torch.Tensor:
+        return H.replica_checksum(self.eng.master)
+
+    def perturb_replica(self):            # fault injection (DMLC_FAULT_MODE=diverge)
+        self.eng.master[0] += 1e-3
 
 
 class _FusedResNetAdapter(_FusedAdapter):
@@ -225,6 +232,13 @@ class _EagerAdapter:
         if self.tr.device.type == "cuda":
             torch.cuda.synchronize(self.tr.device)
 
+    def param_checksum(self) -> torch.Tensor:
+        return H.replica_checksum(self.tr.model.flat)
+
+    def perturb_replica(self):            # fault injection (DMLC_FAULT_MODE=diverge)
+        with torch.no_grad():
+            self.tr.model.flat.data[0] += 1e-3
+
 
 def pick_impl(cfg: C.TrainConfig, device: torch.device) -> str:
     if cfg.impl != "auto":
@@ -249,11 +263,23 @@ def _fault_step() -> Optional[int]:
     return int(fs)
 
 
-def _fault_injection(step: int, rank: int):
+def _fault_injection(step: int, rank: int, engine=None):
+    """DMLC_FAULT_MODE: ``exit`` (default; the process dies, exit 17), ``stop`` (SIGSTOP: alive but
+    silent -- only the heartbeat can detect it), ``diverge`` (this rank's replica is perturbed: the
+    replica check must catch it)."""
     fs = _fault_step()
     if fs is not None and step == fs and rank == int(os.environ.get("DMLC_FAULT_RANK", "0")):
-        print(f"[fault-injection] rank {rank} exiting at global_step {step}", flush=True)
-        os._exit(17)
+        mode = os.environ.get("DMLC_FAULT_MODE", "exit")
+        if mode == "stop":
+            print(f"[fault-injection] rank {rank} stopping (SIGSTOP) at global_step {step}", flush=True)
+            import signal
+            os.kill(os.getpid(), signal.SIGSTOP)
+        elif mode == "diverge" and engine is not None:
+            print(f"[fault-injection] rank {rank} perturbing its replica at global_step {step}", flush=True)
+            engine.perturb_replica()
+        else:
+            print(f"[fault-injection] rank {rank} exiting at global_step {step}", flush=True)
+            os._exit(17)
 
 
 class Session:
@@ -329,20 +355,35 @@ class Session:
             time.sleep(0.0002)
         self.engine.check_comm()
 
+    def _check_replicas(self):
+        """Every synchronous replica must hold bit-identical parameters (parallel/health.py)."""
+        if self.info.world_size <= 1 or not self.cfg.check_replicas or not hasattr(self.engine, "param_checksum"):
+            return
+        cs = self.engine.param_checksum()
+        dev = self.info.device if self.info.backend == "nccl" else torch.device("cpu")
+        if not H.replicas_agree(cs, device=dev):
+            marker = H.mark_divergence(self.cfg.log_dir, f"rank {self.info.rank} global_step {self.engine.global_step} "
+                                                        f"allreduce={self.cfg.allreduce}")
+            raise CommFailure(f"replica divergence at global_step {self.engine.global_step} "
+                              f"(marker {marker}: the next start uses --allreduce=rccl)")
+
     def run(self) -> Dict[str, float]:
         cfg, eng = self.cfg, self.engine
         self.restore()
         self.save(force=True)            # CheckpointSaverHook.after_create_session
+        # the pre-capture step of start() is a real training step: it is fault-injectable and
+        # counts as a local iteration (i below), like every other step
+        start = eng.global_step
+        _fault_injection(eng.global_step, self.info.rank, eng)
         eng.start(log=self.log)
         self.log(f"[dmlc] engine={self.impl} model={cfg.model} dtype={cfg.dtype} batch={cfg.batch_size} "
                  f"world={self.info.world_size} device={self.info.device}")
         self.log("Starting Training")
-        start = eng.global_step
         last_t, last_step = time.time(), eng.global_step
         result = {}
         pending = None
         while eng.global_step < cfg.generations:        # StopAtStepHook(last_step=GENERATIONS)
-            _fault_injection(eng.global_step, self.info.rank)
+            _fault_injection(eng.global_step, self.info.rank, eng)
             i = eng.global_step - start                  # local iterations so far (the reference's i)
             n = self._chunk(eng.global_step, i)
             with self.tracer.range("steps"):
@@ -369,6 +410,7 @@ class Session:
                                                           "learning_rate": st["lr"]})
                 last_t, last_step = now, eng.global_step
                 result = dict(st, images_per_sec=ips)
+                self._check_replicas()
             if i % cfg.eval_every == 0:
                 self._wait_progress(pending)
                 with self.tracer.range("eval"):
@@ -381,8 +423,11 @@ class Session:
                 self._wait_progress(pending)             # never save weights of a broken exchange
                 with self.tracer.range("checkpoint"):
                     self.save()
-        eng.sync()
+        # the watchdog first: a collective captured in the last chunk that stalls on a dead peer must
+        # become a CommFailure (exit 75), not a rank blocked forever inside synchronize()
         self._wait_progress(pending)
+        eng.sync()
+        self._check_replicas()
         self.tracer.close()
         self.save(force=True)            # CheckpointSaverHook.end
         result["global_step"] = eng.global_step
@@ -406,10 +451,20 @@ def main(argv=None) -> int:
         return 0                          # unknown --job_name: the reference silently did nothing
     if role.kind == "ps":
         return D.serve_ps(role, log=lambda m: print(m, flush=True))
+    if cfg.allreduce == "auto" and H.divergence_marked(cfg.log_dir):
+        print(f"[dmlc] {os.path.join(cfg.log_dir, H.DIVERGENCE_MARKER)} exists (replicas diverged in an earlier "
+              "run): using --allreduce=rccl", flush=True)
+        cfg = cfg.replace(allreduce="rccl")
     info = D.init(D.role_info(role), device=cfg.device, timeout_s=cfg.pg_timeout_s, rccl_channels=cfg.rccl_channels)
+    hb = None
+    if info.world_size > 1 and cfg.heartbeat_timeout_s > 0:
+        hb = H.Heartbeat(info.rank, info.world_size, info.master_addr, info.master_port,
+                         interval_s=cfg.heartbeat_s, timeout_s=cfg.heartbeat_timeout_s).start()
     try:
         sess = Session(cfg, info, log=lambda m: print(m, flush=True))
         res = sess.run()
+        if hb is not None:
+            hb.stop(done=True)
         if info.rank == 0:
             print(f"done: {res}", flush=True)
         D.report_done(info)

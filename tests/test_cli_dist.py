@@ -232,3 +232,89 @@ def test_rccl_channel_env(monkeypatch):
     assert D.rccl_env(7) == {"NCCL_MIN_NCHANNELS": "28", "NCCL_MAX_NCHANNELS": "28"}
     from dmlc import cli
     assert cli.parse(["--rccl_channels=7"])[0].rccl_channels == 7
+
+
+# ---- bounded failure detection without the dmlc.launch supervisor (parallel/health.py) ----------------
+def _two_workers(tmp_path, extra_env, flags, timeout=200):
+    p1, p2 = cli.free_port(), cli.free_port()
+    hosts = [f"--worker_hosts=localhost:{p1},localhost:{p2}"]
+    env = _env()
+    env.update(extra_env)
+    ws = [subprocess.Popen([sys.executable, ENTRY, "--job_name=worker", f"--task_index={k}"] + hosts + COMMON + flags
+                           + [f"--log_dir={tmp_path}"], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                           text=True, start_new_session=True) for k in range(2)]
+    return ws
+
+
+@pytest.mark.timeout(300)
+def test_heartbeat_survivor_exits_75_when_peer_goes_silent(tmp_path):
+    """A SIGSTOPped peer (alive, silent) holds every collective: only the heartbeat can see it.  The
+    survivor must exit 75 within the heartbeat timeout (5 s here; the bound asked for is <= 30 s), not
+    after the 300 s process-group timeout -- launched as the reference's terminals, no supervisor."""
+    import signal
+    import time
+    ws = _two_workers(tmp_path, dict(DMLC_FAULT_STEP="6", DMLC_FAULT_RANK="1", DMLC_FAULT_MODE="stop"),
+                      ["--generations=100000", "--heartbeat_timeout_s=5", "--output_every=1000", "--eval_every=100000"])
+    try:
+        t0 = None
+        out0 = ""
+        deadline = time.time() + 240
+        while time.time() < deadline and ws[0].poll() is None:
+            time.sleep(0.2)
+        out0 = ws[0].communicate(timeout=30)[0]
+        assert ws[0].returncode == 75, out0
+        assert "silent for" in out0 and "exiting for restart" in out0, out0
+    finally:
+        for w in ws:
+            if w.poll() is None:
+                os.killpg(w.pid, signal.SIGKILL)
+                w.wait()
+    out1 = ws[1].communicate()[0]
+    assert "[fault-injection] rank 1 stopping (SIGSTOP) at global_step 6" in out1, out1
+
+
+@pytest.mark.timeout(300)
+def test_heartbeat_detection_time_is_bounded(tmp_path):
+    """Time from the peer's fault to the survivor's exit is within heartbeat timeout + slack."""
+    import signal
+    import time
+    ws = _two_workers(tmp_path, dict(DMLC_FAULT_STEP="4", DMLC_FAULT_RANK="1", DMLC_FAULT_MODE="stop"),
+                      ["--generations=100000", "--heartbeat_timeout_s=8", "--output_every=1000", "--eval_every=100000"])
+    try:
+        # wait for the fault line on rank 1 (its stdout is a pipe: read until it stops)
+        t_fault = None
+        deadline = time.time() + 200
+        while time.time() < deadline:
+            line = ws[1].stdout.readline()
+            if "stopping (SIGSTOP)" in line:
+                t_fault = time.time()
+                break
+            if not line and ws[1].poll() is not None:
+                break
+        assert t_fault is not None
+        ws[0].wait(timeout=60)
+        dt = time.time() - t_fault
+        assert ws[0].returncode == 75
+        assert dt <= 30.0, dt
+    finally:
+        for w in ws:
+            if w.poll() is None:
+                os.killpg(w.pid, signal.SIGKILL)
+                w.wait()
+
+
+@pytest.mark.timeout(300)
+def test_replica_divergence_is_detected_and_forces_rccl(tmp_path):
+    """A replica that stops matching the others (here: perturbed on rank 1) is caught at the next
+    output point on EVERY rank (exit 75), a marker is left in log_dir and the next start falls back
+    from the custom all-reduce to RCCL."""
+    ws = _two_workers(tmp_path, dict(DMLC_FAULT_STEP="3", DMLC_FAULT_RANK="1", DMLC_FAULT_MODE="diverge"),
+                      ["--generations=50", "--output_every=5", "--eval_every=100000"])
+    outs = [w.communicate(timeout=240)[0] for w in ws]
+    assert [w.returncode for w in ws] == [75, 75], outs
+    assert all("replica divergence at global_step 5" in o for o in outs), outs
+    assert os.path.exists(tmp_path / ".dmlc_replica_divergence")
+    ws = _two_workers(tmp_path, {}, ["--generations=6", "--output_every=5", "--eval_every=100000"])
+    outs = [w.communicate(timeout=240)[0] for w in ws]
+    assert [w.returncode for w in ws] == [0, 0], outs
+    assert "using --allreduce=rccl" in outs[0]

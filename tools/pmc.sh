@@ -28,6 +28,3 @@ for p in $PASSES; do
 done
 echo "pmc done"
 exit 0
-pass fetch FETCH_SIZE
-pass write WRITE_SIZE
-echo "pmc done"
