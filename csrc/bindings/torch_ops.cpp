@@ -138,6 +138,63 @@ void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const 
   CHECK_HIP(dmlc_conv2_dgrad(&a, stream_of(dp2)));
 }
 
+// channel-split forward / input gradient (cnn_split.hip): same tensors as conv1_fwd / conv2_fwd /
+// conv2_dgrad; the kernel batch must be a multiple of 8 (the engine pads it to 16)
+void conv1_fwd_split(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
+                     int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& out, const Tensor& am,
+                     const c10::optional<Tensor>& xraw, int64_t nsplit) {
+  const int64_t B = out.size(0);
+  TORCH_CHECK(B % 8 == 0, "split kernels need a batch multiple of 8");
+  TORCH_CHECK(nsplit == 2 || nsplit == 4, "conv1 split must be 2 or 4");
+  check_data(data);
+  TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
+  check(w1f, "w1f", at::kBFloat16, {64, 160});
+  check_numel(b1, "b1", at::kFloat, 64);
+  check(out, "out", at::kBFloat16, {B, 12, 12, 64});
+  check(am, "am", at::kByte, {B, 12, 12, 64});
+  c10::DeviceGuard guard(out.device());
+  DmlcConv1FwdArgs a;
+  a.data = data.data_ptr<uint8_t>();
+  a.src = index_src(idx, counter, period, B);
+  check_order_fits(a.src, data.size(0));
+  a.B = (int)B; a.cy = (int)cy; a.cx = (int)cx;
+  a.w = w1f.data_ptr(); a.bias = b1.data_ptr<float>();
+  a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>();
+  a.amax = nullptr;
+  a.xraw = xraw_ptr(xraw, B);
+  CHECK_HIP(dmlc_conv1_fwd_split(&a, (int)nsplit, stream_of(out)));
+}
+
+void conv2_fwd_split(const Tensor& in, const Tensor& w2f, const Tensor& b2, const Tensor& out, const Tensor& am) {
+  const int64_t B = in.size(0);
+  TORCH_CHECK(B % 8 == 0, "split kernels need a batch multiple of 8");
+  check(in, "in", at::kBFloat16, {B, 12, 12, 64});
+  check(w2f, "w2f", at::kBFloat16, {64, 1600});
+  check_numel(b2, "b2", at::kFloat, 64);
+  check(out, "out", at::kBFloat16, {B, 6, 6, 64});
+  check(am, "am", at::kByte, {B, 6, 6, 64});
+  c10::DeviceGuard guard(in.device());
+  DmlcConv2FwdArgs a;
+  a.in = in.data_ptr(); a.w = w2f.data_ptr(); a.bias = b2.data_ptr<float>();
+  a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>(); a.B = (int)B;
+  CHECK_HIP(dmlc_conv2_fwd_split(&a, stream_of(in)));
+}
+
+void conv2_dgrad_split(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const Tensor& dp1, const Tensor& dy2) {
+  const int64_t B = dp2.size(0);
+  TORCH_CHECK(B % 8 == 0, "split kernels need a batch multiple of 8");
+  check(dp2, "dp2", at::kBFloat16, {B, 6, 6, 64});
+  check(am2, "am2", at::kByte, {B, 6, 6, 64});
+  check(w2d, "w2d", at::kBFloat16, {64, 1600});
+  check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
+  c10::DeviceGuard guard(dp2.device());
+  DmlcConv2DgradArgs a;
+  a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
+  a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B;
+  CHECK_HIP(dmlc_conv2_dgrad_split(&a, stream_of(dp2)));
+}
+
 void conv2_dgrad_fp8(const Tensor& dp2, const Tensor& am2, const Tensor& w2d8, const Tensor& scale_w, const Tensor& dp1,
                      const Tensor& dy2) {
   const int64_t B = dp2.size(0);
@@ -456,6 +513,10 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(a!) p1, Tensor(b!) am1, Tensor w2f, Tensor b2, Tensor(c!) p2, Tensor(d!) am2, "
         "Tensor(e!)? xraw=None) -> ()");
   m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
+  m.def("conv1_fwd_split(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
+        "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? xraw, int nsplit) -> ()");
+  m.def("conv2_fwd_split(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
+  m.def("conv2_dgrad_split(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv2_dgrad_fp8(Tensor dp2, Tensor am2, Tensor w2d8, Tensor scale_w, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv2_dgrad_w1(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!)? dp1, Tensor(b!) dy2, Tensor am1, Tensor xraw, "
         "int cy, int cx, Tensor(c!) part1, Tensor(d!) partb1) -> ()");
@@ -485,6 +546,9 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("conv2_fwd_fp8", &conv2_fwd_fp8);
   m.impl("fp8_roundtrip", &fp8_roundtrip);
   m.impl("conv2_dgrad", &conv2_dgrad);
+  m.impl("conv1_fwd_split", &conv1_fwd_split);
+  m.impl("conv2_fwd_split", &conv2_fwd_split);
+  m.impl("conv2_dgrad_split", &conv2_dgrad_split);
   m.impl("conv2_dgrad_fp8", &conv2_dgrad_fp8);
   m.impl("conv2_dgrad_w1", &conv2_dgrad_w1);
   m.impl("conv1_wgrad", &conv1_wgrad);

@@ -25,34 +25,6 @@
 namespace dmlc {
 
 
-// ---------------------------------------------------------------------------------------------
-// conv1 input image: 24x24 crop of the uint8 NHWC image at (cy,cx), zero halo of 2, stored as
-// [28 rows][32 cols][4 ch] bf16 (col 28..31 and ch 3 zero).  Pixel (iy,ix) -> (iy+2, ix+2).
-constexpr int C1_XIN = 28 * 32 * 4;        // 3584 bf16
-constexpr int C1_OUT = 576 * 64;           // 36864 bf16
-
-// The whole 3 KB uint8 image in ONE 16-byte load per thread (threads 0..191) into LDS (`raw`), and
-// optionally out to xraw (the weight-gradient kernel then reads it without the index -> dataset
-// chain); then expanded from LDS.  Call stage_conv1_raw, barrier, stage_conv1_input.
-DEV void stage_conv1_raw(uint8_t* raw, const uint8_t* src, uint8_t* xraw, int tid) {
-  if (tid < 192) {
-    const uint4 v = reinterpret_cast<const uint4*>(src)[tid];
-    reinterpret_cast<uint4*>(raw)[tid] = v;
-    if (xraw) reinterpret_cast<uint4*>(xraw)[tid] = v;
-  }
-}
-
-DEV void stage_conv1_input(bf16* xin, const uint8_t* raw, int cy, int cx, int tid) {
-  for (int p = tid; p < 28 * 32; p += NT) {
-    const int r = p >> 5, c = p & 31;
-    const int iy = r - 2, ix = c - 2;
-    const bool ok = iy >= 0 && iy < 24 && ix >= 0 && ix < 24;
-    const uint8_t* s = raw + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);
-    const float c0 = s[0], c1 = s[1], c2 = s[2];
-    *reinterpret_cast<bf16x4*>(xin + p * 4) = ok ? pack4(c0, c1, c2, 0.f) : pack4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
 // conv1 implicit GEMM of one wave: co tiles 2cp, 2cp+1 (weights wa in registers) x pixel tiles
 // 9pq .. 9pq+8.  Software-pipelined: the 5 B fragments of pixel tile t+1 are read from LDS while tile
 // t's 10 MFMAs run (wait_lds retires tile t's reads first; see common.h).
@@ -152,8 +124,6 @@ __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
 // conv2-shaped implicit GEMM core shared by forward and dgrad:
 //   C[c_out][px] = sum_{kh,kw,c_in} Wt[c_out][(kh*5+kw)*64 + c_in] * Xpad[(y+kh)*16 + x+kw][c_in]
 // Xpad: LDS [16*16][64] bf16 (swizzled), wave w -> c_out tile 16w, 9 pixel tiles of 16.
-constexpr int C2_XIN = 256 * 64;
-constexpr int C2_OUT = 144 * 64;
 
 // conv2-shaped implicit GEMM core, weights staged through LDS.
 // The 64 x 1600 weight matrix is consumed one kh slice (64 co x 320 k, 40 KB) at a time.  Each slice

@@ -74,6 +74,37 @@ struct PrefetchAll {
   }
 };
 
+// conv1 input image: 24x24 crop of the uint8 NHWC image at (cy,cx), zero halo of 2, stored as
+// [28 rows][32 cols][4 ch] bf16 (col 28..31 and ch 3 zero).  Pixel (iy,ix) -> (iy+2, ix+2).
+constexpr int C1_XIN = 28 * 32 * 4;        // 3584 bf16
+constexpr int C1_OUT = 576 * 64;           // 36864 bf16
+
+// The whole 3 KB uint8 image in ONE 16-byte load per thread (threads 0..191) into LDS (`raw`), and
+// optionally out to xraw (the weight-gradient kernel then reads it without the index -> dataset
+// chain); then expanded from LDS.  Call stage_conv1_raw, barrier, stage_conv1_input.
+DEV void stage_conv1_raw(uint8_t* raw, const uint8_t* src, uint8_t* xraw, int tid) {
+  if (tid < 192) {
+    const uint4 v = reinterpret_cast<const uint4*>(src)[tid];
+    reinterpret_cast<uint4*>(raw)[tid] = v;
+    if (xraw) reinterpret_cast<uint4*>(xraw)[tid] = v;
+  }
+}
+
+DEV void stage_conv1_input(bf16* xin, const uint8_t* raw, int cy, int cx, int tid) {
+  for (int p = tid; p < 28 * 32; p += NT) {
+    const int r = p >> 5, c = p & 31;
+    const int iy = r - 2, ix = c - 2;
+    const bool ok = iy >= 0 && iy < 24 && ix >= 0 && ix < 24;
+    const uint8_t* s = raw + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);
+    const float c0 = s[0], c1 = s[1], c2 = s[2];
+    *reinterpret_cast<bf16x4*>(xin + p * 4) = ok ? pack4(c0, c1, c2, 0.f) : pack4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// conv2 input / output LDS images: padded [16*16][64] (swzpad) and [144][64] bf16
+constexpr int C2_XIN = 256 * 64;
+constexpr int C2_OUT = 144 * 64;
+
 DEV float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 DEV float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 

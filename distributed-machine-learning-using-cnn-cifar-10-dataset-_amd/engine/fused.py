@@ -75,7 +75,8 @@ class FusedCifarEngine:
                  process_group=None, seed: int = 0, fc1_split: Optional[int] = None, g1: Optional[int] = None,
                  g2: Optional[int] = None, stats_len: int = 4096, comm_dtype: str = "fp32",
                  capture_comm: Optional[bool] = None, dtype: str = "bf16", allreduce: str = "auto",
-                 dp_schedule: str = "serial", dp_force: bool = False, warmup_steps: int = 0):
+                 dp_schedule: str = "serial", dp_force: bool = False, warmup_steps: int = 0,
+                 conv_split: Optional[int] = None, conv1_split: Optional[int] = None):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -163,6 +164,16 @@ class FusedCifarEngine:
         self.merged_wgrad = os.environ.get("DMLC_SPLIT_WGRAD", "0") != "1"
         # conv1 and conv2 forward in one launch (bf16 path; DMLC_SPLIT_FWD=1: two launches)
         self.fused_fwd = os.environ.get("DMLC_SPLIT_FWD", "0") != "1"
+        # channel-split convolutions (cnn_split.hip): conv_split = 2 runs conv1 forward (conv1_split =
+        # 2 or 4 workgroups per image), conv2 forward and the conv2 input gradient as 2 workgroups per
+        # image, so a small batch fills the 256 CUs; 1 = one workgroup per image (cnn_conv.hip).
+        # DMLC_CONV_SPLIT / DMLC_CONV1_SPLIT override (A/B runs).
+        env_cs = int(os.environ.get("DMLC_CONV_SPLIT", "0")) or None
+        env_c1 = int(os.environ.get("DMLC_CONV1_SPLIT", "0")) or None
+        self.conv_split = 1 if self.fp8 else (conv_split or env_cs or (2 if B <= 256 else 1))
+        self.conv1_split = conv1_split or env_c1 or (4 if B <= 128 else 2)
+        if self.conv_split not in (1, 2) or self.conv1_split not in (2, 4):
+            raise ValueError(f"conv_split must be 1 or 2 and conv1_split 2 or 4 ({self.conv_split}, {self.conv1_split})")
         # DMLC_FUSED_W1=1: the conv1 weight gradient inside the conv2-dgrad launch (one slab per image,
         # dp1 stays in LDS) and a conv2-only weight-gradient launch on the whole chip.  Measured at
         # B=256 (r2): dgrad+w1 18.4 us + conv2 wgrad (40 pairs) 18.7 us = 37.1 us vs dgrad 11.2 us +
@@ -301,7 +312,11 @@ class FusedCifarEngine:
     # --- kernels ------------------------------------------------------------------------------
     def _forward(self, idx, counter, period, train=True, logits_out=None):
         o, p = self.ops, self.pv
-        if self.fused_fwd and not self.fp8:        # conv1 + pool1 + conv2 + pool2 in one launch
+        if self.conv_split == 2 and not self.fp8:  # channel-split: B * nsplit workgroups per conv
+            o.conv1_fwd_split(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
+                              self.am1, self.xraw if train else None, self.conv1_split)
+            o.conv2_fwd_split(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
+        elif self.fused_fwd and not self.fp8:      # conv1 + pool1 + conv2 + pool2 in one launch
             o.conv12_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
                          self.am1, self.w2f, p["conv2_bias"], self.p2, self.am2, self.xraw if train else None)
         else:
@@ -309,7 +324,7 @@ class FusedCifarEngine:
                         self.am1, self.amax_x if self.fp8 else None, self.xraw if train else None)
         if self.fp8:
             o.conv2_fwd_fp8(self.p1, self.w2f8[0], p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
-        elif not self.fused_fwd:
+        elif not self.fused_fwd and self.conv_split == 1:
             o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
         f = self._fc1_fwd
         o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
@@ -334,6 +349,8 @@ class FusedCifarEngine:
             return
         if self.fp8_dgrad:
             o.conv2_dgrad_fp8(self.dp2, self.am2, self.w2f8[1], self.scale_w, self.dp1, self.dy2)
+        elif self.conv_split == 2:
+            o.conv2_dgrad_split(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         else:
             o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         if self.merged_wgrad:

@@ -31,7 +31,7 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedu
     x, y = _data()
     eng = FusedCifarEngine(B, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
                            relu_logits=False, comm_dtype=comm_dtype, allreduce=allreduce,
-                           dp_schedule=schedule)
+                           dp_schedule=schedule, staircase=False)
     assert eng.comm_info["allreduce"] == ("xgmi" if allreduce == "xgmi" else "rccl"), eng.comm_info
     if allreduce == "xgmi":
         assert eng.comm_info["wire"] == comm_dtype, eng.comm_info      # bf16 no longer forces RCCL
@@ -46,37 +46,71 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedu
     dist.destroy_process_group()
 
 
-@pytest.mark.timeout(240)
-@pytest.mark.parametrize("graph,comm_dtype,allreduce,schedule",
-                         [(False, "fp32", "rccl", "overlap"), (True, "fp32", "rccl", "overlap"),
-                          (True, "bf16", "rccl", "overlap"), (False, "fp32", "xgmi", "overlap"),
-                          (True, "fp32", "xgmi", "overlap"), (True, "fp32", "rccl", "serial"),
-                          (False, "fp32", "xgmi", "serial"), (True, "fp32", "xgmi", "serial"),
-                          (True, "bf16", "xgmi", "serial")])
-def test_dp2_matches_single_process_union_batch(tmp_path, graph, comm_dtype, allreduce, schedule):
+def _dp_reference(world, B, steps, batches, comm_dtype, allreduce):
+    """Replays the data-parallel run on ONE world-1 engine: at every step each rank's gradient on its
+    own batch from the shared weights (the DP kernels compute exactly it / world: the loss scale
+    1/(B*world) is a power-of-two multiple of 1/B here, which commutes with every rounding), summed in
+    rank order like the xGMI kernel (bf16 wire: bf16 inputs, fp32 sum, bf16 result), then the SAME
+    apply-only SGD kernel.  Returns (initial, final) flat parameters."""
+    from dmlc.engine.fused import FusedCifarEngine
+    x, y = _data()
+    ref = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, staircase=False)
+    init = ref.flat_params().clone()
+    bf = (lambda t: t.to(torch.bfloat16).float()) if comm_dtype == "bf16" else (lambda t: t)
+    for s in range(steps):
+        tot = None
+        for r in range(world):
+            g = bf(ref.compute_gradients(idx=batches[r][s]).clone() / world)
+            tot = g if tot is None else tot + g
+        ref.grad.copy_(bf(tot))
+        ref._sgd(mode=2)
+    torch.cuda.synchronize()
+    return init, ref.flat_params()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,graph,comm_dtype,allreduce,schedule",
+                         [(2, False, "fp32", "rccl", "overlap"), (2, True, "fp32", "rccl", "overlap"),
+                          (2, True, "bf16", "rccl", "overlap"), (2, False, "fp32", "xgmi", "overlap"),
+                          (2, True, "fp32", "xgmi", "overlap"), (2, True, "fp32", "rccl", "serial"),
+                          (2, False, "fp32", "xgmi", "serial"), (2, True, "fp32", "xgmi", "serial"),
+                          (2, True, "bf16", "xgmi", "serial"), (4, True, "fp32", "rccl", "serial"),
+                          (4, True, "fp32", "xgmi", "serial"), (4, True, "fp32", "xgmi", "overlap"),
+                          (4, True, "bf16", "xgmi", "serial")])
+def test_dp_matches_mean_of_rank_gradients(tmp_path, world, graph, comm_dtype, allreduce, schedule):
+    """DP-2 / DP-4 (ranks sharing the test box's GPU; "rccl" runs over gloo here, RCCL on a node) for
+    10 steps against the exact replay of the DP semantics on one engine (_dp_reference): a bucket
+    offset, a missing or doubled 1/world or a stale bucket shows up as O(1e-2..1); what may remain is
+    fp32 summation order inside the collective (gloo's ring) -- asserted at 1e-5.  The replicas are
+    bit-identical to each other after every run."""
     import torch.multiprocessing as mp
     from dmlc.cli import free_port
-    from dmlc.engine.fused import FusedCifarEngine
-    B, steps = 32, 3
-    mp.spawn(_rank, args=(2, free_port(), str(tmp_path), B, steps, graph, comm_dtype, allreduce, schedule),
-             nprocs=2, join=True)
-    r0 = torch.load(tmp_path / "r0.pt", weights_only=True)
-    r1 = torch.load(tmp_path / "r1.pt", weights_only=True)
-    assert r0["step"] == r1["step"] == steps
-    assert torch.equal(r0["flat"], r1["flat"])           # replicas identical after every step
-    # single process, batch 2B: the generated order makes its batch of every step exactly the two
-    # ranks' batches of that step, in rank order (data/order.py)
-    x, y = _data()
-    ref = FusedCifarEngine(2 * B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False)
-    for s in range(steps):
-        assert torch.equal(ref.batch_indices(s), torch.cat([r0["batches"][s], r1["batches"][s]]))
-    init = ref.flat_params().clone()
-    for _ in range(steps):
-        ref.step()
-    torch.cuda.synchronize()
-    d_dp, d_ref = r0["flat"] - init, ref.flat_params() - init
+    B, steps = 32, 10
+    mp.spawn(_rank, args=(world, free_port(), str(tmp_path), B, steps, graph, comm_dtype, allreduce, schedule),
+             nprocs=world, join=True)
+    rs = [torch.load(tmp_path / f"r{k}.pt", weights_only=True) for k in range(world)]
+    assert all(r["step"] == steps for r in rs)
+    for r in rs[1:]:
+        assert torch.equal(rs[0]["flat"], r["flat"])      # replicas identical
+    init, want = _dp_reference(world, B, steps, [r["batches"] for r in rs], comm_dtype, allreduce)
+    d_dp, d_ref = rs[0]["flat"] - init, want - init
     rel = float((d_dp - d_ref).norm() / d_ref.norm())
-    assert rel < (2e-2 if comm_dtype == "bf16" else 1e-2), rel
+    tol = 1e-2 if (comm_dtype == "bf16" and allreduce == "rccl") else 1e-5
+    assert rel <= tol, rel
+    if allreduce == "xgmi" and world == 2:
+        assert torch.equal(rs[0]["flat"], want)           # same sums, same order, same kernels
+
+
+def test_dp_reference_union_batch_consistency():
+    """The generated order makes the W ranks' batches of a step exactly the union batch a single
+    process with batch W*B trains on (data/order.py), in rank order."""
+    from dmlc.engine.fused import FusedCifarEngine
+    x, y = _data()
+    single = FusedCifarEngine(64, x, y, device="cuda:0", seed=5)
+    from dmlc.data.order import OrderSpec
+    specs = [OrderSpec(x.shape[0], 32, 2, r, 5) for r in (0, 1)]
+    for s in (0, 1, 7, 15, 16, 40):
+        assert torch.equal(single.batch_indices(s).long(), torch.cat([sp.batch(s).long() for sp in specs]))
 
 
 def _tune_rank(rank, world, port, out, allreduce):

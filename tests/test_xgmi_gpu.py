@@ -169,3 +169,70 @@ def test_xgmi_allreduce_bf16_wire(tmp_path):
         for r in rs:
             assert r["self_test"] and r["err"] == 0
             assert torch.equal(r[key], want), (key, float((r[key] - want).abs().max()))
+
+
+def _rank_exact_w(rank, world, port, out, wire):
+    """One rank of the W-rank exact-sum check: two odd-sized buckets eager, then the whole buffer
+    captured into a HIP graph and replayed on fresh data."""
+    dist = _init(rank, world, port)
+    from dmlc.parallel.xgmi import XgmiAllReduce
+    ar = XgmiAllReduce(4 * 9973 + 4 * 3 * world, rank, world, wire=wire)
+    res = {"self_test": ar.self_test(), "n": ar.numel}
+    ar.buf.copy_(_data(rank, ar.numel, 10).cuda())
+    dist.barrier()
+    cut = 4 * 1237                     # neither bucket a multiple of W, of the block size or of 64
+    ar.all_reduce(0, cut)
+    ar.all_reduce(cut, ar.numel - cut)
+    torch.cuda.synchronize()
+    res["eager"] = ar.buf.cpu().clone()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        ar.all_reduce(0, ar.numel, 3)
+    torch.cuda.current_stream().wait_stream(s)
+    reps = []
+    for it in (11, 12):
+        ar.buf.copy_(_data(rank, ar.numel, it).cuda())
+        torch.cuda.synchronize()
+        dist.barrier()
+        g.replay()
+        torch.cuda.synchronize()
+        reps.append(ar.buf.cpu().clone())
+    res["graph"] = reps
+    res["err"] = ar.error()
+    dist.barrier()
+    ar.close()
+    torch.save(res, os.path.join(out, f"w{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("world,wire", [(3, "fp32"), (3, "bf16"), (8, "fp32"), (8, "bf16")])
+def test_xgmi_allreduce_w_ranks_exact(tmp_path, world, wire):
+    """W = 3 and W = 8 ranks (all on the test box's one GPU, each mapping every peer through HIP IPC as
+    on an 8-GPU node): every replica holds, bit for bit, the rank-ordered fp32 sum (bf16 wire: of the
+    bf16-rounded inputs, rounded to bf16) for two buckets whose sizes divide by nothing convenient,
+    eager and graph-replayed; no timeout.  The W = 3, 5-8 kernel instances had never executed."""
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    mp.spawn(_rank_exact_w, args=(world, free_port(), str(tmp_path), wire), nprocs=world, join=True)
+    rs = [torch.load(tmp_path / f"w{r}.pt", weights_only=True) for r in range(world)]
+    n = rs[0]["n"]
+    bf = (lambda t: t.to(torch.bfloat16).float()) if wire == "bf16" else (lambda t: t)
+
+    def want(it):
+        s = bf(_data(0, n, it))
+        for r in range(1, world):
+            s = s + bf(_data(r, n, it))
+        return bf(s)
+
+    for r in rs:
+        assert r["self_test"] and r["err"] == 0
+    w10 = want(10)
+    for r in rs:
+        assert torch.equal(r["eager"], w10), float((r["eager"] - w10).abs().max())
+    for k, it in enumerate((11, 12)):
+        w = want(it)
+        for r in rs:
+            assert torch.equal(r["graph"][k], w), (k, float((r["graph"][k] - w).abs().max()))

@@ -73,7 +73,7 @@ def main():
             slots[sl] = [round(float(np.median(d)), 2), round(float(d.max()), 2)]
         rec["slot_med_max_us"] = slots
         if NAMES[k] == "sgd":      # per block-role breakdown (see cnn_sgd.hip block ranges)
-            roles = {"conv2_rows": (0, 400), "conv1_rows": (400, 550), "conv_bias": (550, 552),
+            roles = {"conv1_rows": (0, 150), "conv_bias": (150, 152), "conv2_rows": (152, 552),
                      "fc1": (552, 769), "fc2": (769, 793), "fc_tail": (793, 802)}
             raw = t[k]
             for name, (lo, hi) in roles.items():
