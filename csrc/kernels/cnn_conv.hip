@@ -149,9 +149,32 @@ DEV void ws_dma(const bf16* Wg, int kh, bf16* buf, int w, int lane) {
   }
 }
 
+// s0: where kernel row 0 of the weights already sits (the caller issued its LDS-DMA at kernel entry,
+// so its latency hides behind the staging instead of opening the core), or null: the core copies it
+// into ws.  Rows 1..4 alternate between the two ws buffers (row kh in buffer kh & 1).
+DEV const bf16* slice_buf(const bf16* s0, const bf16* ws, int kh) { return kh == 0 ? s0 : ws + (kh & 1) * WS_ELEMS; }
+
+// The same copy through registers: the loads can be issued long before the LDS is free (kernel entry)
+// and stored once it is.  (An early LDS-DMA instead makes hipcc wait vmcnt(0) before every later LDS
+// read it cannot prove disjoint -- e.g. each pool iteration -- and its waits stop counting in order.)
+// (named members, passed by value: as an array hipcc kept the five chunks in scratch)
+struct Slice5 { uint4 a, b, c, d, e; };
+DEV uint4 ws_chunk(const bf16* Wg, int kh, int w, int lane, int i) {
+  const int P = (w * 5 + i) * 64 + lane, row = P / 40, pc = P - row * 40, lc = pc ^ (row & 7);
+  return *reinterpret_cast<const uint4*>(Wg + row * 1600 + kh * 320 + lc * 8);
+}
+DEV Slice5 ws_fetch(const bf16* Wg, int kh, int w, int lane) {
+  return Slice5{ws_chunk(Wg, kh, w, lane, 0), ws_chunk(Wg, kh, w, lane, 1), ws_chunk(Wg, kh, w, lane, 2),
+                ws_chunk(Wg, kh, w, lane, 3), ws_chunk(Wg, kh, w, lane, 4)};
+}
+DEV void ws_put(bf16* buf, int w, int lane, Slice5 v) {
+  uint4* p = reinterpret_cast<uint4*>(buf) + w * 5 * 64 + lane;
+  p[0] = v.a; p[64] = v.b; p[128] = v.c; p[192] = v.d; p[256] = v.e;
+}
+
 template <int NPX>
 DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][NPX], int pg, int cp,
-                    int g, int li, int tid) {
+                    int g, int li, int tid, const bf16* s0, int tk = -1) {
   const int w = wave_id(), lane = tid & 63, sw = li & 7;
   // Per-lane LDS element offsets, computed once: every fragment read of the loop is then one
   // ds_read_b128 at (offset register + compile-time immediate), no per-chunk address VALU (the swizzle
@@ -176,14 +199,15 @@ DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][N
   for (int s = 0; s < 2; ++s) ao[s] = (32 * cp + li) * 320 + (((4 * s + g) ^ sw) << 3);
 #pragma unroll
   for (int t = 0; t < NPX; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
-  ws_dma(Wg, 0, ws, w, lane);
+  if (!s0) ws_dma(Wg, 0, ws, w, lane);
+  const bf16* sb0 = s0 ? s0 : ws;
   __syncthreads();                                       // (waits vmcnt(0): the DMA has landed)
   // One k-chunk (kw, s) = 2 A + NPX B fragments.  The fragments of chunk j+1 are read into the other
   // register set BEFORE chunk j's MFMAs issue, so the LDS latency of a chunk hides behind the previous
   // chunk's MFMAs (lgkmcnt waits for the older reads only) instead of one exposed latency per chunk.
   auto load_chunk = [&](int kh, int j, bf16x8& a0, bf16x8& a1, bf16x8 (&bx)[NPX]) {
     const int kw = j >> 1, s = j & 1;
-    const bf16* wr = ws + (kh & 1) * WS_ELEMS + kw * 64 + ao[s];
+    const bf16* wr = slice_buf(sb0, ws, kh) + kw * 64 + ao[s];
     a0 = lds_b128(wr);
     a1 = lds_b128(wr + 16 * 320);
 #pragma unroll
@@ -211,24 +235,116 @@ DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][N
       __builtin_amdgcn_sched_barrier(0);
     }
     if (kh < 4) __syncthreads();                         // next slice landed; this one fully read
+    if (tk >= 0 && (kh == 0 || kh == 2)) DMLC_STAMP(tk, 5 + kh / 2);
   }
+  if (tk >= 0) DMLC_STAMP(tk, 7);
 }
 
-// fn(co_tile, px_tile, acc) for every finished 16x16 output tile of this wave.
+// Wide-tile variant (DMLC_CONV2_WIDE=1): wave w owns ALL 4 c_out tiles x pixel group pg x K half kk (input
+// channels 32kk..32kk+31 of every tap), pg = (w + kk) & 3 so the 3-tile group is not paired with itself
+// on a SIMD (waves w, w+4): per k-chunk 4 A + 2-3 B fragment reads for 8-12 MFMAs, i.e. 1250 instead
+// of 1700 ds_read_b128 per image (the core was LDS-bandwidth co-bound).  The two K halves meet once
+// through the slice buffer the last kernel row did not use (fixed order: deterministic).
+template <int NPX>
+DEV void conv2_core_wide(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[4][NPX], int pg, int kk,
+                         int g, int li, int tid, const bf16* s0) {
+  const int w = wave_id(), lane = tid & 63;
+  int xo[NPX][8];
+#pragma unroll
+  for (int t = 0; t < NPX; ++t) {
+    const int px = 16 * (pg + 4 * t) + li;
+    const int y = px / 12, x = px - y * 12;
+    const int pb = y * 16 + x, key0 = (x + 4 * y) & 7;
+#pragma unroll
+    for (int d = 0; d < 8; ++d) xo[t][d] = pb * 64 + (((4 * kk + g) ^ ((key0 + d) & 7)) << 3);
+  }
+  const int ao = li * 320 + (((4 * kk + g) ^ (li & 7)) << 3);
+#pragma unroll
+  for (int t = 0; t < NPX; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c][t] = zero4();
+  if (!s0) ws_dma(Wg, 0, ws, w, lane);
+  const bf16* sb0 = s0 ? s0 : ws;
+  __syncthreads();                                       // (waits vmcnt(0): the DMA has landed)
+  auto load_chunk = [&](int kh, int kw, bf16x8 (&a)[4], bf16x8 (&bx)[NPX]) {
+    const bf16* wr = slice_buf(sb0, ws, kh) + kw * 64 + ao;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a[c] = lds_b128(wr + c * 16 * 320);
+#pragma unroll
+    for (int t = 0; t < NPX; ++t) bx[t] = lds_b128(xin + xo[t][(kw + 4 * kh) & 7] + (kh * 16 + kw) * 64);
+  };
+#pragma unroll
+  for (int kh = 0; kh < 5; ++kh) {
+    if (kh < 4) ws_dma(Wg, kh + 1, ws + ((kh + 1) & 1) * WS_ELEMS, w, lane);
+    bf16x8 A[2][4], BX[2][NPX];
+    load_chunk(kh, 0, A[0], BX[0]);
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+      const int cur = kw & 1;
+      wait_lds();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kw + 1 < 5) load_chunk(kh, kw + 1, A[cur ^ 1], BX[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < NPX; ++t)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c][t] = mfma16(A[cur][c], BX[cur][t], acc[c][t]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (kh < 4) __syncthreads();                         // next slice landed; this one fully read
+  }
+}
+static_assert(9 * 4 * 64 * 16 <= WS_ELEMS * 2, "K-half partials fit one slice buffer");
+
+// fn(co_tile, px_tile, acc) for every finished 16x16 output tile (called by the waves that own it).
+// Default: the 2 co x 2-3 px tiling without a K split; DMLC_CONV2_WIDE=1 (a variant build) selects the
+// wide tiles -- measured 0.8-1.3 % SLOWER per step at B = 128 / 256 / 512 (r3, same-session A/B), so the
+// core is not bound by its LDS read bandwidth.
 template <class F>
-DEV void conv2_tiles(const bf16* Wg, const bf16* xin, bf16* ws, int w, int g, int li, int tid, F&& fn) {
+DEV void conv2_tiles(const bf16* Wg, const bf16* xin, bf16* ws, int w, int g, int li, int tid, const bf16* s0,
+                     F&& fn, int tk = -1) {
+#if !defined(DMLC_CONV2_WIDE) || !DMLC_CONV2_WIDE
   const int cp = w & 1, pg = w >> 1;
   if (pg == 0) {
     f32x4 acc[2][3];
-    conv2_core<3>(Wg, xin, ws, acc, pg, cp, g, li, tid);
+    conv2_core<3>(Wg, xin, ws, acc, pg, cp, g, li, tid, s0, tk);
 #pragma unroll
     for (int t = 0; t < 3; ++t) { fn(2 * cp, pg + 4 * t, acc[0][t]); fn(2 * cp + 1, pg + 4 * t, acc[1][t]); }
   } else {
     f32x4 acc[2][2];
-    conv2_core<2>(Wg, xin, ws, acc, pg, cp, g, li, tid);
+    conv2_core<2>(Wg, xin, ws, acc, pg, cp, g, li, tid, s0, tk);
 #pragma unroll
     for (int t = 0; t < 2; ++t) { fn(2 * cp, pg + 4 * t, acc[0][t]); fn(2 * cp + 1, pg + 4 * t, acc[1][t]); }
   }
+#else
+  const int kk = w >> 2, pg = (w + kk) & 3, lane = tid & 63;
+  f32x4* red = reinterpret_cast<f32x4*>(ws + WS_ELEMS);   // slice buffer 1: free after kernel row 3
+  auto finish = [&](auto& acc, auto npx) {
+    constexpr int NPX = decltype(npx)::value;
+    if (kk == 1) {
+#pragma unroll
+      for (int t = 0; t < NPX; ++t)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) red[((pg + 4 * t) * 4 + c) * 64 + lane] = acc[c][t];
+    }
+    lds_barrier();
+    if (kk == 0) {
+#pragma unroll
+      for (int t = 0; t < NPX; ++t)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) fn(c, pg + 4 * t, acc[c][t] + red[((pg + 4 * t) * 4 + c) * 64 + lane]);
+    }
+  };
+  if (pg == 0) {
+    f32x4 acc[4][3];
+    conv2_core_wide<3>(Wg, xin, ws, acc, pg, kk, g, li, tid, s0);
+    finish(acc, std::integral_constant<int, 3>{});
+  } else {
+    f32x4 acc[4][2];
+    conv2_core_wide<2>(Wg, xin, ws, acc, pg, kk, g, li, tid, s0);
+    finish(acc, std::integral_constant<int, 2>{});
+  }
+#endif
 }
 
 __global__ __launch_bounds__(NT, 1) void k_conv2_fwd(DmlcConv2FwdArgs a) {
@@ -254,16 +370,16 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd(DmlcConv2FwdArgs a) {
     const int s = tid + i * NT;
     *reinterpret_cast<uint4*>(xin + swzpad(s >> 3, s & 7)) = v[i];
   }
-  float b4[2][4];
+  ws_dma(reinterpret_cast<const bf16*>(a.w), 0, ws, w, lane);   // kernel row 0, landed by the core's barrier
+  float b4[4][4];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) b4[h][i] = a.bias[32 * (w & 1) + 16 * h + 4 * g + i];
-  __syncthreads();
+    for (int i = 0; i < 4; ++i) b4[c][i] = a.bias[16 * c + 4 * g + i];
   DMLC_STAMP(DMLC_TK_CONV2_FWD, 1);
 
-  conv2_tiles(reinterpret_cast<const bf16*>(a.w), xin, ws, w, g, li, tid, [&](int ct, int t, const f32x4& acc) {
-    store_relu_tile(cout, 16 * t + li, 16 * ct + 4 * g, acc, b4[ct & 1]);
+  conv2_tiles(reinterpret_cast<const bf16*>(a.w), xin, ws, w, g, li, tid, ws, [&](int ct, int t, const f32x4& acc) {
+    store_relu_tile(cout, 16 * t + li, 16 * ct + 4 * g, acc, b4[ct]);
   });
   __syncthreads();
   DMLC_STAMP(DMLC_TK_CONV2_FWD, 2);
@@ -283,6 +399,8 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
   DMLC_STAMP(DMLC_TK_DGRAD, 0);
   stage16<288>(dp2, reinterpret_cast<const bf16*>(a.dp2) + (size_t)b * 2304, tid);
   stage16<144>(am2, a.am2 + (size_t)b * 2304, tid);
+  // kernel row 0 of the weights into registers: in flight during the pool backward (see ws_fetch)
+  const Slice5 s0v = ws_fetch(reinterpret_cast<const bf16*>(a.wd), 0, w, lane);
   bf16* dy2 = reinterpret_cast<bf16*>(a.dy2) + (size_t)b * 9216;
 
   // halo of the padded 16x16 grad image
@@ -291,24 +409,35 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
     const int r = pix >> 4, col = pix & 15;
     if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(dyp + swzpad(pix, c)) = bf16x8{};
   }
-  __syncthreads();
+  lds_barrier();   // (not __syncthreads: its vmcnt(0) would wait for the row-0 loads right here)
   DMLC_STAMP(DMLC_TK_DGRAD, 1);
-  for (int task = tid; task < 36 * 8; task += NT) {
-    const int win = task >> 3, c = task & 7, py = win / 6, px = win - py * 6;
+  static_assert(36 * 8 <= NT, "one pool-bwd task per thread");
+  const int win = tid >> 3, pc = tid & 7, py = win / 6, px = win - py * 6;
+  bf16x8 dv[4];
+  if (tid < 36 * 8) {
     float o[4][8];
-    pool_bwd_2x2<6>(dp2, am2, py, px, c, o);
+    pool_bwd_2x2<6>(dp2, am2, py, px, pc, o);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
-      const bf16x8 v = to_bf16x8(o[k]);
-      *reinterpret_cast<bf16x8*>(dyp + swzpad((y + 2) * 16 + x + 2, c)) = v;
-      *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8) = v;
+      dv[k] = to_bf16x8(o[k]);
+      *reinterpret_cast<bf16x8*>(dyp + swzpad((y + 2) * 16 + x + 2, pc)) = dv[k];
+    }
+  }
+  // kernel row 0 into its slice buffer BEFORE the dy2 stores go out: the wait for the row-0 loads
+  // then cannot include them (a store in one branch of a join makes hipcc wait vmcnt(0))
+  ws_put(ws, w, lane, s0v);                        // published by the core's first barrier
+  if (tid < 36 * 8) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
+      *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + pc * 8) = dv[k];
     }
   }
   lds_barrier();   // publishes dyp only; the dy2 global stores need not drain here
   DMLC_STAMP(DMLC_TK_DGRAD, 2);
 
-  conv2_tiles(reinterpret_cast<const bf16*>(a.wd), dyp, ws, w, g, li, tid, [&](int ct, int t, const f32x4& acc) {
+  conv2_tiles(reinterpret_cast<const bf16*>(a.wd), dyp, ws, w, g, li, tid, ws, [&](int ct, int t, const f32x4& acc) {
     const int px = 16 * t + li, cb = 16 * ct + 4 * g;
     const bf16x4 v = pack4(acc[0], acc[1], acc[2], acc[3]);
     *reinterpret_cast<bf16x4*>(outs + swz128(px, cb >> 3) + ((cb >> 2) & 1) * 4) = v;
@@ -362,6 +491,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_w1(DmlcConv2DgradArgs a, 
   dma_kb(img, w1.xraw + (size_t)b * 3072, 3, w, lane);
   stage16<288>(dp2, reinterpret_cast<const bf16*>(a.dp2) + (size_t)b * 2304, tid);
   stage16<144>(am2, a.am2 + (size_t)b * 2304, tid);
+  ws_dma(reinterpret_cast<const bf16*>(a.wd), 0, ws, w, lane);  // kernel row 0 of the weights
   bf16* dy2 = reinterpret_cast<bf16*>(a.dy2) + (size_t)b * 9216;
   for (int s = tid; s < 2048; s += NT) {           // halo of the padded 16x16 grad image
     const int pix = s >> 3, c = s & 7;
@@ -385,7 +515,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_w1(DmlcConv2DgradArgs a, 
   lds_barrier();   // publishes dyp only; the dy2 global stores need not drain here
   DMLC_STAMP(DMLC_TK_DGRAD, 2);
 
-  conv2_tiles(reinterpret_cast<const bf16*>(a.wd), dyp, ws, w, g, li, tid, [&](int ct, int t, const f32x4& acc) {
+  conv2_tiles(reinterpret_cast<const bf16*>(a.wd), dyp, ws, w, g, li, tid, ws, [&](int ct, int t, const f32x4& acc) {
     const int px = 16 * t + li, cb = 16 * ct + 4 * g;
     *reinterpret_cast<bf16x4*>(outs + px * 64 + cb) = pack4(acc[0], acc[1], acc[2], acc[3]);
   });
@@ -421,6 +551,9 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_w1(DmlcConv2DgradArgs a, 
 // round-tripping through global memory and a second launch (p1 / am1 are still written for the
 // backward).  LDS: [0, 80 KB) conv1 input + output, then conv2's two weight-slice buffers;
 // [80, 112 KB) conv2's padded input; [112, 130 KB) conv2's output.
+// Kernel row 0 of the conv2 weights is loaded into registers at entry and stored into the first
+// slice buffer after pool1: its L2 latency hides behind conv1 instead of opening the conv2 core
+// (~1 us of the core's first row, r3 phase stamps).
 constexpr size_t C12_WS = 0, C12_XIN2 = 81920, C12_OUT2 = C12_XIN2 + C2_XIN * 2;
 constexpr size_t C12_LDS = C12_OUT2 + C2_OUT * 2;
 static_assert((C1_XIN + C1_OUT) * 2 <= C12_XIN2 && WS_BYTES <= C12_XIN2, "conv12 LDS map");
@@ -436,16 +569,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
   const int g = lane >> 4, li = lane & 15, cp = w & 1, pq = w >> 1;
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 
-  const int img = batch_index(a1.src, a1.B, b);
-  uint8_t* raw = reinterpret_cast<uint8_t*>(cout);          // the conv1 output region is free until its epilogue
-  stage_conv1_raw(raw, a1.data + (size_t)img * 3072, a1.xraw ? a1.xraw + (size_t)b * 3072 : nullptr, tid);
-  __syncthreads();
-  stage_conv1_input(xin, raw, a1.cy, a1.cx, tid);
-  // conv2's padded input: zero halo (rows/cols 0,1,14,15); the interior comes from pool1
-  for (int s = tid; s < 2048; s += NT) {
-    const int pix = s >> 3, c = s & 7, r = pix >> 4, col = pix & 15;
-    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(xin2 + swzpad(pix, c)) = bf16x8{};
-  }
+  // conv1 weights / biases first: in flight together with the index -> image chain
   const bf16* W = reinterpret_cast<const bf16*>(a1.w) + (32 * cp + li) * 160 + 8 * g;
   bf16x8 wa[2][5];
 #pragma unroll
@@ -457,7 +581,20 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int i = 0; i < 4; ++i) b4[h][i] = a1.bias[32 * cp + 16 * h + 4 * g + i];
-  __syncthreads();
+  const int img = batch_index(a1.src, a1.B, b);
+  uint8_t* raw = reinterpret_cast<uint8_t*>(cout);          // the conv1 output region is free until its epilogue
+  stage_conv1_raw(raw, a1.data + (size_t)img * 3072, a1.xraw ? a1.xraw + (size_t)b * 3072 : nullptr, tid);
+  lds_barrier();   // (the xraw copy's global stores need not drain)
+  stage_conv1_input(xin, raw, a1.cy, a1.cx, tid);
+  // conv2's padded input: zero halo (rows/cols 0,1,14,15); the interior comes from pool1
+  for (int s = tid; s < 2048; s += NT) {
+    const int pix = s >> 3, c = s & 7, r = pix >> 4, col = pix & 15;
+    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(xin2 + swzpad(pix, c)) = bf16x8{};
+  }
+  // conv2 kernel row 0 into registers, in flight during conv1 + pool1 (issued after every load that
+  // conv1 waits for, so those waits count past it); stored to LDS once pool1 has freed the conv1 region
+  const Slice5 s0v = ws_fetch(reinterpret_cast<const bf16*>(a2.w), 0, w, lane);
+  lds_barrier();
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 1);
 
   {
@@ -469,20 +606,21 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
       for (int h = 0; h < 2; ++h)
         store_relu_tile(cout, (pq * 9 + t) * 16 + li, 32 * cp + 16 * h + 4 * g, acc[h][t], b4[h]);
   }
-  __syncthreads();
+  lds_barrier();
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 2);
   pool_emit<24>(cout, reinterpret_cast<bf16*>(a1.out) + (size_t)b * 9216, a1.am + (size_t)b * 9216, tid, nullptr, xin2);
-  float c2b[2][4];
+  float c2b[4][4];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) c2b[h][i] = a2.bias[32 * (w & 1) + 16 * h + 4 * g + i];
-  __syncthreads();                                     // conv2 input complete; conv1 region free
+    for (int i = 0; i < 4; ++i) c2b[c][i] = a2.bias[16 * c + 4 * g + i];
+  lds_barrier();                                       // conv2 input complete; conv1 region free
+  ws_put(ws, w, lane, s0v);                            // published by the core's first barrier
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 3);
 
-  conv2_tiles(reinterpret_cast<const bf16*>(a2.w), xin2, ws, w, g, li, tid, [&](int ct, int t, const f32x4& acc) {
-    store_relu_tile(cout2, 16 * t + li, 16 * ct + 4 * g, acc, c2b[ct & 1]);
-  });
+  conv2_tiles(reinterpret_cast<const bf16*>(a2.w), xin2, ws, w, g, li, tid, ws, [&](int ct, int t, const f32x4& acc) {
+    store_relu_tile(cout2, 16 * t + li, 16 * ct + 4 * g, acc, c2b[ct]);
+  }, DMLC_TK_CONV1_FWD);
   __syncthreads();
   pool_emit<12>(cout2, reinterpret_cast<bf16*>(a2.out) + (size_t)b * 2304, a2.am + (size_t)b * 2304, tid);
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 4);

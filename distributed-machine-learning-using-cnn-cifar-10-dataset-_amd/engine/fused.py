@@ -170,8 +170,10 @@ class FusedCifarEngine:
         # DMLC_CONV_SPLIT / DMLC_CONV1_SPLIT override (A/B runs).
         env_cs = int(os.environ.get("DMLC_CONV_SPLIT", "0")) or None
         env_c1 = int(os.environ.get("DMLC_CONV1_SPLIT", "0")) or None
-        self.conv_split = 1 if self.fp8 else (conv_split or env_cs or (2 if B <= 256 else 1))
-        self.conv1_split = conv1_split or env_c1 or (4 if B <= 128 else 2)
+        # same-session A/B (r3): B=128 73.5 us (split, conv1 2-way) vs 74.6 (conv1 4-way) vs 79.0 (one
+        # workgroup per image); B=256 85.1 vs 82.9 -- the split pays only while the chip is not full
+        self.conv_split = 1 if self.fp8 else (conv_split or env_cs or (2 if B <= 128 else 1))
+        self.conv1_split = conv1_split or env_c1 or 2
         if self.conv_split not in (1, 2) or self.conv1_split not in (2, 4):
             raise ValueError(f"conv_split must be 1 or 2 and conv1_split 2 or 4 ({self.conv_split}, {self.conv1_split})")
         # DMLC_FUSED_W1=1: the conv1 weight gradient inside the conv2-dgrad launch (one slab per image,

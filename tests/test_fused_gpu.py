@@ -285,11 +285,11 @@ def test_fused_dgrad_conv1_wgrad_matches_separate_launches(B, monkeypatch):
     equal to that group's slab, the whole gradient equal up to fp32 summation order."""
     data, labels = _synthetic(4 * B, seed=8)
     monkeypatch.setenv("DMLC_FUSED_W1", "1")
-    fused = FusedCifarEngine(B, data, labels, seed=9)
+    fused = FusedCifarEngine(B, data, labels, seed=9, conv_split=1)   # the per-image dgrad core in both
     assert fused.fused_w1 and fused.g1 == B
     g_f = fused.compute_gradients().cpu().clone()
     monkeypatch.setenv("DMLC_FUSED_W1", "0")
-    ref = FusedCifarEngine(B, data, labels, seed=9, g2=fused.groups2)
+    ref = FusedCifarEngine(B, data, labels, seed=9, g2=fused.groups2, conv_split=1)
     assert not ref.fused_w1
     g_r = ref.compute_gradients().cpu().clone()
     assert torch.equal(fused.dy2, ref.dy2)

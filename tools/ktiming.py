@@ -29,6 +29,8 @@ NK, NB, NS = 8, 1024, 8
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--graph", action="store_true",
+                    help="time the second step of a 2-step graph chain (kernels back to back, as in bench.py)")
     a = ap.parse_args()
     g = torch.Generator().manual_seed(0)
     data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
@@ -39,8 +41,15 @@ def main():
     for _ in range(5):
         eng.step()
     torch.cuda.synchronize()
-    lib.dmlc_timing_clear()
-    eng.step()
+    if a.graph:
+        eng.capture(steps_per_graph=2)
+        eng.run(4)
+        torch.cuda.synchronize()
+        lib.dmlc_timing_clear()
+        eng.chains[2].replay()
+    else:
+        lib.dmlc_timing_clear()
+        eng.step()
     torch.cuda.synchronize()
     buf = np.zeros(NK * NB * NS, dtype=np.uint64)
     assert lib.dmlc_timing_read(buf.ctypes.data_as(ctypes.c_void_p)) == 0
