@@ -182,6 +182,10 @@ class FusedCifarEngine:
         # merged wgrad ~26 us -- equal, and the SGD pays for 256 per-image slabs: off by default.
         self.fused_w1 = self.merged_wgrad and os.environ.get("DMLC_FUSED_W1", "0") == "1"
         self.keep_dp1 = False          # tests: also write the pool1 gradient to global memory
+        # single-GPU step with the fc weight gradients + fc SGD on a second graph branch (they feed
+        # nothing on the conv backward path): main = dp2 GEMM -> conv backward -> (join) -> conv SGD;
+        # side = dW1/dW2/dW3/db GEMMs -> fc SGD.  DMLC_FC_BRANCH=0/1 overrides the default.
+        self.fc_branch = os.environ.get("DMLC_FC_BRANCH", "0") == "1"
         # conv2 weight gradient: one block per (input-channel quarter, image group), one fp32 slab per
         # group (self.g2 = groups = slabs the SGD kernel reduces); conv1: one block per image group.
         # DMLC_W2_GROUPS / DMLC_W1_GROUPS override the defaults (kbench sweeps).
@@ -198,7 +202,9 @@ class FusedCifarEngine:
             # both in one launch of g1 + 4 * g2 <= 256 blocks (one wave of workgroups); multiples of 8
             # keep every group's images on one XCD (cnn_wgrad.hip).  B=256: 128 + 4*32 -> 19.1 us vs
             # 96 + 4*40 -> 19.8, 64 + 4*48 -> 23.4 (r2, register-staged conv1 scatter)
-            g2_ = max(1, min(B, 32, B // 8))
+            # (B=128: 32 groups of 4 images -> 69.2 us per step vs 16 groups of 8 -> 73.7, r3 sweep;
+            # B=256: 32 -> 81.7 vs 24 -> 85.1, 40 -> 83.1, 48 -> 86.8)
+            g2_ = max(1, min(B, 32, B // 4))
             self.g2 = g2 or (g2_ // 8 * 8 if g2_ >= 8 else g2_)
             # conv1: the CUs the conv2 blocks leave (one block per CU; past B=256 every block takes
             # several images instead of the grid growing beyond the chip)
@@ -245,6 +251,12 @@ class FusedCifarEngine:
                     + _gemm_params(384, 8, B, 384, 0, 8, 0, 1, 3, nvalid=384)      # db1
                     + _gemm_params(192, 8, B, 192, 0, 8, 0, 1, 3, nvalid=192)      # db2
                     + _gemm_params(16, 8, B, 16, 0, 8, 0, 1, 3, nvalid=10)))       # db3
+        # the same problems as two launches: dp2 (conv backward path) | the fc weight / bias gradients
+        fb = self._fc_bwd
+        self._fc_dx = {k: fb[k][:1] for k in ("A", "B", "C", "bias")}
+        self._fc_dx["params"] = fb["params"][:12]
+        self._fc_dw = {k: fb[k][1:] for k in ("A", "B", "C", "bias")}
+        self._fc_dw["params"] = fb["params"][12:]
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.chains: Dict[int, Optional[torch.cuda.CUDAGraph]] = {}   # k -> graph of k chained steps
@@ -445,6 +457,9 @@ class FusedCifarEngine:
 
     def _eager_step(self):
         if not self.dp:
+            if self.fc_branch:
+                self._branched_step()
+                return
             self._seg_compute_a()
             self._seg_compute_b()
             return
@@ -452,6 +467,23 @@ class FusedCifarEngine:
             self._serial_dp_step([self._seg_compute_ab, self._seg_apply])
             return
         self._dp_step([self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv])
+
+    def _branched_step(self):
+        """Single-GPU step on two graph branches (fc_branch): the fc weight gradients and the fc SGD
+        run beside the conv backward; the conv SGD (which bumps global_step) after the join."""
+        o = self.ops
+        self._forward(self.bidx, None, 1, train=True)
+        f = self._fc_dx
+        o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
+        main = torch.cuda.current_stream(self.device)
+        self.side_stream.wait_stream(main)
+        with torch.cuda.stream(self.side_stream):
+            f = self._fc_dw
+            o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
+            self._sgd(mode=0, roles=2, finalize=False)
+        self._conv_backward()
+        main.wait_stream(self.side_stream)
+        self._sgd(mode=0, roles=1, finalize=True)
 
     def _seg_compute_ab(self):
         self._seg_compute_a()

@@ -301,3 +301,25 @@ def test_fused_dgrad_conv1_wgrad_matches_separate_launches(B, monkeypatch):
     for s in M.PARAM_SPECS:
         a, b = g_f[s.offset:s.offset + s.numel], g_r[s.offset:s.offset + s.numel]
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()) + 1e-12), s.name
+
+
+@pytest.mark.parametrize("B", [128, 256])
+def test_fc_branch_step_is_bit_identical(B, monkeypatch):
+    """DMLC_FC_BRANCH=1: the fc weight gradients + fc SGD on a second graph branch beside the conv
+    backward, the conv SGD after the join.  Same kernels on the same data: after graph-replayed steps
+    the parameters, step counter and stats equal the one-branch step bit for bit."""
+    data, labels = _synthetic(8 * B, seed=41)
+    kw = dict(seed=40, lr=1e-4, relu_logits=False)     # (lr 1e-2 on raw pixels diverges to NaN in ~4 steps)
+    ref = FusedCifarEngine(B, data, labels, **kw)
+    monkeypatch.setenv("DMLC_FC_BRANCH", "1")
+    br = FusedCifarEngine(B, data, labels, **kw)
+    assert br.fc_branch and not ref.fc_branch
+    for eng in (ref, br):
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(7)
+    torch.cuda.synchronize()
+    assert ref.global_step() == br.global_step() == 8
+    assert torch.isfinite(ref.master).all()
+    assert torch.equal(ref.master, br.master)
+    assert ref.read_stats(8) == br.read_stats(8)
