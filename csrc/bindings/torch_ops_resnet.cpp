@@ -38,19 +38,28 @@ float* det_ptr(const c10::optional<Tensor>& det, int64_t B) {
   return det->data_ptr<float>();
 }
 
+// nvalid: the first nvalid images are real, the rest batch padding (0: all B); every BatchNorm mean is
+// over the real images only
+int64_t valid_count(int64_t nvalid, int64_t B) {
+  const int64_t nv = nvalid > 0 ? nvalid : B;
+  TORCH_CHECK(nv >= 1 && nv <= B, "nvalid must be in [1, B]");
+  return nv;
+}
+
 void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::optional<Tensor>& data,
             const c10::optional<Tensor>& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
             int64_t cx, const c10::optional<Tensor>& z_prev, const c10::optional<Tensor>& stat_prev,
             const c10::optional<Tensor>& gamma_prev, const c10::optional<Tensor>& beta_prev,
             const c10::optional<Tensor>& sc_src, int64_t sc_mode, const c10::optional<Tensor>& a_out, const Tensor& w,
-            const Tensor& z, const Tensor& stat, const c10::optional<Tensor>& stat_det) {
+            const Tensor& z, const Tensor& stat, const c10::optional<Tensor>& stat_det, int64_t nvalid) {
   const Geom g = geom(cin, cout, hin, stride);
-  const int64_t B = z.size(0);
+  const int64_t B = z.size(0), nv = valid_count(nvalid, B);
   check(w, "w", at::kBFloat16, {g.cout, g.kp()});
   check(z, "z", at::kBFloat16, {B, g.hout(), g.hout(), g.cout});
   check_stat(stat, "stat");
   DmlcRnFwdArgs a{};
   a.B = (int)B;
+  a.nvalid = (int)nv;
   if (cin == 3) {
     TORCH_CHECK(data.has_value() && idx.has_value(), "rn_fwd stem needs data and idx");
     check_data(*data);
@@ -76,7 +85,7 @@ void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::o
     a.z_prev = z_prev->data_ptr(); a.stat_prev = stat_prev->data_ptr<double>();
     a.gamma_prev = gamma_prev->data_ptr<float>(); a.beta_prev = beta_prev->data_ptr<float>();
     a.sc_src = sc_mode ? sc_src->data_ptr() : nullptr; a.sc_mode = (int)sc_mode;
-    a.a_out = a_out->data_ptr(); a.inv_n_prev = 1.f / (float)(B * hin * hin);
+    a.a_out = a_out->data_ptr(); a.inv_n_prev = 1.f / (float)(nv * hin * hin);
   }
   a.w = w.data_ptr(); a.z = z.data_ptr(); a.stat = stat.data_ptr<double>();
   a.stat_det = det_ptr(stat_det, B);
@@ -89,9 +98,9 @@ DmlcRnDgradArgs dgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
                            const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd,
                            const Tensor& a_prev, const Tensor& z_prev, const Tensor& stat_prev,
                            const c10::optional<Tensor>& gy_sc, int64_t sc_mode, const Tensor& gy_prev,
-                           const Tensor& red_prev, const c10::optional<Tensor>& red_det) {
+                           const Tensor& red_prev, const c10::optional<Tensor>& red_det, int64_t nvalid) {
   TORCH_CHECK(cin >= 16, "rn_dgrad: the stem has no input gradient");
-  const int64_t B = gy.size(0), ho = g.hout();
+  const int64_t B = gy.size(0), ho = g.hout(), nv = valid_count(nvalid, B);
   check(gy, "gy", at::kBFloat16, {B, ho, ho, cout});
   check(z, "z", at::kBFloat16, {B, ho, ho, cout});
   check_stat(stat, "stat"); check_stat(red, "red"); check_stat(stat_prev, "stat_prev"); check_stat(red_prev, "red_prev");
@@ -110,10 +119,11 @@ DmlcRnDgradArgs dgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
   }
   DmlcRnDgradArgs a{};
   a.gy = gy.data_ptr(); a.z = z.data_ptr(); a.stat = stat.data_ptr<double>(); a.red = red.data_ptr<double>();
-  a.gamma = gamma.data_ptr<float>(); a.inv_n = 1.f / (float)(B * ho * ho);
+  a.gamma = gamma.data_ptr<float>(); a.inv_n = 1.f / (float)(nv * ho * ho);
   a.wd = wd.data_ptr();
   a.a_prev = a_prev.data_ptr(); a.z_prev = z_prev.data_ptr(); a.stat_prev = stat_prev.data_ptr<double>();
-  a.inv_n_prev = 1.f / (float)(B * hin * hin);
+  a.inv_n_prev = 1.f / (float)(nv * hin * hin);
+  a.nvalid = (int)nv;
   a.gy_sc = sc_mode ? gy_sc->data_ptr() : nullptr; a.sc_mode = (int)sc_mode;
   a.gy_prev = gy_prev.data_ptr(); a.red_prev = red_prev.data_ptr<double>(); a.B = (int)B;
   a.red_det = det_ptr(red_det, B);
@@ -123,10 +133,10 @@ DmlcRnDgradArgs dgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
 void rn_dgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
               const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
               const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
-              const Tensor& gy_prev, const Tensor& red_prev, const c10::optional<Tensor>& red_det) {
+              const Tensor& gy_prev, const Tensor& red_prev, const c10::optional<Tensor>& red_det, int64_t nvalid) {
   const Geom g = geom(cin, cout, hin, stride);
   const DmlcRnDgradArgs a = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
-                                       gy_sc, sc_mode, gy_prev, red_prev, red_det);
+                                       gy_sc, sc_mode, gy_prev, red_prev, red_det, nvalid);
   c10::DeviceGuard guard(gy.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_dgrad(&gc, &a, stream_of(gy)));
@@ -136,8 +146,8 @@ DmlcRnWgradArgs wgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
                            const c10::optional<Tensor>& data, const c10::optional<Tensor>& idx,
                            const c10::optional<Tensor>& counter, int64_t period, int64_t cy, int64_t cx,
                            const c10::optional<Tensor>& x, const Tensor& gy, const Tensor& z, const Tensor& stat,
-                           const Tensor& red, const Tensor& gamma, const Tensor& part) {
-  const int64_t B = gy.size(0), ho = g.hout(), G = part.size(0);
+                           const Tensor& red, const Tensor& gamma, const Tensor& part, int64_t nvalid) {
+  const int64_t B = gy.size(0), ho = g.hout(), G = part.size(0), nv = valid_count(nvalid, B);
   check(gy, "gy", at::kBFloat16, {B, ho, ho, cout});
   check(z, "z", at::kBFloat16, {B, ho, ho, cout});
   check_stat(stat, "stat"); check_stat(red, "red");
@@ -158,18 +168,18 @@ DmlcRnWgradArgs wgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
     a.x = x->data_ptr();
   }
   a.gy = gy.data_ptr(); a.z = z.data_ptr(); a.stat = stat.data_ptr<double>(); a.red = red.data_ptr<double>();
-  a.gamma = gamma.data_ptr<float>(); a.inv_n = 1.f / (float)(B * ho * ho);
-  a.part = part.data_ptr<float>(); a.G = (int)G; a.B = (int)B;
+  a.gamma = gamma.data_ptr<float>(); a.inv_n = 1.f / (float)(nv * ho * ho);
+  a.part = part.data_ptr<float>(); a.G = (int)G; a.B = (int)B; a.nvalid = (int)nv;
   return a;
 }
 
 void rn_wgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::optional<Tensor>& data,
               const c10::optional<Tensor>& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
               int64_t cx, const c10::optional<Tensor>& x, const Tensor& gy, const Tensor& z, const Tensor& stat,
-              const Tensor& red, const Tensor& gamma, const Tensor& part) {
+              const Tensor& red, const Tensor& gamma, const Tensor& part, int64_t nvalid) {
   const Geom g = geom(cin, cout, hin, stride);
   const DmlcRnWgradArgs a = wgrad_args(g, cin, cout, hin, data, idx, counter, period, cy, cx, x, gy, z, stat, red,
-                                       gamma, part);
+                                       gamma, part, nvalid);
   c10::DeviceGuard guard(gy.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_wgrad(&gc, &a, stream_of(gy)));
@@ -179,12 +189,13 @@ void rn_wgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10:
 void rn_bwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
             const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
             const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
-            const Tensor& gy_prev, const Tensor& red_prev, const Tensor& part, const c10::optional<Tensor>& red_det) {
+            const Tensor& gy_prev, const Tensor& red_prev, const Tensor& part, const c10::optional<Tensor>& red_det,
+            int64_t nvalid) {
   const Geom g = geom(cin, cout, hin, stride);
   const DmlcRnDgradArgs d = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
-                                       gy_sc, sc_mode, gy_prev, red_prev, red_det);
+                                       gy_sc, sc_mode, gy_prev, red_prev, red_det, nvalid);
   const DmlcRnWgradArgs w = wgrad_args(g, cin, cout, hin, c10::nullopt, c10::nullopt, c10::nullopt, 1, 0, 0, a_prev, gy,
-                                       z, stat, red, gamma, part);
+                                       z, stat, red, gamma, part, nvalid);
   c10::DeviceGuard guard(gy.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_bwd(&gc, &d, &w, stream_of(gy)));
@@ -194,8 +205,8 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
              const Tensor& fcw, const Tensor& fcb, const Tensor& labels, const Tensor& idx,
              const c10::optional<Tensor>& counter, int64_t period, double inv_batch, const Tensor& gy,
              const Tensor& red, const Tensor& fc_part, const Tensor& loss_img, const Tensor& correct_img,
-             const c10::optional<Tensor>& logits, const c10::optional<Tensor>& red_det) {
-  const int64_t B = z.size(0);
+             const c10::optional<Tensor>& logits, const c10::optional<Tensor>& red_det, int64_t nvalid) {
+  const int64_t B = z.size(0), nv = valid_count(nvalid, B);
   check(z, "z", at::kBFloat16, {B, 8, 8, 64});
   check_stat(stat, "stat"); check_stat(red, "red");
   check_numel(gamma, "gamma", at::kFloat, 64);
@@ -211,7 +222,7 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
   check_numel(correct_img, "correct_img", at::kInt, B);
   DmlcRnHeadArgs a{};
   a.z = z.data_ptr(); a.stat = stat.data_ptr<double>(); a.gamma = gamma.data_ptr<float>();
-  a.beta = beta.data_ptr<float>(); a.inv_n = 1.f / (float)(B * 64);
+  a.beta = beta.data_ptr<float>(); a.inv_n = 1.f / (float)(nv * 64);
   a.sc = sc.data_ptr(); a.fcw = fcw.data_ptr<float>(); a.fcb = fcb.data_ptr<float>();
   a.labels = labels.data_ptr<int>(); a.src = index_src(idx, counter, period, B);
   check_order_fits(a.src, labels.size(0));
@@ -225,6 +236,7 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
     a.logits_out = logits->data_ptr<float>();
   }
   a.B = (int)B;
+  a.nvalid = (int)nv;
   c10::DeviceGuard guard(z.device());
   CHECK_HIP(dmlc_rn_head(&a, stream_of(z)));
 }
@@ -242,7 +254,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
             at::TensorList wd, const Tensor& stat, const Tensor& red, const Tensor& fc_part, const Tensor& loss_img,
             const Tensor& correct_img, const Tensor& step, const Tensor& ticket, const Tensor& stats, int64_t mode,
             double lr0, double decay, double decay_steps, bool staircase, double bn_momentum, double warmup,
-            int64_t layer_lo, int64_t layer_hi, bool tail) {
+            int64_t layer_lo, int64_t layer_hi, bool tail, int64_t nvalid) {
   constexpr int L = DMLC_RN_LAYERS;
   TORCH_CHECK(layer_lo >= 0 && layer_lo <= layer_hi && layer_hi <= L, "rn_sgd: bad layer range");
   TORCH_CHECK(tail || mode == 0, "rn_sgd: a partial (tail=False) launch is mode 0 only");
@@ -250,7 +262,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
   TORCH_CHECK(conv_off.size() == L && gamma_off.size() == L && beta_off.size() == L && mm_off.size() == L &&
                   mv_off.size() == L, "rn_sgd: 19 offsets per table");
   TORCH_CHECK(part.size() == L && wf.size() == L && wd.size() == L, "rn_sgd: 19 slabs / shadows");
-  const int64_t B = loss_img.numel();
+  const int64_t B = loss_img.numel(), nv = valid_count(nvalid, B);
   dev(master, "master"); dev(state, "state");
   TORCH_CHECK(master.scalar_type() == at::kFloat && state.scalar_type() == at::kFloat, "master/state must be fp32");
   const int64_t np = master.numel(), ns = state.numel();
@@ -292,7 +304,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
       check(wd[l], "wd", at::kBFloat16, {g.cin, g.kpd()});
       a.wd[l] = wd[l].data_ptr();
     }
-    a.inv_n[l] = 1.f / (float)(B * g.hout() * g.hout());
+    a.inv_n[l] = 1.f / (float)(nv * g.hout() * g.hout());
   }
   a.stat = stat.data_ptr<double>(); a.red = red.data_ptr<double>();
   a.state = state.data_ptr<float>(); a.bn_momentum = (float)bn_momentum;
@@ -305,6 +317,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
   a.ticket = reinterpret_cast<unsigned int*>(ticket.data_ptr<int>());
   a.loss_img = loss_img.data_ptr<float>(); a.correct_img = correct_img.data_ptr<int>();
   a.stats = stats.data_ptr<float>(); a.stats_len = (int)stats.size(0);
+  a.nvalid = (int)nv;
   c10::DeviceGuard guard(master.device());
   CHECK_HIP(dmlc_rn_sgd(&a, stream_of(master)));
 }
@@ -314,26 +327,27 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
 TORCH_LIBRARY_FRAGMENT(dmlc, m) {
   m.def("rn_fwd(int cin, int cout, int hin, int stride, Tensor? data, Tensor? idx, Tensor? counter, int period, "
         "int cy, int cx, Tensor? z_prev, Tensor? stat_prev, Tensor? gamma_prev, Tensor? beta_prev, Tensor? sc_src, "
-        "int sc_mode, Tensor(a!)? a_out, Tensor w, Tensor(b!) z, Tensor(c!) stat, Tensor(d!)? stat_det=None) -> ()");
+        "int sc_mode, Tensor(a!)? a_out, Tensor w, Tensor(b!) z, Tensor(c!) stat, Tensor(d!)? stat_det=None, "
+        "int nvalid=0) -> ()");
   m.def("rn_dgrad(int cin, int cout, int hin, int stride, Tensor gy, Tensor z, Tensor stat, Tensor red, "
         "Tensor gamma, Tensor wd, Tensor a_prev, Tensor z_prev, Tensor stat_prev, Tensor? gy_sc, int sc_mode, "
-        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!)? red_det=None) -> ()");
+        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!)? red_det=None, int nvalid=0) -> ()");
   m.def("rn_wgrad(int cin, int cout, int hin, int stride, Tensor? data, Tensor? idx, Tensor? counter, int period, "
         "int cy, int cx, Tensor? x, Tensor gy, Tensor z, Tensor stat, Tensor red, Tensor gamma, "
-        "Tensor(a!) part) -> ()");
+        "Tensor(a!) part, int nvalid=0) -> ()");
   m.def("rn_bwd(int cin, int cout, int hin, int stride, Tensor gy, Tensor z, Tensor stat, Tensor red, "
         "Tensor gamma, Tensor wd, Tensor a_prev, Tensor z_prev, Tensor stat_prev, Tensor? gy_sc, int sc_mode, "
-        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part, Tensor(d!)? red_det=None) -> ()");
+        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part, Tensor(d!)? red_det=None, int nvalid=0) -> ()");
   m.def("rn_head(Tensor z, Tensor stat, Tensor gamma, Tensor beta, Tensor sc, Tensor fcw, Tensor fcb, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, Tensor(a!) gy, Tensor(b!) red, "
         "Tensor(c!) fc_part, Tensor(d!) loss_img, Tensor(e!) correct_img, Tensor(f!)? logits, "
-        "Tensor(g!)? red_det=None) -> ()");
+        "Tensor(g!)? red_det=None, int nvalid=0) -> ()");
   m.def("rn_sgd(Tensor(a!) master, Tensor(b!)? grad, float grad_scale, Tensor(c!) state, int[] conv_off, "
         "int[] gamma_off, int[] beta_off, int[] mm_off, int[] mv_off, int fcw_off, int fcb_off, Tensor[] part, "
         "Tensor(d!)[] wf, Tensor(e!)[] wd, Tensor stat, Tensor red, Tensor fc_part, Tensor loss_img, "
         "Tensor correct_img, Tensor(f!) step, Tensor(g!) ticket, Tensor(h!) stats, int mode, float lr0, "
         "float decay, float decay_steps, bool staircase, float bn_momentum, float warmup=0.0, int layer_lo=0, "
-        "int layer_hi=19, bool tail=True) -> ()");
+        "int layer_hi=19, bool tail=True, int nvalid=0) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

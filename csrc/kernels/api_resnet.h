@@ -8,6 +8,9 @@
 //   fwd   w [COUT][KP]  k  = tap*CINP + ci        (tap = kh*3 + kw, CINP = max(CIN, 8), KP = 9*CINP -> x32)
 //   dgrad wd [CIN][KPD] k' = tap'*COUT + co       (tap' = 8 - tap: rotated 180 degrees, KPD = 9*COUT -> x32)
 // Layer l computes z_l = conv_l(x_l) with x_l = a_{l-1}, a = relu(bn(z) [+ shortcut]).
+// Any batch size: the kernels run on B (a multiple of 16) images, the first `nvalid` real; the padding
+// images are excluded from every BatchNorm statistic (inv_n = 1 / (nvalid * H * W)) and get exactly zero
+// loss weight and gradient, so the step equals the eager model's at batch nvalid.
 #pragma once
 #include "api.h"
 
@@ -32,6 +35,7 @@ struct DmlcRnFwdArgs {
   double* stat;              // [NSLOT][2][64] accumulators of layer l
   float* stat_det;           // nullable: deterministic side buffer [B][128] fp32 partials + 8x32 tickets
   int B;
+  int nvalid;                // images b >= nvalid are batch padding: no contribution to the statistics
 };
 
 struct DmlcRnDgradArgs {
@@ -46,6 +50,7 @@ struct DmlcRnDgradArgs {
   double* red_prev;          // [NSLOT][2][64]
   float* red_det;            // nullable: deterministic side buffer of red_prev (see stat_det)
   int B;
+  int nvalid;                // padding images (b >= nvalid) get g_z = 0 (their g_y is 0 already)
 };
 
 struct DmlcRnWgradArgs {
@@ -54,6 +59,7 @@ struct DmlcRnWgradArgs {
   const void* gy; const void* z; const double* stat; const double* red; const float* gamma; float inv_n;
   float* part;               // [G][KP][COUT] fp32 split-K slabs
   int G, B;
+  int nvalid;                // padding images contribute nothing (g_z = 0)
 };
 
 struct DmlcRnHeadArgs {
@@ -68,6 +74,7 @@ struct DmlcRnHeadArgs {
   float* loss_img; int* correct_img;    // [B]
   float* logits_out;         // nullable [B][10]
   int B;
+  int nvalid;                // images b >= nvalid: no loss, no accuracy, zero gradient
 };
 
 #define DMLC_RN_LAYERS 19
@@ -97,6 +104,7 @@ struct DmlcRnSgdArgs {
   unsigned int* ticket;
   const float* loss_img; const int* correct_img;
   float* stats; int stats_len;
+  int nvalid;                // valid images of the batch (loss / accuracy means)
 };
 
 hipError_t dmlc_rn_fwd(const DmlcRnLayerGeom* g, const DmlcRnFwdArgs* a, hipStream_t s);

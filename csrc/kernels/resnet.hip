@@ -337,6 +337,10 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
     for (int r = 0; r < 4; ++r) { s1[r] += acc[i][r]; s2[r] += acc[i][r] * acc[i][r]; }
   }
   if (TS) DMLC_STAMP(0, 4);                       // 4: z stored, partial sums ready
+  if (b >= a.nvalid) {                            // batch padding: not part of the BN statistics
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[r] = 0.f; s2[r] = 0.f; }
+  }
   reduce_flush<F::CT, COUT>(s1, s2, red, a.stat, w, g, li, tid, a.stat_det, a.B);
   if (TS) DMLC_STAMP(0, 5);                       // 5: statistics flushed (end)
 }
@@ -396,7 +400,7 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
       const int q = (ok ? oy * HOUT + ox : 0) * C8 + c8;
       gv[i] = gyp[q];
       zv[i] = zp[q];
-      okv[i] = ok && (tid + i * RT) < D::NCH;
+      okv[i] = ok && (tid + i * RT) < D::NCH && b < a.nvalid;   // padding image: g_z = 0
     }
     lds_barrier();
     float A[8], Bc[8], Cc[8];
@@ -634,11 +638,13 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
         if (e < NB * G::GCH) {
           const int im = e / G::GCH, e1 = e - im * G::GCH;
           const uint32_t gw[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w}, zw[4] = {zv[i].x, zv[i].y, zv[i].z, zv[i].w};
+          const bool real = bb + im < a.nvalid;          // batch padding: g_z = 0
           uint32_t ow[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            ow[k] = pack2(A[2 * k] * bf16_lo(gw[k]) + Bc[2 * k] * bf16_lo(zw[k]) + Cc[2 * k],
-                          A[2 * k + 1] * bf16_hi(gw[k]) + Bc[2 * k + 1] * bf16_hi(zw[k]) + Cc[2 * k + 1]);
+            ow[k] = real ? pack2(A[2 * k] * bf16_lo(gw[k]) + Bc[2 * k] * bf16_lo(zw[k]) + Cc[2 * k],
+                                 A[2 * k + 1] * bf16_hi(gw[k]) + Bc[2 * k + 1] * bf16_hi(zw[k]) + Cc[2 * k + 1])
+                         : 0u;
           *reinterpret_cast<uint4*>(gz + im * G::GE + (e1 / C8) * GLD + (e1 % C8) * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         }
       }
@@ -810,10 +816,11 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
     for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o));
     const float lse = m + __logf(se);
     const float lgl = __shfl(lg, lab);
-    if (lane == 0) { a.loss_img[b] = lse - lgl; a.correct_img[b] = am == lab ? 1 : 0; }
+    const bool real = b < a.nvalid;             // batch padding: no loss, accuracy or gradient
+    if (lane == 0) { a.loss_img[b] = real ? lse - lgl : 0.f; a.correct_img[b] = real && am == lab ? 1 : 0; }
     if (lane < 10) {
       if (a.logits_out) a.logits_out[b * 10 + lane] = lg;
-      dlog[lane] = (e / se - (lane == lab ? 1.f : 0.f)) * a.inv_batch;
+      dlog[lane] = real ? (e / se - (lane == lab ? 1.f : 0.f)) * a.inv_batch : 0.f;
     }
   }
   __syncthreads();
@@ -1006,8 +1013,8 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
       __syncthreads();
       if (tid == 0) {
         float* st = a.stats + (size_t)(step % a.stats_len) * 4;
-        st[1] = (lred[0][0] + lred[0][1] + lred[0][2] + lred[0][3]) / (float)a.B;
-        st[2] = (lred[1][0] + lred[1][1] + lred[1][2] + lred[1][3]) / (float)a.B;
+        st[1] = (lred[0][0] + lred[0][1] + lred[0][2] + lred[0][3]) / (float)a.nvalid;
+        st[2] = (lred[1][0] + lred[1][1] + lred[1][2] + lred[1][3]) / (float)a.nvalid;
       }
     }
   }

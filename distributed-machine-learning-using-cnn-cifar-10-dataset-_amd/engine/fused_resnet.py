@@ -95,10 +95,13 @@ class FusedResNetEngine:
         self.ops = ops
         self.device = torch.device(device or "cuda")
         dev = self.device
-        B = int(batch_size)
-        if B < 16 or B % 16 != 0:
-            raise ValueError("fused ResNet engine needs a batch size that is a positive multiple of 16")
-        self.B = B
+        Bv = int(batch_size)
+        if Bv < 1:
+            raise ValueError("batch size must be >= 1")
+        # any batch size: the kernels run on the batch padded to the 16-image tile; the padding images
+        # are excluded from every BatchNorm statistic and get zero loss weight / gradient (nvalid)
+        B = -(-Bv // 16) * 16
+        self.B, self.Bv = B, Bv
         self.world_size, self.rank, self.pg = world_size, rank, process_group
         self.lr0, self.decay, self.decay_steps, self.staircase = lr, lr_decay, decay_steps, staircase
         self.warmup = float(warmup_steps)      # linear LR warm-up, in the SGD kernel
@@ -114,7 +117,7 @@ class FusedResNetEngine:
         self.data = data.to(dev).contiguous()
         self.labels = labels.to(dev, torch.int32).contiguous()
         self.n_data = self.data.shape[0]
-        self.order = OrderSpec(self.n_data, B, world_size, rank, seed)   # generated order (data/order.py)
+        self.order = OrderSpec(self.n_data, Bv, world_size, rank, seed)   # generated order (data/order.py)
         self.period = self.order.period
         self.order_desc = self.order.descriptor()
 
@@ -250,7 +253,7 @@ class FusedResNetEngine:
         for l, (_, ci, co, h, s) in enumerate(LAYERS):
             if l == 0:
                 o.rn_fwd(ci, co, h, s, self.data, idx, counter, period, 0, 0, None, None, None, None, None, 0, None,
-                         self.wf[0], self.z[0], self.stat[0], self._det_stat[0])
+                         self.wf[0], self.z[0], self.stat[0], self._det_stat[0], self.Bv)
                 continue
             p = l - 1
             sc_mode, sc_src = 0, None
@@ -258,20 +261,20 @@ class FusedResNetEngine:
                 sc_mode = _block_sc_mode(p)
                 sc_src = self.a[p - 2]
             o.rn_fwd(ci, co, h, s, None, None, None, 1, 0, 0, self.z[p], self.stat[p], self.gamma[p], self.beta[p],
-                     sc_src, sc_mode, self.a[p], self.wf[l], self.z[l], self.stat[l], self._det_stat[l])
+                     sc_src, sc_mode, self.a[p], self.wf[l], self.z[l], self.stat[l], self._det_stat[l], self.Bv)
         o.rn_head(self.z[18], self.stat[18], self.gamma[18], self.beta[18], self.a[16], self.fcw, self.fcb,
-                  self.labels, idx, counter, period, 1.0 / (self.B * self.world_size), self.gy[18], self.red[18],
-                  self.fc_part, self.loss_img, self.correct_img, logits_out, self._det_red[18])
+                  self.labels, idx, counter, period, 1.0 / (self.Bv * self.world_size), self.gy[18], self.red[18],
+                  self.fc_part, self.loss_img, self.correct_img, logits_out, self._det_red[18], self.Bv)
 
     def _wgrad(self, l):
         _, ci, co, h, s = LAYERS[l]
         if l == 0:
             idx, counter, period = self._stem_src or (self.order_desc, self.step_t, self.period)
             self.ops.rn_wgrad(ci, co, h, s, self.data, idx, counter, period, 0, 0, None, self.gy[0],
-                              self.z[0], self.stat[0], self.red[0], self.gamma[0], self.part[0])
+                              self.z[0], self.stat[0], self.red[0], self.gamma[0], self.part[0], self.Bv)
         else:
             self.ops.rn_wgrad(ci, co, h, s, None, None, None, 1, 0, 0, self.a[l - 1], self.gy[l], self.z[l],
-                              self.stat[l], self.red[l], self.gamma[l], self.part[l])
+                              self.stat[l], self.red[l], self.gamma[l], self.part[l], self.Bv)
 
     def _backward(self):
         o = self.ops
@@ -287,7 +290,7 @@ class FusedResNetEngine:
                     gy_sc = self.gy[l + 1]
                 o.rn_bwd(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
                          self.a[l - 1], self.z[l - 1], self.stat[l - 1], gy_sc, sc_mode, self.gy[l - 1],
-                         self.red[l - 1], self.part[l], self._det_red[l - 1])
+                         self.red[l - 1], self.part[l], self._det_red[l - 1], self.Bv)
                 if self.sgd_split and l in self._sgd_points:
                     # layers >= l: slabs complete, weights no longer read this step
                     self.side_stream.wait_stream(main)
@@ -313,7 +316,7 @@ class FusedResNetEngine:
                 gy_sc = self.gy[l + 1]
             o.rn_dgrad(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
                        self.a[p], self.z[p], self.stat[p], gy_sc, sc_mode, self.gy[p], self.red[p],
-                       self._det_red[p])
+                       self._det_red[p], self.Bv)
         if side is not main:
             main.wait_stream(side)
 
@@ -322,7 +325,7 @@ class FusedResNetEngine:
                         self.mm_off, self.mv_off, self.fcw_off, self.fcb_off, self.part, self.wf, self.wd, self.stat,
                         self.red, self.fc_part, self.loss_img, self.correct_img, self.step_t, self.ticket, self.stats,
                         mode, self.lr0, self.decay, self.decay_steps, self.staircase, R.BN_MOMENTUM, self.warmup,
-                        layers[0], layers[1], tail)
+                        layers[0], layers[1], tail, self.Bv)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -366,7 +369,7 @@ class FusedResNetEngine:
         if self.grad is None:
             self.grad = torch.zeros_like(self.master)
         if idx is not None:
-            ids = idx.to(self.device, torch.int32).contiguous()
+            ids = self._padded(idx)
             self._stem_src = (ids, None, 1)
             try:
                 self._forward(ids, None, 1)
@@ -449,23 +452,31 @@ class FusedResNetEngine:
         """Test accuracy with the BN moving statistics (eval-mode forward of the same weights)."""
         m = self.eval_model()
         n = data.shape[0]
-        nb = math.ceil(n / self.B)
+        nb = math.ceil(n / self.Bv)
         if max_batches:
             nb = min(nb, max_batches)
         correct = total = 0
         for i in range(nb):
-            x = data[i * self.B:(i + 1) * self.B].to(self.device).float()
-            y = labels[i * self.B:(i + 1) * self.B].to(self.device).long()
+            x = data[i * self.Bv:(i + 1) * self.Bv].to(self.device).float()
+            y = labels[i * self.Bv:(i + 1) * self.Bv].to(self.device).long()
             correct += int((m(x).argmax(1) == y).sum())
             total += y.numel()
         return correct / max(1, total)
 
+    def _padded(self, idx: torch.Tensor) -> torch.Tensor:
+        """An explicit list of Bv dataset rows, padded to the kernel batch (last row repeated)."""
+        idx = idx.to(self.device, torch.int32).reshape(-1)
+        assert idx.numel() == self.Bv, (idx.numel(), self.Bv)
+        if self.Bv == self.B:
+            return idx.contiguous()
+        return torch.cat([idx, idx[-1:].expand(self.B - self.Bv)]).contiguous()
+
     @torch.no_grad()
     def forward_logits(self, idx: torch.Tensor) -> torch.Tensor:
-        """Train-mode (batch statistics) logits of dataset rows ``idx`` via the fused kernels — for
-        tests.  Writes activations / statistics but updates nothing."""
-        self._forward(idx.to(self.device, torch.int32).contiguous(), None, 1, logits_out=self.logits_buf)
-        return self.logits_buf.clone()
+        """Train-mode (batch statistics) logits of the Bv dataset rows ``idx`` via the fused kernels —
+        for tests.  Writes activations / statistics but updates nothing."""
+        self._forward(self._padded(idx), None, 1, logits_out=self.logits_buf)
+        return self.logits_buf[:self.Bv].clone()
 
     # --- state ----------------------------------------------------------------------------------
     def read_stats(self, step: int) -> Dict[str, float]:

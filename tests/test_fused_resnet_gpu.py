@@ -264,3 +264,32 @@ def test_branch_sgd_split_equals_single_sgd_launch(monkeypatch):
     assert split.global_step() == one.global_step() == 7
     assert torch.equal(split.master, one.master)
     assert torch.equal(split.state, one.state)
+
+
+@pytest.mark.parametrize("B", [20, 1, 100])
+def test_any_batch_size_masked_tail(B):
+    """Any batch size (BASELINE config 4 at the reference's arbitrary BATCH_SIZE): the kernels run on the
+    batch padded to 16 images; the padding images must not enter any BatchNorm statistic and must get
+    exactly zero gradient.  Checked: g_y of every padding image is exactly 0 at every layer; logits,
+    loss, gradients and the BN running statistics of one step agree with the fp32 eager model at batch B."""
+    data, labels = _data(4 * max(B, 16), seed=31)
+    eng = FusedResNetEngine(B, data, labels, seed=7, lr=0.05)
+    assert eng.Bv == B and eng.B % 16 == 0 and eng.B >= B
+    idx = eng.batch_indices(eng.host_step)
+    assert idx.numel() == B
+    got = eng.forward_logits(idx).cpu()
+    ref_logits, loss, gref, _ = _ref(eng.flat_params(), eng.state.cpu(), data, labels, idx)
+    assert got.shape == (B, 10)
+    assert _rel(got, ref_logits.cpu()) < 5e-2, _rel(got, ref_logits.cpu())
+    grad = eng.compute_gradients().cpu()
+    for l in range(len(eng.gy)):
+        assert int(eng.gy[l][B:].float().abs().sum()) == 0, l
+    cos = float(F.cosine_similarity(grad, gref, dim=0))
+    assert cos > 0.9, cos
+    before, st0 = eng.flat_params().clone(), eng.state.cpu().clone()
+    eng.step()
+    torch.cuda.synchronize()
+    st = eng.read_stats(1)
+    assert abs(st["loss"] - float(loss)) / max(1.0, float(loss)) < 5e-2, (st, float(loss))
+    _, _, _, st_ref = _ref(before, st0, data, labels, idx)
+    assert _rel(eng.state.cpu(), st_ref) < 2e-2
