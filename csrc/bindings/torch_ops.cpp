@@ -263,16 +263,23 @@ void conv1_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tens
   CHECK_HIP(dmlc_conv1_wgrad(&a, stream_of(dp1)));
 }
 
+// conv2 weight-gradient slabs: [g2][1600][64] fp32 or bf16 (the two kernels agree via part2_bf16)
+static int check_part2(const Tensor& part2, int64_t g2) {
+  const bool b = part2.scalar_type() == at::kBFloat16;
+  check(part2, "part2", b ? at::kBFloat16 : at::kFloat, {g2, 1600, 64});
+  return b ? 1 : 0;
+}
+
 void conv2_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2) {
   const int64_t B = p1.size(0), g2 = part2.size(0);
   TORCH_CHECK(g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
   check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+  const int p2b = check_part2(part2, g2);
   check(partb2, "partb2", at::kFloat, {g2, 64});
   c10::DeviceGuard guard(p1.device());
   DmlcConv2WgradArgs a;
-  a.p1 = p1.data_ptr(); a.dy2 = dy2.data_ptr(); a.part2 = part2.data_ptr<float>();
+  a.p1 = p1.data_ptr(); a.dy2 = dy2.data_ptr(); a.part2 = part2.data_ptr(); a.part2_bf16 = p2b;
   a.partb2 = partb2.data_ptr<float>(); a.g2 = (int)g2; a.B = (int)B;
   CHECK_HIP(dmlc_conv2_wgrad(&a, stream_of(p1)));
 }
@@ -295,7 +302,7 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
   }
   check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+  const int p2b = check_part2(part2, g2);
   check(partb2, "partb2", at::kFloat, {g2, 64});
   c10::DeviceGuard guard(dp1.device());
   DmlcWgradArgs a;
@@ -305,7 +312,7 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
   a.w1.dp1 = dp1.data_ptr(); a.w1.am1 = am1.data_ptr<uint8_t>();
   a.w1.part1 = part1.data_ptr<float>(); a.w1.partb1 = partb1.data_ptr<float>(); a.w1.g1 = (int)g1; a.w1.B = (int)B;
   a.w1.xraw = xraw_ptr(xraw, B);
-  a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr<float>();
+  a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr(); a.w2.part2_bf16 = p2b;
   a.w2.partb2 = partb2.data_ptr<float>(); a.w2.g2 = (int)g2; a.w2.B = (int)B;
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
 }
@@ -434,7 +441,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   const int64_t g1 = part1.size(0), g2 = part2.size(0);
   check(part1, "part1", at::kFloat, {g1, 80, 64});
   check(partb1, "partb1", at::kFloat, {g1, 64});
-  check(part2, "part2", at::kFloat, {g2, 1600, 64});
+  const int p2b = check_part2(part2, g2);
   check(partb2, "partb2", at::kFloat, {g2, 64});
   TORCH_CHECK(loss_part.numel() >= 1, "loss partials missing");
   const int64_t B = batch;
@@ -460,7 +467,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   a.mode = (int)mode; a.grad_scale = (float)grad_scale;
   for (int i = 0; i < 10; ++i) a.off[i] = (int)off[i];
   a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1;
-  a.part2 = part2.data_ptr<float>(); a.g2 = (int)g2;
+  a.part2 = part2.data_ptr(); a.part2_bf16 = p2b; a.g2 = (int)g2;
   a.partb2 = partb2.data_ptr<float>(); a.B = (int)B;
   a.w1f = w1f.data_ptr(); a.w2f = w2f.data_ptr(); a.w2d = w2d.data_ptr(); a.fc1n = fc1n.data_ptr();
   a.fc2t = fc2t.data_ptr(); a.fc2n = fc2n.data_ptr(); a.fc3t = fc3t.data_ptr(); a.fc3d = fc3d.data_ptr();

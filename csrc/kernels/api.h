@@ -111,10 +111,11 @@ struct DmlcConv1WgradArgs {
 struct DmlcConv2WgradArgs {
   const void* p1;           // bf16 [B][12][12][64]   (conv2 input)
   const void* dy2;          // bf16 [B][144][64]      (conv2 pre-activation gradient)
-  float* part2;             // [g2][1600][64]
+  void* part2;              // [g2][1600][64] fp32, or bf16 when part2_bf16
   float* partb2;            // [g2][64] conv2 bias-grad partials (written by the c4 == 0 blocks)
   int g2;
   int B;
+  int part2_bf16;           // slabs stored as bf16 (partial sums of g2-th of the batch, rounded once)
 };
 
 // Both weight gradients in one launch (blocks [0,g1): conv1; then 4 * g2 conv2 blocks, one slab per group).
@@ -173,7 +174,8 @@ struct DmlcSgdArgs {
   // flat offsets of the 10 tensors, TF order
   int off[10];
   const float* part1; const float* partb1; int g1;   // conv1 partials [g1][80][64], [g1][64]
-  const float* part2; int g2;                        // conv2 partials [g2][1600][64]
+  const void* part2; int g2;                         // conv2 partials [g2][1600][64] (fp32 or bf16)
+  int part2_bf16;
   const float* partb2; int B;                        // conv2 bias partials [g2][64]
   // bf16 shadows
   void* w1f; void* w2f; void* w2d; void* fc1n; void* fc2t; void* fc2n; void* fc3t; void* fc3d;

@@ -205,7 +205,17 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
     if (b == b0) DMLC_STAMP(DMLC_TK_W2, 4);
   }
   DMLC_STAMP(DMLC_TK_W2, 2);
-  float* out = a.part2 + (size_t)grp * 1600 * 64;
+  // slab element e of this group: fp32, or bf16 (half the bytes the SGD reads back and the kernel
+  // boundary writes back from L2; each element is a partial sum over G-th of the batch, rounded once)
+  const size_t slab0 = (size_t)grp * 1600 * 64;
+  auto put4 = [&](size_t e, const f32x4& v) {
+    if (a.part2_bf16) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.part2) + slab0 + e) = pack4(v[0], v[1], v[2], v[3]);
+    else *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.part2) + slab0 + e) = v;
+  };
+  auto put1 = [&](size_t e, float v) {
+    if (a.part2_bf16) reinterpret_cast<bf16*>(a.part2)[slab0 + e] = (bf16)v;
+    else reinterpret_cast<float*>(a.part2)[slab0 + e] = v;
+  };
   __syncthreads();                             // every MFMA read of LDS is done: reuse it for staging
   if (c4 == 0) {
     float* red = reinterpret_cast<float*>(smem);
@@ -233,13 +243,13 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
     for (int k = 0; k < 4; ++k) {
       const int row = 4 * k + (lane >> 4), c16 = lane & 15;
       const f32x4 v = *reinterpret_cast<const f32x4*>(st + row * W2_ST + 4 * c16);
-      *reinterpret_cast<f32x4*>(out + ((3 * w + j) * 64 + 16 * c4 + row) * 64 + 4 * c16) = v;
+      put4(((size_t)(3 * w + j) * 64 + 16 * c4 + row) * 64 + 4 * c16, v);
     }
     lds_barrier();
   }
   if (w < 4) {                                 // tap 24, co tile w
 #pragma unroll
-    for (int i = 0; i < 4; ++i) out[(24 * 64 + 16 * c4 + 4 * g + i) * 64 + 16 * w + li] = acc[12][i];
+    for (int i = 0; i < 4; ++i) put1((size_t)(24 * 64 + 16 * c4 + 4 * g + i) * 64 + 16 * w + li, acc[12][i]);
   }
   DMLC_STAMP(DMLC_TK_W2, 3);
 }
