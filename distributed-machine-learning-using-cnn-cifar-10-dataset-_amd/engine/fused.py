@@ -1,17 +1,22 @@
 """Fused MI355X training engine for the reference CNN (hand-written HIP kernels + HIP graphs + RCCL).
 
 One training step (= one ``mon_sess.run([train_op, loss])`` of /root/reference/cifar10cnn.py:230,
-SURVEY.md §3.3) is nine kernel launches, all reading their inputs from device memory:
+SURVEY.md §3.3) is seven kernel launches on the bf16 path (B > 128), all reading their inputs
+from device memory:
 
-  1 conv1_fwd    uint8 gather + center crop + conv1 + bias + ReLU + pool1 (+argmax)
-  2 conv2_fwd    conv2 + bias + ReLU + pool2 (+argmax)
-  3 gemm         fc1 forward, split-K fp32 partials
-  4 head         fc1 reduce/bias/ReLU, fc2, fc3, ReLU-logits, softmax-xent, accuracy, dlogits→dh2→dh1
-  5 gemm (x7)    fc1 dgrad + dW1 + dW2 + dW3 + db1 + db2 + db3 in ONE grouped launch
-  6 conv2_dgrad  pool2/ReLU backward (2x2-ownership gather) + conv2 input-gradient
-  7 wgrad        ONE launch, two block roles: pool1/ReLU backward + conv1 weight/bias gradients,
-                 and conv2 weight/bias gradients (8-wave blocks as two 4-wave halves); split-K slabs
-  8 sgd          partial reduction + SGD + LR schedule + bf16 shadow refresh + global_step++ + stats
+  1 conv12_fwd   uint8 gather + center crop + conv1 + bias + ReLU + pool1 (+argmax), handed through
+                 LDS to conv2 + bias + ReLU + pool2 (+argmax) -- one workgroup per image
+  2 gemm         fc1 forward, split-K fp32 partials
+  3 head         fc1 reduce/bias/ReLU, fc2, fc3, ReLU-logits, softmax-xent, accuracy, dlogits→dh2→dh1
+  4 gemm (x7)    fc1 dgrad + dW1 + dW2 + dW3 + db1 + db2 + db3 in ONE grouped launch
+  5 conv2_dgrad  pool2/ReLU backward (2x2-ownership gather) + conv2 input-gradient
+  6 wgrad        ONE launch, two block roles: pool1/ReLU backward + conv1 weight/bias gradients,
+                 and conv2 weight/bias gradients per (input-channel quarter, image group); split-K slabs
+  7 sgd          slab reduction + SGD + LR schedule + bf16 shadow refresh + global_step++ + stats
+
+At B <= 128 (conv_split = 2, cnn_split.hip) launch 1 becomes conv1_fwd_split + conv2_fwd_split and
+launch 5 conv2_dgrad_split (two or four workgroups per image, so a small batch fills the 256 CUs):
+eight launches.  The fp8 path runs conv1 and conv2 forward as two launches.
 
 Every data-consuming kernel computes its batch rows from the device-resident global_step and the
 generated epoch order (data/order.py: a keyed Feistel permutation per epoch, no index buffer), so
