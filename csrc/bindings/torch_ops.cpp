@@ -317,28 +317,42 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
 }
 
-// params per problem (12 ints): M, N, K, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit, relu, nvalid
+// params per problem (14 ints): M, N, K, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit, relu, nvalid,
+// b_par, s_par.  c_mode 0 fp32 C, 1 bf16 C, 2 split-K fp32 slabs, 3 column sums, 4 fused SGD (C = fp32
+// master weights updated in place, bf16 shadow into `shadow` at parity offset s_par; needs `step` and
+// sched = {lr0, decay, decay_steps, staircase, warmup, grad_scale}).  b_par != 0: the B operand of odd
+// steps lives b_par elements further on (double-buffered shadow; needs `step`).
 void gemm_grouped(at::TensorList A, at::TensorList Bm, at::TensorList C, const c10::List<c10::optional<Tensor>>& bias,
-                  at::IntArrayRef params) {
+                  at::IntArrayRef params, const c10::optional<Tensor>& step, const c10::optional<Tensor>& shadow,
+                  at::ArrayRef<double> sched) {
   const int n = (int)A.size();
   TORCH_CHECK(n >= 1 && n <= DMLC_MAX_GEMM, "1..8 problems per group");
   TORCH_CHECK((int)Bm.size() == n && (int)C.size() == n && (int)bias.size() == n, "list lengths differ");
-  TORCH_CHECK((int)params.size() == 12 * n, "params must hold 12 ints per problem");
+  TORCH_CHECK((int)params.size() == 14 * n, "params must hold 14 ints per problem");
   DmlcGemmGroup G;
   memset(&G, 0, sizeof(G));
   G.nprob = n;
+  if (step.has_value()) {
+    check_numel(*step, "step", at::kLong, 1);
+    G.step = step->data_ptr<int64_t>();
+  }
   for (int i = 0; i < n; ++i) {
-    const int64_t* q = params.data() + 12 * i;
+    const int64_t* q = params.data() + 14 * i;
     DmlcGemmProblem& P = G.p[i];
     P.M = (int)q[0]; P.N = (int)q[1]; P.K = (int)q[2];
     P.lda = (int)q[3]; P.a_kmajor = (int)q[4]; P.ldb = (int)q[5]; P.b_kmajor = (int)q[6];
     P.ldc = (int)q[7]; P.c_mode = (int)q[8]; P.ksplit = (int)q[9]; P.relu = (int)q[10]; P.nvalid = (int)q[11];
+    P.b_par = q[12]; P.s_par = q[13];
+    TORCH_CHECK(P.c_mode >= 0 && P.c_mode <= 4, "gemm ", i, ": c_mode must be 0..4");
+    TORCH_CHECK(P.b_par >= 0 && P.s_par >= 0, "gemm ", i, ": negative parity offset");
+    TORCH_CHECK(P.b_par == 0 || G.step, "gemm ", i, ": a parity-buffered B needs the step counter");
     TORCH_CHECK(P.M > 0 && P.K > 0 && P.M % 8 == 0 && P.K % 8 == 0, "gemm ", i, ": M,K must be positive multiples of 8");
     TORCH_CHECK(P.lda % 8 == 0, "gemm ", i, ": lda must be a multiple of 8 (16-byte rows)");
     check_min(A[i], "A", at::kBFloat16, P.a_kmajor ? (int64_t)(P.M - 1) * P.lda + P.K : (int64_t)(P.K - 1) * P.lda + P.M);
     TORCH_CHECK(P.a_kmajor ? P.lda >= P.K : P.lda >= P.M, "gemm ", i, ": lda too small");
     if (P.c_mode == 3) {
       TORCH_CHECK(P.a_kmajor == 0, "gemm ", i, ": column sums need an m-major A");
+      TORCH_CHECK(P.b_par == 0, "gemm ", i, ": column sums read no B");
       check_min(C[i], "C", at::kFloat, std::min(P.M, P.nvalid));
       P.ksplit = 1;
       continue;
@@ -346,11 +360,24 @@ void gemm_grouped(at::TensorList A, at::TensorList Bm, at::TensorList C, const c
     TORCH_CHECK(P.N > 0 && P.N % 8 == 0, "gemm ", i, ": N must be a positive multiple of 8");
     TORCH_CHECK(P.ldb % 8 == 0, "gemm ", i, ": ldb must be a multiple of 8");
     TORCH_CHECK(P.b_kmajor ? P.ldb >= P.K : P.ldb >= P.N, "gemm ", i, ": ldb too small");
-    check_min(Bm[i], "B", at::kBFloat16, P.b_kmajor ? (int64_t)(P.N - 1) * P.ldb + P.K : (int64_t)(P.K - 1) * P.ldb + P.N);
+    check_min(Bm[i], "B", at::kBFloat16,
+              P.b_par + (P.b_kmajor ? (int64_t)(P.N - 1) * P.ldb + P.K : (int64_t)(P.K - 1) * P.ldb + P.N));
     TORCH_CHECK(P.ksplit >= 1 && (P.ksplit == 1 || P.c_mode == 2), "gemm ", i, ": split-K needs c_mode 2");
     TORCH_CHECK(P.nvalid >= 1 && P.nvalid <= P.N && P.ldc >= P.nvalid, "gemm ", i, ": bad nvalid/ldc");
     const int64_t cneed = (int64_t)(P.c_mode == 2 ? P.ksplit : 1) * P.M * P.ldc;
     check_min(C[i], "C", P.c_mode == 1 ? at::kBFloat16 : at::kFloat, cneed);
+    P.S = nullptr;
+    if (P.c_mode == 4) {
+      TORCH_CHECK(G.step && shadow.has_value() && sched.size() == 6, "gemm ", i,
+                  ": the fused SGD epilogue needs step, shadow and sched = {lr0, decay, decay_steps, staircase, warmup, grad_scale}");
+      TORCH_CHECK(P.ksplit == 1 && P.nvalid == P.N && P.N % 4 == 0 && P.ldc % 4 == 0 && !P.bias && !P.relu,
+                  "gemm ", i, ": the fused SGD epilogue needs ksplit 1, full 16-B rows, no bias / ReLU");
+      TORCH_CHECK(!bias.get(i).has_value(), "gemm ", i, ": the fused SGD epilogue takes no bias");
+      check_min(*shadow, "shadow", at::kBFloat16, P.s_par + (int64_t)P.M * P.ldc);
+      P.S = shadow->data_ptr();
+      G.lr0 = (float)sched[0]; G.decay = (float)sched[1]; G.decay_steps = (float)sched[2];
+      G.staircase = sched[3] != 0.0; G.warmup = (float)sched[4]; G.grad_scale = (float)sched[5];
+    }
     P.A = A[i].data_ptr(); P.B = Bm[i].data_ptr(); P.C = C[i].data_ptr();
     P.bias = nullptr;
     const c10::optional<Tensor> bo = bias.get(i);
@@ -426,7 +453,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
          bool staircase, const Tensor& ticket, const Tensor& loss_part, const Tensor& correct_part,
          const Tensor& stats, const c10::optional<Tensor>& w2f8, const c10::optional<Tensor>& amax_w,
          const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize, int64_t batch,
-         const c10::optional<Tensor>& bidx, const c10::optional<Tensor>& order, double warmup) {
+         const c10::optional<Tensor>& bidx, const c10::optional<Tensor>& order, double warmup, bool fc1_fused) {
   TORCH_CHECK(roles >= 0 && roles <= 2, "sgd roles must be 0..2");
   TORCH_CHECK(warmup >= 0.0, "sgd: warmup must be >= 0");
   TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
@@ -449,7 +476,8 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   check(w1f, "w1f", at::kBFloat16, {64, 160});
   check(w2f, "w2f", at::kBFloat16, {64, 1600});
   check(w2d, "w2d", at::kBFloat16, {64, 1600});
-  check(fc1n, "fc1n", at::kBFloat16, {2304, 384});
+  check(fc1n, "fc1n", at::kBFloat16, {2, 2304, 384});          // step-parity double buffer
+  TORCH_CHECK(!fc1_fused || mode == 0, "sgd: fc1_fused only in mode 0 (single GPU)");
   check(fc2t, "fc2t", at::kBFloat16, {192, 384});
   check(fc2n, "fc2n", at::kBFloat16, {384, 192});
   check(fc3t, "fc3t", at::kBFloat16, {16, 192});
@@ -472,7 +500,7 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   a.w1f = w1f.data_ptr(); a.w2f = w2f.data_ptr(); a.w2d = w2d.data_ptr(); a.fc1n = fc1n.data_ptr();
   a.fc2t = fc2t.data_ptr(); a.fc2n = fc2n.data_ptr(); a.fc3t = fc3t.data_ptr(); a.fc3d = fc3d.data_ptr();
   a.step = step.data_ptr<int64_t>(); a.lr0 = (float)lr0; a.decay = (float)decay;
-  a.decay_steps = (float)decay_steps; a.staircase = staircase; a.warmup = (float)warmup;
+  a.decay_steps = (float)decay_steps; a.staircase = staircase; a.warmup = (float)warmup; a.fc1_fused = fc1_fused ? 1 : 0;
   a.ticket = reinterpret_cast<unsigned int*>(ticket.data_ptr<int>());
   a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
   a.nhead = (int)loss_part.numel();
@@ -533,7 +561,8 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor(a!) part1, Tensor(b!) partb1, Tensor p1, Tensor dy2, Tensor(c!) part2, Tensor(d!) partb2, "
         "int groups2, Tensor? xraw=None, bool with_conv1=True) -> ()");
-  m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params) -> ()");
+  m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params, Tensor? step=None, "
+        "Tensor(b!)? shadow=None, float[] sched=[]) -> ()");
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
         "Tensor(a!) h1, Tensor(b!) h2, Tensor(c!) dl, Tensor(d!) dh1, Tensor(e!) dh2, Tensor(f!) loss_part, "
@@ -543,7 +572,8 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
-        "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0) -> ()");
+        "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
+        "bool fc1_fused=False) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

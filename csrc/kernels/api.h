@@ -137,6 +137,11 @@ struct DmlcGemmProblem {
   int ksplit;
   const float* bias; int relu;
   int nvalid;               // store only columns n < nvalid
+  // step-parity double buffers (G.step): b_par != 0 -> the B operand is B + b_par elements on odd
+  // steps; c_mode 4 (fused SGD, fp32 C = the master weights): w -= lr(step) * grad_scale * acc, and
+  // the bf16 shadow of the NEXT step goes to S + (step+1 odd ? s_par : 0) at the same [m][ldc] offsets
+  long long b_par, s_par;
+  void* S;
   int tiles_m, tiles_n, block_start;   // filled by dmlc_gemm_grouped
 };
 #define DMLC_MAX_GEMM 8
@@ -144,6 +149,10 @@ struct DmlcGemmGroup {
   DmlcGemmProblem p[DMLC_MAX_GEMM];
   int nprob;
   int nblocks;
+  // device step counter (nullable: parity 0) and the SGD schedule for c_mode 4 (same as DmlcSgdArgs)
+  const int64_t* step;
+  float lr0, decay, decay_steps, warmup, grad_scale;
+  int staircase;
 };
 
 // MLP head, rows-parallel (rows = 2 or 4 per workgroup; B / rows workgroups): fc1 split-K reduce + bias + ReLU, fc2, fc3,
@@ -203,6 +212,10 @@ struct DmlcSgdArgs {
   // evaluating the Feistel order themselves (~150 scalar instructions per row per wave).
   int* bidx; int bidx_n;
   DmlcIndexSrc next;
+  // fc1n is [2][2304][384] (step-parity double buffer: kernels of step s read fc1n[s & 1]); modes
+  // 0/2 write fc1n[(s+1) & 1], mode 3 fc1n[s & 1].  fc1_fused (mode 0): the fc1 WEIGHT update already
+  // ran in the dW1 GEMM's epilogue (c_mode 4) -- the fc1 role covers the fc1 bias only
+  int fc1_fused;
 };
 
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);

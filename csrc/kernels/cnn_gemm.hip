@@ -107,8 +107,10 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
   const int ksteps = (P.K + 31) >> 5;
   const int per = (ksteps + P.ksplit - 1) / P.ksplit;
   const int kbeg = split * per * 32, kend = min(P.K, (split * per + per) * 32);
+  // step parity (double-buffered bf16 weight shadows, fused SGD epilogue): one scalar load
+  const int64_t st = ((P.b_par != 0 || P.c_mode == 4) && G.step) ? *G.step : 0;
   const bf16* A = reinterpret_cast<const bf16*>(P.A);
-  const bf16* B = reinterpret_cast<const bf16*>(P.B);
+  const bf16* B = reinterpret_cast<const bf16*>(P.B) + ((st & 1) ? P.b_par : 0);
   const int wm = w >> 1, wn = w & 1;
 
   f32x4 acc[2][2];
@@ -160,6 +162,36 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
       for (int r = 0; r < 4; ++r) ct[(32 * wm + 16 * i + 4 * g + r) * CT_LD + 32 * wn + 16 * j + li] = acc[i][j][r];
   __syncthreads();
   const bool vec = (P.ldc & 3) == 0;
+  if (P.c_mode == 4) {
+    // fused SGD (single GPU): acc is the complete weight gradient of this tile (K = the whole batch,
+    // no split); master update + the next step's bf16 shadow, both 16-B row vectors (ldc % 4 == 0,
+    // nvalid == N, checked by the binding)
+    const float f = lr_sched(G.lr0, G.decay, G.decay_steps, G.staircase, G.warmup, st) * G.grad_scale;
+    bf16* S = reinterpret_cast<bf16*>(P.S) + (((st + 1) & 1) ? P.s_par : 0);
+    float4 wv[4];
+    int ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {                   // master loads first: one latency for all four
+      const int e = tid + u * 256, rr = e >> 4, cc = (e & 15) * 4;
+      const int m = m0 + rr, n = n0 + cc;
+      ok[u] = m < P.M && n < P.nvalid;
+      const size_t q = ok[u] ? (size_t)m * P.ldc + n : 0;
+      wv[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.C) + q);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!ok[u]) continue;
+      const int e = tid + u * 256, rr = e >> 4, cc = (e & 15) * 4;
+      const size_t q = (size_t)(m0 + rr) * P.ldc + n0 + cc;
+      const float4 g = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
+      float4 v = wv[u];
+      v.x -= f * g.x; v.y -= f * g.y; v.z -= f * g.z; v.w -= f * g.w;
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(P.C) + q) = v;
+      *reinterpret_cast<bf16x4*>(S + q) = pack4(v.x, v.y, v.z, v.w);
+    }
+    DMLC_STAMP(DMLC_TK_GEMM, 2);
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int e = tid + u * 256, rr = e >> 4, cc = (e & 15) * 4;

@@ -37,16 +37,15 @@ constexpr int FC2_BLOCKS = (384 / FC2_ROWS) * (192 / FC2_COLS);   // 24
 constexpr int FC_TAIL = 192 + 1920 + 10;                      // fc2 bias, fc3 weight + bias
 constexpr int FC_TAIL_BLOCKS = (FC_TAIL + 255) / 256;         // one element per thread
 
-// fc1 weight + bias (contiguous float4 range, same-layout shadow): blocks of 1024 float4
+// fc1 weight + bias (contiguous float4 range, same-layout shadow): blocks of 1024 float4; with
+// fc1_fused only the bias (the weights were updated by the dW1 GEMM epilogue)
+__host__ __device__ inline int fc1_first(const DmlcSgdArgs& a) { return a.fc1_fused ? a.off[5] : a.off[4]; }
 __host__ __device__ inline int fc1_blocks(const DmlcSgdArgs& a) {
-  return ((a.off[6] - a.off[4]) / 4 + 256 * FC_F4_PER_THREAD - 1) / (256 * FC_F4_PER_THREAD);
+  return ((a.off[6] - fc1_first(a)) / 4 + 256 * FC_F4_PER_THREAD - 1) / (256 * FC_F4_PER_THREAD);
 }
 
-// staircase (or constant) decay, times a linear warm-up ramp (step + 1) / warmup over the first
-// `warmup` steps (large-batch recipe, BASELINE config 5)
 DEV float lr_of(const DmlcSgdArgs& a, int64_t step) {
-  const float lr = a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
-  return a.warmup > 0.f && (float)step < a.warmup ? lr * ((float)step + 1.f) / a.warmup : lr;
+  return lr_sched(a.lr0, a.decay, a.decay_steps, a.staircase, a.warmup, step);
 }
 
 DEV float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
@@ -213,8 +212,10 @@ DEV void conv_bias(const DmlcSgdArgs& a, int which, float lr, float4* lds) {
   sgd4(a.master + a.off[seg] + c, w0, g, lr, a.grad_scale, a.mode != 3);
 }
 
-DEV void fc1_block(const DmlcSgdArgs& a, int blk, float lr) {
-  const int base4 = a.off[4] >> 2, end4 = a.off[6] >> 2;
+DEV void fc1_block(const DmlcSgdArgs& a, int blk, float lr, int64_t step) {
+  const int base4 = fc1_first(a) >> 2, end4 = a.off[6] >> 2;
+  // the shadow the NEXT step's kernels read (mode 3: this step's)
+  bf16* shadow = reinterpret_cast<bf16*>(a.fc1n) + ((((a.mode == 3 ? step : step + 1) & 1) != 0) ? 884736 : 0);
   const bool apply = a.mode != 3;
   const float f = lr * a.grad_scale;
   int i4[FC_F4_PER_THREAD];
@@ -236,7 +237,7 @@ DEV void fc1_block(const DmlcSgdArgs& a, int blk, float lr) {
       reinterpret_cast<float4*>(a.master)[i4[u]] = v;
     }
     if (i < a.off[5])                                 // fc1 weight [2304][384]: same layout shadow
-      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.fc1n) + (i - a.off[4])) = pack4(v.x, v.y, v.z, v.w);
+      *reinterpret_cast<bf16x4*>(shadow + (i - a.off[4])) = pack4(v.x, v.y, v.z, v.w);
   }
 }
 
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
   if (blk < C1_BLOCKS) conv1_rows(a, blk, lr, lds);
   else if ((blk -= C1_BLOCKS) < 2) conv_bias(a, blk, lr, lds);
   else if ((blk -= 2) < C2_BLOCKS) conv2_rows(a, blk, lr, lds);
-  else if ((blk -= C2_BLOCKS) < nfc1) fc1_block(a, blk, lr);
+  else if ((blk -= C2_BLOCKS) < nfc1) fc1_block(a, blk, lr, step);
   else if ((blk -= nfc1) < FC2_BLOCKS) fc2_block(a, blk, lr, reinterpret_cast<bf16*>(lds));
   else fc_tail_block(a, blk - FC2_BLOCKS, lr);
   DMLC_STAMP(DMLC_TK_SGD, 1);

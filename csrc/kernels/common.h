@@ -82,6 +82,14 @@ DEV uint32_t pk_fp8x4(float a, float b, float c, float d) {
   return (uint32_t)w;
 }
 
+// staircase (or constant) decay, times a linear warm-up ramp (step + 1) / warmup over the first
+// `warmup` steps (large-batch recipe, BASELINE config 5).  The SGD kernel and the fused-SGD GEMM
+// epilogue evaluate the SAME expression, so both see bit-identical rates.
+DEV float lr_sched(float lr0, float decay, float decay_steps, int staircase, float warmup, int64_t step) {
+  const float lr = staircase ? lr0 * powf(decay, floorf((float)step / decay_steps)) : lr0;
+  return warmup > 0.f && (float)step < warmup ? lr * ((float)step + 1.f) / warmup : lr;
+}
+
 DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -65,8 +65,13 @@ TICKET_WORDS = 9 * 32
 SEG = {M.short(s.name): s for s in M.PARAM_SPECS}
 
 
-def _gemm_params(M_, N_, K_, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit=1, relu=0, nvalid=None):
-    return [M_, N_, K_, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit, relu, N_ if nvalid is None else nvalid]
+def _gemm_params(M_, N_, K_, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit=1, relu=0, nvalid=None, b_par=0,
+                 s_par=0):
+    return [M_, N_, K_, lda, a_kmajor, ldb, b_kmajor, ldc, c_mode, ksplit, relu, N_ if nvalid is None else nvalid,
+            b_par, s_par]
+
+
+FC1_NUMEL = 2304 * 384
 
 
 class FusedCifarEngine:
@@ -150,7 +155,11 @@ class FusedCifarEngine:
         bf = torch.bfloat16
         z = lambda *s, dt=bf: torch.zeros(*s, dtype=dt, device=dev)
         self.w1f, self.w2f, self.w2d = z(64, 160), z(64, 1600), z(64, 1600)
-        self.fc1n, self.fc2t, self.fc2n = z(2304, 384), z(192, 384), z(384, 192)
+        # fc1's bf16 shadow is double-buffered by step parity ([2][2304][384]): the kernels of step s
+        # read fc1n[s & 1] and the update writes fc1n[(s + 1) & 1], so at N=1 the dW1 GEMM can apply
+        # the fc1 update in its epilogue while the dp2 problem of the same launch still reads the
+        # current weights (fc1_epilogue below)
+        self.fc1n, self.fc2t, self.fc2n = z(2, 2304, 384), z(192, 384), z(384, 192)
         self.fc3t, self.fc3d = z(16, 192), z(192, 32)
         # fp8 conv2 forward + input gradient (BASELINE config 5): e4m3 weight shadows [0] forward
         # (co-major) and [1] the dgrad's flipped ci-major copy, delayed per-tensor weight scale;
@@ -253,14 +262,15 @@ class FusedCifarEngine:
 
         # grouped GEMM problem lists
         self._fc1_fwd = dict(A=[self.p2.view(B, 2304)], B=[self.fc1n], C=[self.h1part], bias=[None],
-                             params=_gemm_params(B, 384, 2304, 2304, 1, 384, 0, 384, 2, self.fc1_split))
+                             params=_gemm_params(B, 384, 2304, 2304, 1, 384, 0, 384, 2, self.fc1_split,
+                                                 b_par=FC1_NUMEL))
         self._fc_bwd = dict(
             A=[self.dh1, self.p2.view(B, 2304), self.h1, self.h2, self.dh1, self.dh2, self.dl],
             B=[self.fc1n, self.dh1, self.dh2, self.dl, self.dh1, self.dh2, self.dl],
             C=[self.dp2.view(B, 2304), gv["full_weight_1"], gv["full_weight_2"], gv["full_weight_3"],
                gv["full_bias_1"], gv["full_bias_2"], gv["full_bias_3"]],
             bias=[None] * 7,
-            params=(_gemm_params(B, 2304, 384, 384, 1, 384, 1, 2304, 1)            # dp2 = dh1 W1^T
+            params=(_gemm_params(B, 2304, 384, 384, 1, 384, 1, 2304, 1, b_par=FC1_NUMEL)  # dp2 = dh1 W1^T
                     + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 0)          # dW1 = p2^T dh1
                     + _gemm_params(384, 192, B, 384, 0, 192, 0, 192, 0)            # dW2 = h1^T dh2
                     + _gemm_params(192, 16, B, 192, 0, 16, 0, 10, 0, nvalid=10)    # dW3 = h2^T dl
@@ -270,9 +280,19 @@ class FusedCifarEngine:
         # the same problems as two launches: dp2 (conv backward path) | the fc weight / bias gradients
         fb = self._fc_bwd
         self._fc_dx = {k: fb[k][:1] for k in ("A", "B", "C", "bias")}
-        self._fc_dx["params"] = fb["params"][:12]
+        self._fc_dx["params"] = fb["params"][:14]
         self._fc_dw = {k: fb[k][1:] for k in ("A", "B", "C", "bias")}
-        self._fc_dw["params"] = fb["params"][12:]
+        self._fc_dw["params"] = fb["params"][14:]
+        # single GPU: the same launch with dW1 as a fused SGD epilogue (c_mode 4) -- the fc1 weights
+        # (83 % of the parameters) are updated where their gradient is produced instead of the fp32
+        # gradient going through HBM to the SGD kernel (which then updates the fc1 bias only).
+        # Bitwise the same update (same lr expression, same fp32 arithmetic); DMLC_FC1_EPILOGUE=0 off
+        self.fc1_epilogue = (not self.dp and not self.fc_branch
+                             and os.environ.get("DMLC_FC1_EPILOGUE", "1") != "0")
+        self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
+                                params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
+                                                                        s_par=FC1_NUMEL)
+                                + fb["params"][28:])
 
         self.graphs: List[torch.cuda.CUDAGraph] = []
         self.chains: Dict[int, Optional[torch.cuda.CUDAGraph]] = {}   # k -> graph of k chained steps
@@ -314,6 +334,9 @@ class FusedCifarEngine:
         self._sgd(mode=3)
 
     def set_step(self, step: int):
+        old = int(self.step_t.item())
+        if (old ^ int(step)) & 1:      # the current fc1 shadow moves to the new step's parity slot
+            self.fc1n[int(step) & 1].copy_(self.fc1n[old & 1])
         self.step_t.fill_(int(step))
         self.host_step = int(step)
         self._sync_bidx()
@@ -356,16 +379,21 @@ class FusedCifarEngine:
             o.conv2_fwd_fp8(self.p1, self.w2f8[0], p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
         elif not self.fused_fwd and self.conv_split == 1:
             o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
-        f = self._fc1_fwd
-        o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
+        self._gemm(self._fc1_fwd)
         o.head(self.h1part, p["full_bias_1"], self.fc2t, p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d,
                self.fc2n, self.labels, idx, counter, period, 1.0 / (self.Bv * self.world_size), self.relu_logits,
                train, self.h1, self.h2, self.dl, self.dh1, self.dh2, self.loss_part, self.correct_part, logits_out,
                self.Bv)
 
-    def _fc_backward(self):
-        f = self._fc_bwd
-        self.ops.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
+    def _gemm(self, f, sgd: bool = False):
+        if sgd:
+            sched = [self.lr0, self.decay, self.decay_steps, 1.0 if self.staircase else 0.0, self.warmup, 1.0]
+            self.ops.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"], self.step_t, self.fc1n, sched)
+        else:
+            self.ops.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"], self.step_t)
+
+    def _fc_backward(self, fused_sgd: bool = False):
+        self._gemm(self._fc_bwd_sgd if fused_sgd else self._fc_bwd, sgd=fused_sgd)
 
     def _conv_backward(self, src=None):
         o = self.ops
@@ -397,13 +425,13 @@ class FusedCifarEngine:
                       self.part1, self.partb1, self.xraw)
         main.wait_stream(self.side_stream)
 
-    def _sgd(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True):
+    def _sgd(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True, fc1_fused: bool = False):
         self.ops.sgd(self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.partb2,
                      self.w1f, self.w2f, self.w2d, self.fc1n, self.fc2t, self.fc2n, self.fc3t, self.fc3d,
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                      self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
                                                                       if self.fp8 else (None, None, None)),
-                     roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup)
+                     roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup, fc1_fused)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -476,6 +504,12 @@ class FusedCifarEngine:
             if self.fc_branch:
                 self._branched_step()
                 return
+            if self.fc1_epilogue:
+                self._forward(self.bidx, None, 1, train=True)
+                self._fc_backward(fused_sgd=True)
+                self._conv_backward()
+                self._sgd(mode=0, fc1_fused=True)
+                return
             self._seg_compute_a()
             self._seg_compute_b()
             return
@@ -489,13 +523,11 @@ class FusedCifarEngine:
         run beside the conv backward; the conv SGD (which bumps global_step) after the join."""
         o = self.ops
         self._forward(self.bidx, None, 1, train=True)
-        f = self._fc_dx
-        o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
+        self._gemm(self._fc_dx)
         main = torch.cuda.current_stream(self.device)
         self.side_stream.wait_stream(main)
         with torch.cuda.stream(self.side_stream):
-            f = self._fc_dw
-            o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"])
+            self._gemm(self._fc_dw)
             self._sgd(mode=0, roles=2, finalize=False)
         self._conv_backward()
         main.wait_stream(self.side_stream)
@@ -712,6 +744,10 @@ class FusedCifarEngine:
 
     def global_step(self) -> int:
         return int(self.step_t.item())
+
+    def fc1n_current(self) -> torch.Tensor:
+        """The bf16 fc1 weight shadow the kernels of the current step read ([2304][384])."""
+        return self.fc1n[self.global_step() & 1]
 
     def flat_params(self) -> torch.Tensor:
         return self.master.detach().cpu()

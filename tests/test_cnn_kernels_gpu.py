@@ -123,7 +123,7 @@ def cnn_local_errors(eng, data, labels, idx):
     out["sgd_master"] = _rel(eng.master, want)
     nb = {k: v.to(torch.bfloat16) for k, v in new.items()}
     out["sgd_shadows"] = max(
-        _rel(eng.fc1n, nb["full_weight_1"]), _rel(eng.fc2n, nb["full_weight_2"]),
+        _rel(eng.fc1n_current(), nb["full_weight_1"]), _rel(eng.fc2n, nb["full_weight_2"]),
         _rel(eng.fc2t, nb["full_weight_2"].t()), _rel(eng.fc3t[:10], nb["full_weight_3"].t()),
         _rel(eng.w2f.view(64, 25, 64), nb["conv2_kernel"].reshape(25, 64, 64).permute(2, 0, 1)))
     return out

@@ -323,3 +323,34 @@ def test_fc_branch_step_is_bit_identical(B, monkeypatch):
     assert torch.isfinite(ref.master).all()
     assert torch.equal(ref.master, br.master)
     assert ref.read_stats(8) == br.read_stats(8)
+
+
+@pytest.mark.parametrize("B", [100, 256])
+def test_fc1_update_in_gemm_epilogue_is_bit_identical(B, monkeypatch):
+    """Single GPU: the fc1 weight update runs in the dW1 GEMM's epilogue (c_mode 4) and the SGD kernel
+    updates only the fc1 bias; the fc1 shadow is double-buffered by step parity.  After eager and
+    graph-replayed steps (odd and even counts, a mid-run set_step, an eval forward) everything equals
+    the plain path (fp32 gradient through HBM, fc1 in the SGD kernel) bit for bit."""
+    data, labels = _synthetic(8 * B, seed=43)
+    kw = dict(seed=44, lr=1e-4, relu_logits=False)
+    fused = FusedCifarEngine(B, data, labels, **kw)
+    monkeypatch.setenv("DMLC_FC1_EPILOGUE", "0")
+    ref = FusedCifarEngine(B, data, labels, **kw)
+    assert fused.fc1_epilogue and not ref.fc1_epilogue
+    idx = torch.arange(B, dtype=torch.int32)
+    for eng in (ref, fused):
+        eng.step()
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(5)
+        eng.set_step(eng.global_step() + 1)     # parity flip from the host
+        eng.run(3)
+    torch.cuda.synchronize()
+    assert ref.global_step() == fused.global_step() == 11
+    assert torch.isfinite(ref.master).all()
+    assert torch.equal(ref.master, fused.master)
+    assert torch.equal(ref.fc1n_current(), fused.fc1n_current())
+    w1 = ref.pv["full_weight_1"].view(2304, 384)
+    assert torch.equal(fused.fc1n_current(), w1.to(torch.bfloat16))
+    assert ref.read_stats(11) == fused.read_stats(11)
+    assert torch.equal(ref.forward_logits(idx), fused.forward_logits(idx))

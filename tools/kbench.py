@@ -63,7 +63,7 @@ def main():
                                                     eng.w1f, p["conv1_bias"], eng.p1, eng.am1, eng.w2f,
                                                     p["conv2_bias"], eng.p2, eng.am2, eng.xraw), a.iters)
     f = eng._fc1_fwd
-    res["fc1_fwd_gemm"] = timeit(lambda: o.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"]), a.iters)
+    res["fc1_fwd_gemm"] = timeit(lambda: eng._gemm(f), a.iters)
     B = eng.B
     res["head"] = timeit(lambda: o.head(eng.h1part, p["full_bias_1"], eng.fc2t, p["full_bias_2"], eng.fc3t,
                                         p["full_bias_3"], eng.fc3d, eng.fc2n, eng.labels, eng.bidx, None,
