@@ -398,7 +398,7 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
           const c10::optional<Tensor>& counter, int64_t period, double inv_batch, bool relu_logits, bool train,
           const Tensor& h1, const Tensor& h2, const Tensor& dl, const Tensor& dh1, const Tensor& dh2,
           const Tensor& loss_part, const Tensor& correct_part, const c10::optional<Tensor>& logits_out,
-          int64_t nvalid) {
+          int64_t nvalid, const c10::optional<Tensor>& step, const c10::optional<Tensor>& step_copy) {
   TORCH_CHECK(h1part.dim() == 3 && h1part.size(2) == 384, "h1part must be [nsplit,B,384]");
   const int64_t nsplit = h1part.size(0), B = h1part.size(1);
   TORCH_CHECK(B % 16 == 0 && B > 0, "head: batch must be a positive multiple of 16");
@@ -443,6 +443,13 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
     check(*logits_out, "logits_out", at::kFloat, {B, 10});
     a.logits_out = logits_out->data_ptr<float>();
   }
+  a.step = nullptr; a.step_copy = nullptr;
+  TORCH_CHECK(step.has_value() == step_copy.has_value(), "head: step and step_copy go together");
+  if (step.has_value()) {
+    check_numel(*step, "step", at::kLong, 1);
+    check_numel(*step_copy, "step_copy", at::kLong, 1);
+    a.step = step->data_ptr<int64_t>(); a.step_copy = step_copy->data_ptr<int64_t>();
+  }
   CHECK_HIP(dmlc_head(&a, stream_of(h1part)));
 }
 
@@ -453,7 +460,8 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
          bool staircase, const Tensor& ticket, const Tensor& loss_part, const Tensor& correct_part,
          const Tensor& stats, const c10::optional<Tensor>& w2f8, const c10::optional<Tensor>& amax_w,
          const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize, int64_t batch,
-         const c10::optional<Tensor>& bidx, const c10::optional<Tensor>& order, double warmup, bool fc1_fused) {
+         const c10::optional<Tensor>& bidx, const c10::optional<Tensor>& order, double warmup, bool fc1_fused,
+         const c10::optional<Tensor>& step_rd) {
   TORCH_CHECK(roles >= 0 && roles <= 2, "sgd roles must be 0..2");
   TORCH_CHECK(warmup >= 0.0, "sgd: warmup must be >= 0");
   TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
@@ -499,7 +507,12 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
   a.partb2 = partb2.data_ptr<float>(); a.B = (int)B;
   a.w1f = w1f.data_ptr(); a.w2f = w2f.data_ptr(); a.w2d = w2d.data_ptr(); a.fc1n = fc1n.data_ptr();
   a.fc2t = fc2t.data_ptr(); a.fc2n = fc2n.data_ptr(); a.fc3t = fc3t.data_ptr(); a.fc3d = fc3d.data_ptr();
-  a.step = step.data_ptr<int64_t>(); a.lr0 = (float)lr0; a.decay = (float)decay;
+  a.step = step.data_ptr<int64_t>(); a.lr0 = (float)lr0;
+  a.step_rd = a.step;
+  if (step_rd.has_value()) {
+    check_numel(*step_rd, "step_rd", at::kLong, 1);
+    a.step_rd = step_rd->data_ptr<int64_t>();
+  } a.decay = (float)decay;
   a.decay_steps = (float)decay_steps; a.staircase = staircase; a.warmup = (float)warmup; a.fc1_fused = fc1_fused ? 1 : 0;
   a.ticket = reinterpret_cast<unsigned int*>(ticket.data_ptr<int>());
   a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
@@ -566,14 +579,14 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
         "Tensor(a!) h1, Tensor(b!) h2, Tensor(c!) dl, Tensor(d!) dh1, Tensor(e!) dh2, Tensor(f!) loss_part, "
-        "Tensor(g!) correct_part, Tensor(h!)? logits_out, int nvalid=-1) -> ()");
+        "Tensor(g!) correct_part, Tensor(h!)? logits_out, int nvalid=-1, Tensor? step=None, Tensor(i!)? step_copy=None) -> ()");
   m.def("sgd(Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor part1, Tensor partb1, "
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
         "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
-        "bool fc1_fused=False) -> ()");
+        "bool fc1_fused=False, Tensor? step_rd=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

@@ -171,6 +171,9 @@ struct DmlcHeadArgs {
   void* h1; void* h2; void* dl; void* dh1; void* dh2;   // bf16 [B][384],[B][192],[B][16],[B][384],[B][192]
   float* loss_part; int* correct_part;                  // [B/rows]
   float* logits_out;                                    // optional fp32 [B][10]
+  // optional: workgroup 0 copies *step to *step_copy -- the value the step's SGD launch reads, so
+  // the SGD can bump *step from any one block without an arrival ticket (no SGD block reads *step)
+  const int64_t* step; int64_t* step_copy;
 };
 
 // Fused SGD over the flat fp32 parameter buffer (+ split-K partial reduction, LR schedule from the
@@ -190,6 +193,9 @@ struct DmlcSgdArgs {
   void* w1f; void* w2f; void* w2d; void* fc1n; void* fc2t; void* fc2n; void* fc3t; void* fc3d;
   // schedule
   int64_t* step; float lr0; float decay; float decay_steps; int staircase;
+  // the step this launch reads (LR, parity slots, stats): == step (then the last arriver of a ticket
+  // bumps it), or the copy the head kernel made (then workgroup 0 bumps step, no ticket)
+  const int64_t* step_rd;
   float warmup;             // linear LR warm-up over this many steps (0: none)
   unsigned int* ticket;     // zero-initialised arrival counter
   const float* loss_part; const int* correct_part; int nhead;

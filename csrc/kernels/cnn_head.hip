@@ -55,6 +55,7 @@ DEV bf16x4 relu_mask4(const f32x4& acc, const bf16x4& h) {
 
 template <int RB>
 __global__ __launch_bounds__(HT, 1) void k_head(DmlcHeadArgs a) {
+  if (a.step_copy && blockIdx.x == 0 && threadIdx.x == 0) *a.step_copy = *a.step;
   using L = HeadLds<RB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* w2s = reinterpret_cast<bf16*>(smem + L::W2);

@@ -126,7 +126,7 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   // (plain stores, no same-address atomics), loaded by wave 0 beside the slab loads
   float am[(C2_BLOCKS + 63) / 64];
   if (a.w2f8 && a.mode != 1 && threadIdx.x < T) {
-    const float* src = a.amax_w + (size_t)(*a.step & 1) * C2_BLOCKS;
+    const float* src = a.amax_w + (size_t)(*a.step_rd & 1) * C2_BLOCKS;
 #pragma unroll
     for (int u = 0; u < (C2_BLOCKS + 63) / 64; ++u) {
       const int i = threadIdx.x + 64 * u;
@@ -142,7 +142,7 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   const float4 w = sgd4(a.master + a.off[2] + e, w0, g, lr, a.grad_scale, a.mode != 3);
   const int ci = krow & 63, khw = krow >> 6;
   if (a.w2f8) {                                       // fp8 shadow for the fp8 conv2 forward
-    const int64_t step = *a.step;
+    const int64_t step = *a.step_rd;
     const int cur = (int)(step & 1), nxt = a.mode == 3 ? cur : cur ^ 1;
     float amax = am[0];
 #pragma unroll
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
   constexpr int LDS4 = FC2_COLS * (FC2_ROWS + 8) * 2 / 16 > 256 ? FC2_COLS * (FC2_ROWS + 8) * 2 / 16 : 256;
   __shared__ float4 lds[LDS4];                                // split sums (4 KB), fc2 transpose (6.8 KB)
   DMLC_STAMP(DMLC_TK_SGD, 0);
-  const int64_t step = *a.step;
+  const int64_t step = *a.step_rd;
   const float lr = lr_of(a, step);
   const int nfc1 = fc1_blocks(a);
   int blk = blockIdx.x + (a.roles == 2 ? C2_BLOCKS + C1_BLOCKS + 2 : 0);
@@ -321,6 +321,27 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
   if (a.bidx && (int)blockIdx.x * 256 < a.bidx_n) {
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r < a.bidx_n) a.bidx[r] = order_row(a.next, step + 1, r);
+  }
+  if (a.step_rd != a.step) {
+    // the step was read from the head's copy: no block of this launch reads *a.step, so workgroup 0
+    // alone sums the head's partials (an earlier launch), publishes the stats and bumps the counter
+    // -- no arrival ticket (two dependent atomic round trips on the launch's critical path)
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+      float loss = 0.f, corr = 0.f;
+      for (int q = threadIdx.x; q < a.nhead; q += 64) { loss += a.loss_part[q]; corr += (float)a.correct_part[q]; }
+      loss = wave_sum(loss);
+      corr = wave_sum(corr);
+      if (threadIdx.x == 0) {
+        float* st = a.stats + (size_t)(step % a.stats_len) * 4;
+        st[0] = (float)(step + 1);
+        st[1] = loss / (float)a.B;
+        st[2] = corr / (float)a.B;
+        st[3] = lr;
+        *a.step = step + 1;
+      }
+    }
+    DMLC_STAMP(DMLC_TK_SGD, 2);
+    return;
   }
   // last arriver: bump global_step, publish stats, re-arm the ticket for the next launch (the engine
   // zeroes it once at creation; every launch that starts also completes, so it stays consistent).

@@ -251,6 +251,10 @@ class FusedCifarEngine:
         self.loss_part = z(B // head_rows(B), dt=torch.float32)
         self.correct_part = z(B // head_rows(B), dt=torch.int32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        # the head kernel copies the step counter here; the SGD launch reads the copy, so one of its
+        # workgroups can bump step_t without an arrival ticket (cnn_sgd.hip)
+        self.step_sgd = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.sgd_ticket = os.environ.get("DMLC_SGD_TICKET", "0") == "1"   # A/B: the last-arriver ticket
         self.ticket = torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)   # two-level arrival counters
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
         self.logits_buf = z(B, 10, dt=torch.float32)
@@ -338,6 +342,7 @@ class FusedCifarEngine:
         if (old ^ int(step)) & 1:      # the current fc1 shadow moves to the new step's parity slot
             self.fc1n[int(step) & 1].copy_(self.fc1n[old & 1])
         self.step_t.fill_(int(step))
+        self.step_sgd.fill_(int(step))
         self.host_step = int(step)
         self._sync_bidx()
 
@@ -383,7 +388,7 @@ class FusedCifarEngine:
         o.head(self.h1part, p["full_bias_1"], self.fc2t, p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d,
                self.fc2n, self.labels, idx, counter, period, 1.0 / (self.Bv * self.world_size), self.relu_logits,
                train, self.h1, self.h2, self.dl, self.dh1, self.dh2, self.loss_part, self.correct_part, logits_out,
-               self.Bv)
+               self.Bv, self.step_t, self.step_sgd)
 
     def _gemm(self, f, sgd: bool = False):
         if sgd:
@@ -431,7 +436,8 @@ class FusedCifarEngine:
                      self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                      self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
                                                                       if self.fp8 else (None, None, None)),
-                     roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup, fc1_fused)
+                     roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup, fc1_fused,
+                     None if mode == 3 or self.sgd_ticket else self.step_sgd)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist

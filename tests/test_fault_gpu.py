@@ -72,3 +72,29 @@ def test_launcher_restarts_world_after_peer_loss(tmp_path):
     path = CK.latest_checkpoint(str(tmp_path))
     assert path.endswith("model.ckpt-100")
     assert int(CK.read_bundle(path)["global_step"]) == 100
+
+
+@pytest.mark.timeout(200)
+def test_survivor_exits_75_when_peer_dies_in_final_chunk(tmp_path):
+    """a peer lost inside the LAST chunk (generations 70, output points every 20: the
+    final chunk is steps 60..70 and rank 1 leaves at 60) -- the survivor's loop must run its progress
+    watchdog before the final device synchronisation, so it exits 75 instead of blocking in it."""
+    p1, p2 = cli.free_port(), cli.free_port()
+    flags = [f"--worker_hosts=localhost:{p1},localhost:{p2}", f"--log_dir={tmp_path}", "--generations=70"] + FLAGS
+    env = _env(DMLC_FAULT_STEP="60", DMLC_FAULT_RANK="1")
+    logs = [open(tmp_path / f"w{k}.log", "w+") for k in range(2)]
+    ws = [subprocess.Popen([sys.executable, ENTRY, "--job_name=worker", f"--task_index={k}"] + flags, env=env,
+                           stdout=logs[k], stderr=subprocess.STDOUT, text=True, start_new_session=True)
+          for k in range(2)]
+    try:
+        rc1 = ws[1].wait(timeout=150)
+        rc0 = ws[0].wait(timeout=40)
+    finally:
+        for w in ws:
+            if w.poll() is None:
+                w.kill()
+                w.wait()
+    out = [open(tmp_path / f"w{k}.log").read() for k in range(2)]
+    assert rc1 == 17, out[1][-3000:]
+    assert rc0 == 75, out[0][-3000:]
+    assert "global_step 60" in out[0] and "global_step 70" not in out[0], out[0][-3000:]

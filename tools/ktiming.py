@@ -82,8 +82,9 @@ def main():
             slots[sl] = [round(float(np.median(d)), 2), round(float(d.max()), 2)]
         rec["slot_med_max_us"] = slots
         if NAMES[k] == "sgd":      # per block-role breakdown (see cnn_sgd.hip block ranges)
+            nfc1 = 1 if getattr(eng, "fc1_epilogue", False) else 217     # fc1 bias only / weight + bias
             roles = {"conv1_rows": (0, 150), "conv_bias": (150, 152), "conv2_rows": (152, 552),
-                     "fc1": (552, 769), "fc2": (769, 793), "fc_tail": (793, 802)}
+                     "fc1": (552, 552 + nfc1), "fc2": (552 + nfc1, 576 + nfc1), "fc_tail": (576 + nfc1, 585 + nfc1)}
             raw = t[k]
             for name, (lo, hi) in roles.items():
                 sub = raw[lo:hi]
