@@ -431,7 +431,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
-      *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + pc * 8) = dv[k];
+      st_maybe_nt<kNtDg>(reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + pc * 8), dv[k]);
     }
   }
   lds_barrier();   // publishes dyp only; the dy2 global stores need not drain here
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
   bf16* dp1 = reinterpret_cast<bf16*>(a.dp1) + (size_t)b * 9216;
   for (int s = tid; s < 1152; s += NT) {
     const int p = s >> 3, c = s & 7;
-    *reinterpret_cast<bf16x8*>(dp1 + p * 64 + c * 8) = lds_b128(outs + swz128(p, c));
+    st_maybe_nt<kNtDg>(reinterpret_cast<bf16x8*>(dp1 + p * 64 + c * 8), lds_b128(outs + swz128(p, c)));
   }
   DMLC_STAMP(DMLC_TK_DGRAD, 4);
 }

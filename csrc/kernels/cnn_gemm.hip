@@ -209,7 +209,10 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
     const size_t base = (P.c_mode == 2 ? (size_t)split * P.M * P.ldc : 0) + (size_t)m * P.ldc + n;
     if (vec && n + 4 <= P.nvalid) {
       if (P.c_mode == 1) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(P.C) + base) = pack4(vv[0], vv[1], vv[2], vv[3]);
-      else *reinterpret_cast<float4*>(reinterpret_cast<float*>(P.C) + base) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      else {
+        const f32x4 o = {vv[0], vv[1], vv[2], vv[3]};
+        st_maybe_nt<kNtGemm>(reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + base), o);
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {

@@ -210,7 +210,7 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
   const size_t slab0 = (size_t)grp * 1600 * 64;
   auto put4 = [&](size_t e, const f32x4& v) {
     if (a.part2_bf16) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.part2) + slab0 + e) = pack4(v[0], v[1], v[2], v[3]);
-    else *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.part2) + slab0 + e) = v;
+    else st_maybe_nt<kNtDefault>(reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.part2) + slab0 + e), v);
   };
   auto put1 = [&](size_t e, float v) {
     if (a.part2_bf16) reinterpret_cast<bf16*>(a.part2)[slab0 + e] = (bf16)v;

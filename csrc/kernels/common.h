@@ -90,6 +90,36 @@ DEV float lr_sched(float lr0, float decay, float decay_steps, int staircase, flo
   return warmup > 0.f && (float)step < warmup ? lr * ((float)step + 1.f) / warmup : lr;
 }
 
+// Producer -> next-launch stores: plain, or streaming (nt: the lines do not stay dirty in this XCD's
+// L2, so the kernel-boundary write-back has less to flush; the consumers run on other XCDs anyway).
+// Same-session A/B at B=256 (r3): 79.3 us/step all plain, 78.8 with the conv2 slabs + dgrad outputs
+// streaming, 77.8-78.2 with conv12's pooled outputs, the conv1 slabs and the GEMM fp32 outputs too.
+// -DDMLC_NO_NT builds every site plain.
+#ifdef DMLC_NO_NT
+constexpr bool kNtDefault = false;
+#else
+constexpr bool kNtDefault = true;
+#endif
+template <bool NT, class T>
+DEV void st_maybe_nt(T* p, const T& v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+DEV void st_maybe_nt(uint4* p, const uint4& v) {
+  st_maybe_nt<NT>(reinterpret_cast<u32x4*>(p), __builtin_bit_cast(u32x4, v));
+}
+template <bool NT>
+DEV void st_maybe_nt(uint2* p, const uint2& v) {
+  st_maybe_nt<NT>(reinterpret_cast<u32x2*>(p), __builtin_bit_cast(u32x2, v));
+}
+constexpr bool kNtFwd = kNtDefault;
+constexpr bool kNtW1 = kNtDefault;
+constexpr bool kNtDg = kNtDefault;
+constexpr bool kNtGemm = kNtDefault;
+
 DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -164,7 +164,7 @@ DEV void w1_flush(char* fl_mem, const f32x4 (&acc)[2][5], float* out, float* out
       const f32x4 s = ((fl[e] + fl[640 + e]) + (fl[1280 + e] + fl[1920 + e]));
       const int tile = e >> 6, ln = e & 63, cp = tile / 5, t = tile - cp * 5;
       const int co = 16 * (2 * cp + h) + 4 * (ln >> 4), kk = 16 * t + (ln & 15);
-      *reinterpret_cast<f32x4*>(out + kk * 64 + co) = s;
+      st_maybe_nt<kNtW1>(reinterpret_cast<f32x4*>(out + kk * 64 + co), s);
       if (kk == 15) *reinterpret_cast<f32x4*>(outb + co) = s;
     }
   }
