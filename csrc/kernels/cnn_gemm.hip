@@ -186,8 +186,9 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
       const float4 g = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
       float4 v = wv[u];
       v.x -= f * g.x; v.y -= f * g.y; v.z -= f * g.z; v.w -= f * g.w;
-      *reinterpret_cast<float4*>(reinterpret_cast<float*>(P.C) + q) = v;
-      *reinterpret_cast<bf16x4*>(S + q) = pack4(v.x, v.y, v.z, v.w);
+      const f32x4 vo = {v.x, v.y, v.z, v.w};
+      st_maybe_nt<kNtX>(reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + q), vo);
+      st_maybe_nt<kNtX>(reinterpret_cast<bf16x4*>(S + q), pack4(v.x, v.y, v.z, v.w));
     }
     DMLC_STAMP(DMLC_TK_GEMM, 2);
     return;

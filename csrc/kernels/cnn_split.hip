@@ -81,8 +81,8 @@ DEV void pool_emit_c(const bf16* img, bf16* out, uint8_t* am, int c0, int tid) {
       if (j < 4) alo |= arg << (8 * j);
       else ahi |= arg << (8 * (j - 4));
     }
-    *reinterpret_cast<uint4*>(out + q * 64 + c0 + c * 8) = o;
-    *reinterpret_cast<uint2*>(am + q * 64 + c0 + c * 8) = make_uint2(alo, ahi);
+    st_maybe_nt<kNtX>(reinterpret_cast<uint4*>(out + q * 64 + c0 + c * 8), o);
+    st_maybe_nt<kNtX>(reinterpret_cast<uint2*>(am + q * 64 + c0 + c * 8), make_uint2(alo, ahi));
   }
 }
 
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(SP_NT, 4) void k_conv2_dgrad_split(DmlcConv2DgradAr
       const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
       const bf16x8 v = to_bf16x8(o[k]);
       *reinterpret_cast<bf16x8*>(dyp + swzpad((y + 2) * 16 + x + 2, c)) = v;
-      if ((c >> 2) == h) *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8) = v;
+      if ((c >> 2) == h) st_maybe_nt<kNtX>(reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8), v);
     }
   }
   lds_barrier();   // dyp published (dy2's global stores need not drain); dp2 / am2 reads done
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(SP_NT, 4) void k_conv2_dgrad_split(DmlcConv2DgradAr
   bf16* dp1 = reinterpret_cast<bf16*>(a.dp1) + (size_t)b * 9216 + 32 * h;
   for (int s = tid; s < 144 * 4; s += SP_NT) {
     const int p = s >> 2, c = s & 3;
-    *reinterpret_cast<bf16x8*>(dp1 + p * 64 + c * 8) = lds_b128(img + swzc<4>(p, c));
+    st_maybe_nt<kNtX>(reinterpret_cast<bf16x8*>(dp1 + p * 64 + c * 8), lds_b128(img + swzc<4>(p, c)));
   }
   DMLC_STAMP(DMLC_TK_DGRAD, 3);
 }

@@ -116,6 +116,7 @@ DEV void st_maybe_nt(uint2* p, const uint2& v) {
   st_maybe_nt<NT>(reinterpret_cast<u32x2*>(p), __builtin_bit_cast(u32x2, v));
 }
 constexpr bool kNtFwd = kNtDefault;
+constexpr bool kNtX = kNtDefault;   // the channel-split kernels' outputs, the fused-SGD epilogue (-0.4 us)
 constexpr bool kNtW1 = kNtDefault;
 constexpr bool kNtDg = kNtDefault;
 constexpr bool kNtGemm = kNtDefault;
