@@ -205,7 +205,8 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
              const Tensor& fcw, const Tensor& fcb, const Tensor& labels, const Tensor& idx,
              const c10::optional<Tensor>& counter, int64_t period, double inv_batch, const Tensor& gy,
              const Tensor& red, const Tensor& fc_part, const Tensor& loss_img, const Tensor& correct_img,
-             const c10::optional<Tensor>& logits, const c10::optional<Tensor>& red_det, int64_t nvalid) {
+             const c10::optional<Tensor>& logits, const c10::optional<Tensor>& red_det, int64_t nvalid,
+             const c10::optional<Tensor>& step, const c10::optional<Tensor>& step_copy) {
   const int64_t B = z.size(0), nv = valid_count(nvalid, B);
   check(z, "z", at::kBFloat16, {B, 8, 8, 64});
   check_stat(stat, "stat"); check_stat(red, "red");
@@ -237,6 +238,12 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
   }
   a.B = (int)B;
   a.nvalid = (int)nv;
+  TORCH_CHECK(step.has_value() == step_copy.has_value(), "rn_head: step and step_copy go together");
+  if (step.has_value()) {
+    check_numel(*step, "step", at::kLong, 1);
+    check_numel(*step_copy, "step_copy", at::kLong, 1);
+    a.step = step->data_ptr<int64_t>(); a.step_copy = step_copy->data_ptr<int64_t>();
+  }
   c10::DeviceGuard guard(z.device());
   CHECK_HIP(dmlc_rn_head(&a, stream_of(z)));
 }
@@ -254,7 +261,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
             at::TensorList wd, const Tensor& stat, const Tensor& red, const Tensor& fc_part, const Tensor& loss_img,
             const Tensor& correct_img, const Tensor& step, const Tensor& ticket, const Tensor& stats, int64_t mode,
             double lr0, double decay, double decay_steps, bool staircase, double bn_momentum, double warmup,
-            int64_t layer_lo, int64_t layer_hi, bool tail, int64_t nvalid) {
+            int64_t layer_lo, int64_t layer_hi, bool tail, int64_t nvalid, const c10::optional<Tensor>& step_rd) {
   constexpr int L = DMLC_RN_LAYERS;
   TORCH_CHECK(layer_lo >= 0 && layer_lo <= layer_hi && layer_hi <= L, "rn_sgd: bad layer range");
   TORCH_CHECK(tail || mode == 0, "rn_sgd: a partial (tail=False) launch is mode 0 only");
@@ -311,7 +318,13 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
   a.fcw_off = (int)fcw_off; a.fcb_off = (int)fcb_off; a.fc_part = fc_part.data_ptr<float>(); a.B = (int)B;
   a.mode = (int)mode;
   a.layer_lo = (int)layer_lo; a.layer_hi = (int)layer_hi; a.tail = tail ? 1 : 0;
-  a.step = step.data_ptr<int64_t>(); a.lr0 = (float)lr0; a.decay = (float)decay; a.decay_steps = (float)decay_steps;
+  a.step = step.data_ptr<int64_t>();
+  a.step_rd = a.step;
+  if (step_rd.has_value()) {
+    check_numel(*step_rd, "step_rd", at::kLong, 1);
+    a.step_rd = step_rd->data_ptr<int64_t>();
+  }
+  a.lr0 = (float)lr0; a.decay = (float)decay; a.decay_steps = (float)decay_steps;
   a.staircase = staircase ? 1 : 0;
   a.warmup = (float)warmup;
   a.ticket = reinterpret_cast<unsigned int*>(ticket.data_ptr<int>());
@@ -341,13 +354,13 @@ TORCH_LIBRARY_FRAGMENT(dmlc, m) {
   m.def("rn_head(Tensor z, Tensor stat, Tensor gamma, Tensor beta, Tensor sc, Tensor fcw, Tensor fcb, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, Tensor(a!) gy, Tensor(b!) red, "
         "Tensor(c!) fc_part, Tensor(d!) loss_img, Tensor(e!) correct_img, Tensor(f!)? logits, "
-        "Tensor(g!)? red_det=None, int nvalid=0) -> ()");
+        "Tensor(g!)? red_det=None, int nvalid=0, Tensor? step=None, Tensor(h!)? step_copy=None) -> ()");
   m.def("rn_sgd(Tensor(a!) master, Tensor(b!)? grad, float grad_scale, Tensor(c!) state, int[] conv_off, "
         "int[] gamma_off, int[] beta_off, int[] mm_off, int[] mv_off, int fcw_off, int fcb_off, Tensor[] part, "
         "Tensor(d!)[] wf, Tensor(e!)[] wd, Tensor stat, Tensor red, Tensor fc_part, Tensor loss_img, "
         "Tensor correct_img, Tensor(f!) step, Tensor(g!) ticket, Tensor(h!) stats, int mode, float lr0, "
         "float decay, float decay_steps, bool staircase, float bn_momentum, float warmup=0.0, int layer_lo=0, "
-        "int layer_hi=19, bool tail=True, int nvalid=0) -> ()");
+        "int layer_hi=19, bool tail=True, int nvalid=0, Tensor? step_rd=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {

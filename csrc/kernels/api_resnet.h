@@ -75,6 +75,7 @@ struct DmlcRnHeadArgs {
   float* logits_out;         // nullable [B][10]
   int B;
   int nvalid;                // images b >= nvalid: no loss, no accuracy, zero gradient
+  const int64_t* step; int64_t* step_copy;   // nullable: workgroup 0 copies *step (read by the SGD)
 };
 
 #define DMLC_RN_LAYERS 19
@@ -102,6 +103,8 @@ struct DmlcRnSgdArgs {
   int64_t* step; float lr0, decay, decay_steps; int staircase;
   float warmup;             // linear LR warm-up steps (0: none)
   unsigned int* ticket;
+  const int64_t* step_rd;   // == step (ticket: the last arriver bumps it) or the head's copy (the BN
+                            // layer-0 block bumps it, no ticket)
   const float* loss_img; const int* correct_img;
   float* stats; int stats_len;
   int nvalid;                // valid images of the batch (loss / accuracy means)

@@ -747,6 +747,7 @@ __global__ __launch_bounds__(RT, 2) void k_rn_bwd(DmlcRnDgradArgs d, DmlcRnWgrad
 // ================================ head =========================================================
 // per image: a18 = relu(bn(z18) + x_in) -> mean pool -> fc 64x10 -> softmax-xent -> backward to g_y18
 __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
+  if (a.step_copy && blockIdx.x == 0 && threadIdx.x == 0) *a.step_copy = *a.step;
   __shared__ float pool_part[4][64];
   __shared__ float pooled[64], dlog[16], gpool[64], cf[2][64];
   __shared__ float redl[2][4][64];
@@ -896,7 +897,7 @@ DEV float4 split_reduce(const float* p, size_t stride, int n, int S, float4* lds
 __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
   __shared__ float4 lds[RT];
   __shared__ float lred[2][4];
-  const int64_t step = *a.step;
+  const int64_t step = *a.step_rd;
   const float lr0 = a.staircase ? a.lr0 * powf(a.decay, floorf((float)step / a.decay_steps)) : a.lr0;
   const float lr = a.warmup > 0.f && (float)step < a.warmup ? lr0 * ((float)step + 1.f) / a.warmup : lr0;
   const int mode = a.mode;
@@ -1018,10 +1019,15 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
         float* st = a.stats + (size_t)(step % a.stats_len) * 4;
         st[1] = (lred[0][0] + lred[0][1] + lred[0][2] + lred[0][3]) / (float)a.nvalid;
         st[2] = (lred[1][0] + lred[1][1] + lred[1][2] + lred[1][3]) / (float)a.nvalid;
+        if (a.step_rd != a.step) {               // no block reads *a.step: publish + bump here
+          st[0] = (float)(step + 1);
+          st[3] = lr;
+          *a.step = step + 1;
+        }
       }
     }
   }
-  if (!apply || !a.tail) return;                 // a partial (layer-range) launch publishes nothing
+  if (!apply || !a.tail || a.step_rd != a.step) return;   // partial launch / ticketless: nothing more
   __syncthreads();
   if (tid == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -183,6 +183,12 @@ class FusedResNetEngine:
         self.correct_img = z(B, dt=torch.int32)
         self.logits_buf = z(B, 10, dt=torch.float32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        # DMLC_SGD_TICKET=0: the head copies the step counter here and the SGD reads the copy, so its
+        # BN layer-0 block bumps step_t without an arrival ticket.  Unlike the CNN step (-0.9 us) this
+        # measured no better here (r3: 0.679 / 0.682 ms vs 0.675 / 0.678 with the ticket), so the
+        # ticket stays the default
+        self.step_sgd = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.sgd_ticket = os.environ.get("DMLC_SGD_TICKET", "1") == "1"
         self.ticket = torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)   # two-level arrival counters
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
 
@@ -236,6 +242,7 @@ class FusedResNetEngine:
 
     def set_step(self, step: int):
         self.step_t.fill_(int(step))
+        self.step_sgd.fill_(int(step))
         self.host_step = int(step)
 
     def epoch_permutation(self, epoch: int) -> torch.Tensor:
@@ -264,7 +271,8 @@ class FusedResNetEngine:
                      sc_src, sc_mode, self.a[p], self.wf[l], self.z[l], self.stat[l], self._det_stat[l], self.Bv)
         o.rn_head(self.z[18], self.stat[18], self.gamma[18], self.beta[18], self.a[16], self.fcw, self.fcb,
                   self.labels, idx, counter, period, 1.0 / (self.Bv * self.world_size), self.gy[18], self.red[18],
-                  self.fc_part, self.loss_img, self.correct_img, logits_out, self._det_red[18], self.Bv)
+                  self.fc_part, self.loss_img, self.correct_img, logits_out, self._det_red[18], self.Bv,
+                  self.step_t, self.step_sgd)
 
     def _wgrad(self, l):
         _, ci, co, h, s = LAYERS[l]
@@ -325,7 +333,8 @@ class FusedResNetEngine:
                         self.mm_off, self.mv_off, self.fcw_off, self.fcb_off, self.part, self.wf, self.wd, self.stat,
                         self.red, self.fc_part, self.loss_img, self.correct_img, self.step_t, self.ticket, self.stats,
                         mode, self.lr0, self.decay, self.decay_steps, self.staircase, R.BN_MOMENTUM, self.warmup,
-                        layers[0], layers[1], tail, self.Bv)
+                        layers[0], layers[1], tail, self.Bv,
+                        None if mode == 3 or self.sgd_ticket else self.step_sgd)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
