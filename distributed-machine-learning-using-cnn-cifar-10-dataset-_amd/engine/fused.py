@@ -189,6 +189,8 @@ class FusedCifarEngine:
         # workgroup per image); B=256 85.1 vs 82.9 -- the split pays only while the chip is not full
         self.conv_split = 1 if self.fp8 else (conv_split or env_cs or (2 if B <= 128 else 1))
         self.conv1_split = conv1_split or env_c1 or 2
+        # the conv2 input gradient's split, independently of the forward's (DMLC_DGRAD_SPLIT, A/B runs)
+        self.dgrad_split = 1 if self.fp8 else int(os.environ.get("DMLC_DGRAD_SPLIT", "0") or 0) or self.conv_split
         if self.conv_split not in (1, 2) or self.conv1_split not in (2, 4):
             raise ValueError(f"conv_split must be 1 or 2 and conv1_split 2 or 4 ({self.conv_split}, {self.conv1_split})")
         # DMLC_FUSED_W1=1: the conv1 weight gradient inside the conv2-dgrad launch (one slab per image,
@@ -412,7 +414,7 @@ class FusedCifarEngine:
             return
         if self.fp8_dgrad:
             o.conv2_dgrad_fp8(self.dp2, self.am2, self.w2f8[1], self.scale_w, self.dp1, self.dy2)
-        elif self.conv_split == 2:
+        elif self.dgrad_split == 2:
             o.conv2_dgrad_split(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         else:
             o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
