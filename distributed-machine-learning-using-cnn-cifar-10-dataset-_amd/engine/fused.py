@@ -173,7 +173,7 @@ class FusedCifarEngine:
             self.scale_w = z(2, dt=torch.float32)
 
         # --- activations / workspaces -------------------------------------------------------
-        self.fc1_split = fc1_split or self._pick_fc1_split(B)
+        self.fc1_split = fc1_split or int(os.environ.get("DMLC_FC1_SPLIT", "0") or 0) or self._pick_fc1_split(B)
         # both weight gradients run in ONE launch (ops.wgrad: no stream fork/join in the graph);
         # DMLC_SPLIT_WGRAD=1 runs them as two kernels on forked streams instead (A/B comparisons)
         self.merged_wgrad = os.environ.get("DMLC_SPLIT_WGRAD", "0") != "1"
