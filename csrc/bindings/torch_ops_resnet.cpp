@@ -190,14 +190,17 @@ void rn_bwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor
             const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
             const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
             const Tensor& gy_prev, const Tensor& red_prev, const Tensor& part, const c10::optional<Tensor>& red_det,
-            int64_t nvalid) {
+            int64_t nvalid, bool per_image) {
   const Geom g = geom(cin, cout, hin, stride);
   const DmlcRnDgradArgs d = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
                                        gy_sc, sc_mode, gy_prev, red_prev, red_det, nvalid);
   const DmlcRnWgradArgs w = wgrad_args(g, cin, cout, hin, c10::nullopt, c10::nullopt, c10::nullopt, 1, 0, 0, a_prev, gy,
                                        z, stat, red, gamma, part, nvalid);
+  TORCH_CHECK(!per_image || (cin == 16 && cout == 16 && hin == 32 && stride == 1 && w.G == w.B),
+              "rn_bwd per_image: 16->16 stride-1 layers with one split-K group per image only");
   c10::DeviceGuard guard(gy.device());
-  const DmlcRnLayerGeom gc = g.c();
+  DmlcRnLayerGeom gc = g.c();
+  gc.per_image = per_image ? 1 : 0;
   CHECK_HIP(dmlc_rn_bwd(&gc, &d, &w, stream_of(gy)));
 }
 
@@ -350,7 +353,8 @@ TORCH_LIBRARY_FRAGMENT(dmlc, m) {
         "Tensor(a!) part, int nvalid=0) -> ()");
   m.def("rn_bwd(int cin, int cout, int hin, int stride, Tensor gy, Tensor z, Tensor stat, Tensor red, "
         "Tensor gamma, Tensor wd, Tensor a_prev, Tensor z_prev, Tensor stat_prev, Tensor? gy_sc, int sc_mode, "
-        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part, Tensor(d!)? red_det=None, int nvalid=0) -> ()");
+        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part, Tensor(d!)? red_det=None, int nvalid=0, "
+        "bool per_image=False) -> ()");
   m.def("rn_head(Tensor z, Tensor stat, Tensor gamma, Tensor beta, Tensor sc, Tensor fcw, Tensor fcb, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, Tensor(a!) gy, Tensor(b!) red, "
         "Tensor(c!) fc_part, Tensor(d!) loss_img, Tensor(e!) correct_img, Tensor(f!)? logits, "

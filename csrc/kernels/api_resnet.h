@@ -18,6 +18,7 @@ extern "C" {
 
 struct DmlcRnLayerGeom {    // runtime copy of the compile-time geometry (validated by the binding)
   int cin, cout, hin, stride;
+  int per_image;             // rn_bwd: one workgroup per image for dgrad AND wgrad (16->16 layers, G == B)
 };
 
 struct DmlcRnFwdArgs {

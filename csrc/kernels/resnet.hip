@@ -75,6 +75,12 @@ DEV void bnb_coeffs(const double* stat, const double* red, const float* gamma, i
   Cc = -A * (float)(r1 * (double)inv_n) - Bc * mean;
 }
 
+// g_z = A*g_y + Bc*z + Cc with the rounding pinned (two explicit FMAs): the dgrad, the wgrad and the
+// per-image backward each rebuild g_z from the same bf16 inputs and must agree bit for bit
+DEV float bnb_apply(float A, float Bc, float Cc, float gy, float z) {
+  return __builtin_fmaf(A, gy, __builtin_fmaf(Bc, z, Cc));
+}
+
 DEV uint32_t pack2(float a, float b) {
   const bf16x4 v = pack4(a, b, 0.f, 0.f);
   return __builtin_bit_cast(uint2, v).x;
@@ -417,8 +423,8 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
         uint32_t ow[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float v0 = A[2 * k] * bf16_lo(gw[k]) + Bc[2 * k] * bf16_lo(zw[k]) + Cc[2 * k];
-          const float v1 = A[2 * k + 1] * bf16_hi(gw[k]) + Bc[2 * k + 1] * bf16_hi(zw[k]) + Cc[2 * k + 1];
+          const float v0 = bnb_apply(A[2 * k], Bc[2 * k], Cc[2 * k], bf16_lo(gw[k]), bf16_lo(zw[k]));
+          const float v1 = bnb_apply(A[2 * k + 1], Bc[2 * k + 1], Cc[2 * k + 1], bf16_hi(gw[k]), bf16_hi(zw[k]));
           ow[k] = okv[i] ? pack2(v0, v1) : 0u;
         }
         reinterpret_cast<uint4*>(gs)[e] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
@@ -508,7 +514,7 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
       for (int r = 0; r < 4; ++r) {
         gy[r] = av4[r] > 0.f ? acc[i][r] + sc4[r] : 0.f;
         s1[r] += gy[r];
-        s2[r] += gy[r] * (zv4[r] - mean[r]) * rstd[r];
+        s2[r] = __builtin_fmaf(gy[r] * (zv4[r] - mean[r]), rstd[r], s2[r]);   // pinned (bitwise across kernels)
       }
       st_maybe_nt<kNtRn>(reinterpret_cast<bf16x4*>(gyo + px * CIN + c0), pack4(gy[0], gy[1], gy[2], gy[3]));
     }
@@ -645,8 +651,8 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
           uint32_t ow[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k)
-            ow[k] = real ? pack2(A[2 * k] * bf16_lo(gw[k]) + Bc[2 * k] * bf16_lo(zw[k]) + Cc[2 * k],
-                                 A[2 * k + 1] * bf16_hi(gw[k]) + Bc[2 * k + 1] * bf16_hi(zw[k]) + Cc[2 * k + 1])
+            ow[k] = real ? pack2(bnb_apply(A[2 * k], Bc[2 * k], Cc[2 * k], bf16_lo(gw[k]), bf16_lo(zw[k])),
+                                 bnb_apply(A[2 * k + 1], Bc[2 * k + 1], Cc[2 * k + 1], bf16_hi(gw[k]), bf16_hi(zw[k])))
                          : 0u;
           *reinterpret_cast<uint4*>(gz + im * G::GE + (e1 / C8) * GLD + (e1 % C8) * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         }
@@ -741,6 +747,240 @@ __global__ __launch_bounds__(RT, 2) void k_rn_bwd(DmlcRnDgradArgs d, DmlcRnWgrad
   } else {
     const int t = (int)blockIdx.x - d.B;
     rn_wgrad_body<CIN, COUT, HIN, S>(w, t % w.G, t / w.G);
+  }
+}
+
+// ============================ per-image backward (stride 1, one slab per image) ====================
+// Layer l's input gradient AND its weight gradient from ONE workgroup per image: the g_z image the
+// dgrad stages (padded, [HPD][HPD][COUT]) is also the weight gradient's B operand, and the layer
+// input a_{l-1} is staged once into LDS (padded) for both the dgrad epilogue's ReLU mask and the
+// weight gradient's A operand -- the separate wgrad blocks re-read g_y, z and a_{l-1} from memory
+// (96 KB per 32x32x16 image).  Needs one split-K group per image (w.G == B, the 16-channel layers'
+// choice at B <= 256): the slab of image b is part[b].  Same per-image sums in the same k-step
+// order as the grouped wgrad body: the step is bitwise the merged launch's.
+template <int CIN, int COUT, int HIN>
+struct BwdImg {
+  using D = Dg<CIN, COUT, HIN, 1>;
+  static constexpr int HP = HIN + 2, CINP = CIN;
+  static constexpr int XCH = HP * HP * CIN / 8, XIT = (XCH + RT - 1) / RT;
+  static constexpr size_t XB = (size_t)HP * HP * CIN * 2;
+  static constexpr int KP = round32(9 * CIN), MT = KP / 16, MJ = (MT + 3) / 4;
+  static constexpr int NPIX = HIN * HIN, KSTEPS = NPIX / 32;
+  static constexpr size_t LDS = D::GB + XB + 4 * 2 * 64 * 4 + 5 * 64 * 4;
+  static_assert(COUT == 16, "per-image backward: one 16-wide c_out tile");
+};
+
+template <int CIN, int COUT, int HIN>
+__global__ __launch_bounds__(RT, 2) void k_rn_bwd_img(DmlcRnDgradArgs a, DmlcRnWgradArgs wa_) {
+  using D = Dg<CIN, COUT, HIN, 1>;
+  using I = BwdImg<CIN, COUT, HIN>;
+  constexpr int HPD = D::HPD, KPD = D::KPD, C8 = COUT / 8, HP = I::HP;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* gs = reinterpret_cast<bf16*>(smem);
+  bf16* xs = reinterpret_cast<bf16*>(smem + D::GB);
+  float* red = reinterpret_cast<float*>(smem + D::GB + I::XB);   // [4][2][64]
+  float* cf = red + 4 * 2 * 64;                                  // [5][64]
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15;
+  const int q = li >> 2, p = li & 3;
+
+  if (tid < COUT) {
+    float A, Bc, Cc;
+    bnb_coeffs(a.stat, a.red, a.gamma, tid, a.inv_n, A, Bc, Cc);
+    cf[tid] = A; cf[64 + tid] = Bc; cf[128 + tid] = Cc;
+  } else if (tid >= 128 && tid < 128 + CIN) {
+    float mean, rstd;
+    bn_mean_rstd(a.stat_prev, tid - 128, a.inv_n_prev, mean, rstd);
+    cf[192 + tid - 128] = mean; cf[256 + tid - 128] = rstd;
+  }
+  // ---- prologue: g_z of layer l on the padded grid (as rn_dgrad_body, stride 1) ----
+  {
+    const int c8 = tid % C8;
+    const uint4* gyp = reinterpret_cast<const uint4*>(a.gy) + (size_t)b * HIN * HIN * C8;
+    const uint4* zp = reinterpret_cast<const uint4*>(a.z) + (size_t)b * HIN * HIN * C8;
+    uint4 gv[D::IT], zv[D::IT];
+    bool okv[D::IT];
+#pragma unroll
+    for (int i = 0; i < D::IT; ++i) {
+      const int e = min(tid + i * RT, D::NCH - 1);
+      const int pp = e / C8, py = pp / HPD, px = pp % HPD;
+      const int oy = py - 1, ox = px - 1;
+      const bool ok = oy >= 0 && oy < HIN && ox >= 0 && ox < HIN;
+      const int qq = (ok ? oy * HIN + ox : 0) * C8 + c8;
+      gv[i] = gyp[qq];
+      zv[i] = zp[qq];
+      okv[i] = ok && (tid + i * RT) < D::NCH && b < a.nvalid;   // padding image: g_z = 0
+    }
+    lds_barrier();
+    float A[8], Bc[8], Cc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { A[j] = cf[c8 * 8 + j]; Bc[j] = cf[64 + c8 * 8 + j]; Cc[j] = cf[128 + c8 * 8 + j]; }
+#pragma unroll
+    for (int i = 0; i < D::IT; ++i) {
+      const int e = tid + i * RT;
+      if (e < D::NCH) {
+        const uint32_t gw[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w}, zw[4] = {zv[i].x, zv[i].y, zv[i].z, zv[i].w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float v0 = bnb_apply(A[2 * k], Bc[2 * k], Cc[2 * k], bf16_lo(gw[k]), bf16_lo(zw[k]));
+          const float v1 = bnb_apply(A[2 * k + 1], Bc[2 * k + 1], Cc[2 * k + 1], bf16_hi(gw[k]), bf16_hi(zw[k]));
+          ow[k] = okv[i] ? pack2(v0, v1) : 0u;
+        }
+        reinterpret_cast<uint4*>(gs)[e] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      }
+    }
+  }
+  // the layer input a_{l-1} (padded, halo 0): its loads fly during the dgrad MFMAs
+  uint4 xv[I::XIT];
+  {
+    constexpr int X8 = CIN / 8;
+    const uint4* xp = reinterpret_cast<const uint4*>(a.a_prev) + (size_t)b * HIN * HIN * X8;
+#pragma unroll
+    for (int i = 0; i < I::XIT; ++i) {
+      const int e = min(tid + i * RT, I::XCH - 1);
+      const int pp = e / X8, iy = pp / HP - 1, ix = pp % HP - 1;
+      const bool ok = iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
+      xv[i] = load_sel(xp + (ok ? (iy * HIN + ix) * X8 + e % X8 : 0), xp, ok);
+    }
+  }
+  const int ct = w % D::CT, pt0 = w / D::CT;
+  const bf16* Wd = reinterpret_cast<const bf16*>(a.wd) + (16 * ct + li) * KPD + 8 * g;
+  bf16x8 wdf[D::KS];
+#pragma unroll
+  for (int ks = 0; ks < D::KS; ++ks) wdf[ks] = glb_b128(Wd + 32 * ks);
+  __syncthreads();
+
+  // ---- dgrad MFMAs (as rn_dgrad_body) ----
+  f32x4 acc[D::NPT];
+#pragma unroll
+  for (int i = 0; i < D::NPT; ++i) acc[i] = zero4();
+#pragma unroll
+  for (int i = 0; i < D::NPT; ++i) {
+    const int px = 16 * (pt0 + D::WPC * i) + li;
+    const int iy = px / HIN, ix = px - (px / HIN) * HIN;
+    const int base = iy * HPD + ix;
+#pragma unroll
+    for (int ks = 0; ks < D::KS; ++ks) {
+      const int k0 = 32 * ks + 8 * g;
+      const int tap = min(k0 / COUT, 8), co0 = k0 % COUT;
+      const int kh = tap / 3, kw = tap - 3 * (tap / 3);
+      const bf16x8 bx = lds_b128(gs + (base + kh * HPD + kw) * COUT + co0);
+      acc[i] = mfma16(wdf[ks], bx, acc[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < I::XIT; ++i) {
+    const int e = tid + i * RT;
+    if (e < I::XCH) reinterpret_cast<uint4*>(xs)[e] = xv[i];
+  }
+  __syncthreads();                                // xs complete (the epilogue's mask reads it)
+
+  // ---- dgrad epilogue: g_a_{l-1} (+ shortcut) -> g_y_{l-1} + its BN reductions ----
+  struct EpiIn { uint2 z, s; };
+  constexpr int EC = D::NPT < 4 ? D::NPT : 4;
+  const int c0 = 16 * ct + 4 * g;
+  const bf16* zpp = reinterpret_cast<const bf16*>(a.z_prev) + (size_t)b * HIN * HIN * CIN;
+  auto epi_load = [&](int i, EpiIn& e) {
+    const int px = 16 * (pt0 + D::WPC * i) + li;
+    const int iy = px / HIN, ix = px - (px / HIN) * HIN;
+    e.z = *reinterpret_cast<const uint2*>(zpp + px * CIN + c0);
+    e.s = make_uint2(0u, 0u);
+    if (a.sc_mode == 1) {
+      e.s = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.gy_sc) + ((size_t)b * HIN * HIN + px) * CIN + c0);
+    } else if (a.sc_mode == 2) {
+      const bool even = !(iy & 1) && !(ix & 1);
+      const int HB = HIN / 2;
+      const size_t qq = ((size_t)b * HB * HB + (even ? (iy / 2) * HB + ix / 2 : 0)) * (2 * CIN) + c0;
+      const uint2 v = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16*>(a.gy_sc) + qq);
+      e.s = even ? v : make_uint2(0u, 0u);
+    }
+  };
+  EpiIn cur[EC];
+#pragma unroll
+  for (int j = 0; j < EC; ++j) epi_load(j, cur[j]);
+  float mean[4], rstd[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { mean[r] = cf[192 + c0 + r]; rstd[r] = cf[256 + c0 + r]; }
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  bf16* gyo = reinterpret_cast<bf16*>(a.gy_prev) + (size_t)b * HIN * HIN * CIN;
+#pragma unroll
+  for (int c = 0; c < D::NPT; c += EC) {
+    EpiIn nxt[EC];
+    if (c + EC < D::NPT) {
+#pragma unroll
+      for (int j = 0; j < EC; ++j) epi_load(c + EC + j, nxt[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < EC; ++j) {
+      const int i = c + j;
+      const int px = 16 * (pt0 + D::WPC * i) + li;
+      const int iy = px / HIN, ix = px - (px / HIN) * HIN;
+      const uint2 av = *reinterpret_cast<const uint2*>(xs + ((iy + 1) * HP + ix + 1) * CIN + c0);
+      const uint2 zv = cur[j].z, sv = cur[j].s;
+      const float sc4[4] = {bf16_lo(sv.x), bf16_hi(sv.x), bf16_lo(sv.y), bf16_hi(sv.y)};
+      const float av4[4] = {bf16_lo(av.x), bf16_hi(av.x), bf16_lo(av.y), bf16_hi(av.y)};
+      const float zv4[4] = {bf16_lo(zv.x), bf16_hi(zv.x), bf16_lo(zv.y), bf16_hi(zv.y)};
+      float gy[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        gy[r] = av4[r] > 0.f ? acc[i][r] + sc4[r] : 0.f;
+        s1[r] += gy[r];
+        s2[r] = __builtin_fmaf(gy[r] * (zv4[r] - mean[r]), rstd[r], s2[r]);   // pinned (bitwise across kernels)
+      }
+      st_maybe_nt<kNtRn>(reinterpret_cast<bf16x4*>(gyo + px * CIN + c0), pack4(gy[0], gy[1], gy[2], gy[3]));
+    }
+    if (c + EC < D::NPT) {
+#pragma unroll
+      for (int j = 0; j < EC; ++j) cur[j] = nxt[j];
+    }
+  }
+  reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid, a.red_det, a.B);
+
+  // ---- weight gradient of this image: C[k = (tap, ci)][co] = sum_px X[px + tap][ci] g_z[px][co] ----
+  int moff[I::MJ];
+  bool mok[I::MJ];
+#pragma unroll
+  for (int j = 0; j < I::MJ; ++j) {
+    const int m = w + 4 * j;
+    mok[j] = m < I::MT;                             // wave-uniform
+    const int tap = min(m, 8);                      // CIN = 16: m-tile m = tap m (m = 9: K padding)
+    moff[j] = (tap / 3) * HP + tap % 3;
+  }
+  auto prow = [&](int r) { return ((r / HIN) + 1) * HPD + (r % HIN) + 1; };   // padded g_z row of pixel r
+  auto frags = [&](int s_, bf16x8& bf, bf16x8 (&af)[I::MJ]) {
+    const int rA = 32 * s_ + 8 * g + q, rB = rA + 4;
+    bf = tr_frag(gs + prow(rA) * COUT + 4 * p, gs + prow(rB) * COUT + 4 * p);
+    const int pA = (rA / HIN) * HP + rA % HIN, pB = (rB / HIN) * HP + rB % HIN;
+#pragma unroll
+    for (int j = 0; j < I::MJ; ++j)
+      if (mok[j]) af[j] = tr_frag(xs + (pA + moff[j]) * CIN + 4 * p, xs + (pB + moff[j]) * CIN + 4 * p);
+  };
+  f32x4 wacc[I::MJ];
+#pragma unroll
+  for (int j = 0; j < I::MJ; ++j) wacc[j] = zero4();
+  bf16x8 bfr, afr[I::MJ];
+  frags(0, bfr, afr);
+  for (int s_ = 0; s_ < I::KSTEPS; ++s_) {
+    bf16x8 bn, an[I::MJ];
+    wait_lds();
+    __builtin_amdgcn_sched_barrier(0);
+    if (s_ + 1 < I::KSTEPS) frags(s_ + 1, bn, an);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < I::MJ; ++j)
+      if (mok[j]) wacc[j] = mfma16(afr[j], bfr, wacc[j]);
+    bfr = bn;
+#pragma unroll
+    for (int j = 0; j < I::MJ; ++j) afr[j] = an[j];
+  }
+  float* out = wa_.part + (size_t)b * I::KP * COUT;
+#pragma unroll
+  for (int j = 0; j < I::MJ; ++j) {
+    const int m = w + 4 * j;
+    if (mok[j]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st_maybe_nt<kNtRn>(out + (16 * m + 4 * g + i) * COUT + li, wacc[j][i]);
+    }
   }
 }
 
@@ -1092,6 +1332,14 @@ hipError_t launch_bwd(const DmlcRnDgradArgs& d, const DmlcRnWgradArgs& w, hipStr
   }
 }
 
+hipError_t launch_bwd_img(const DmlcRnDgradArgs& d, const DmlcRnWgradArgs& w, hipStream_t s) {
+  using I = BwdImg<16, 16, 32>;
+  if (w.G != d.B) return hipErrorInvalidValue;   // one slab per image
+  DMLC_LDS_OPTIN((&k_rn_bwd_img<16, 16, 32>), I::LDS);
+  hipLaunchKernelGGL((k_rn_bwd_img<16, 16, 32>), dim3(d.B), dim3(RT), I::LDS, s, d, w);
+  return hipGetLastError();
+}
+
 template <int CI, int CO, int H, int ST>
 hipError_t launch_wgrad(const DmlcRnWgradArgs& a, hipStream_t s) {
   using G = Wg<CI, CO, H, ST>;
@@ -1130,6 +1378,10 @@ hipError_t dmlc_rn_wgrad(const DmlcRnLayerGeom* g, const DmlcRnWgradArgs* a, hip
 
 hipError_t dmlc_rn_bwd(const DmlcRnLayerGeom* g, const DmlcRnDgradArgs* d, const DmlcRnWgradArgs* w, hipStream_t s) {
   if (d->B != w->B) return hipErrorInvalidValue;
+  if (g->per_image) {                              // one workgroup per image: dgrad + wgrad
+    if (g->cin == 16 && g->cout == 16 && g->hin == 32 && g->stride == 1) return launch_bwd_img(*d, *w, s);
+    return hipErrorInvalidValue;
+  }
 #define X(CI, CO, H, ST) \
   if (CI >= 16 && g->cin == CI && g->cout == CO && g->hin == H && g->stride == ST) return launch_bwd<CI, CO, H, ST>(*d, *w, s);
   DMLC_RN_SHAPES(X)

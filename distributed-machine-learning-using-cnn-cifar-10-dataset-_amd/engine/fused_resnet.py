@@ -209,6 +209,7 @@ class FusedResNetEngine:
             wgrad_branch = os.environ.get("DMLC_RN_WGRAD_BRANCH", "1" if B > 256 else "0") == "1"
         self.wgrad_branch = wgrad_branch
         self.merged_bwd = os.environ.get("DMLC_RN_MERGED_BWD", "1" if B <= 256 else "0") == "1"
+        self.bwd_img = os.environ.get("DMLC_RN_BWD_IMG", "1") != "0"
         # DMLC_RN_SGD_SPLIT=1 (single GPU, merged backward): the SGD of stage 3 (layers 13-18) and of
         # stage 2 (7-12) runs on a graph branch as soon as their weight gradients are complete, beside
         # the stage-2 / stage-1 backward; the main-stream SGD does the rest and publishes the step.
@@ -274,6 +275,13 @@ class FusedResNetEngine:
                   self.fc_part, self.loss_img, self.correct_img, logits_out, self._det_red[18], self.Bv,
                   self.step_t, self.step_sgd)
 
+    def _per_image(self, l) -> bool:
+        """Layer l's dgrad and wgrad from one workgroup per image (k_rn_bwd_img): the 16->16 stride-1
+        layers whose weight gradient already keeps one split-K slab per image (G == B, B <= 256).
+        DMLC_RN_BWD_IMG=0: the merged launch with separate wgrad blocks."""
+        _, ci, co, h, s = LAYERS[l]
+        return (self.bwd_img and (ci, co, h, s) == (16, 16, 32, 1) and self.part[l].shape[0] == self.B)
+
     def _wgrad(self, l):
         _, ci, co, h, s = LAYERS[l]
         if l == 0:
@@ -298,7 +306,7 @@ class FusedResNetEngine:
                     gy_sc = self.gy[l + 1]
                 o.rn_bwd(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
                          self.a[l - 1], self.z[l - 1], self.stat[l - 1], gy_sc, sc_mode, self.gy[l - 1],
-                         self.red[l - 1], self.part[l], self._det_red[l - 1], self.Bv)
+                         self.red[l - 1], self.part[l], self._det_red[l - 1], self.Bv, self._per_image(l))
                 if self.sgd_split and l in self._sgd_points:
                     # layers >= l: slabs complete, weights no longer read this step
                     self.side_stream.wait_stream(main)
