@@ -196,8 +196,9 @@ void rn_bwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor
                                        gy_sc, sc_mode, gy_prev, red_prev, red_det, nvalid);
   const DmlcRnWgradArgs w = wgrad_args(g, cin, cout, hin, c10::nullopt, c10::nullopt, c10::nullopt, 1, 0, 0, a_prev, gy,
                                        z, stat, red, gamma, part, nvalid);
-  TORCH_CHECK(!per_image || (cin == 16 && cout == 16 && hin == 32 && stride == 1 && w.G == w.B),
-              "rn_bwd per_image: 16->16 stride-1 layers with one split-K group per image only");
+  TORCH_CHECK(!per_image || (((cin == 16 && hin == 32) || (cin == 32 && hin == 16)) && cout == cin && stride == 1 &&
+                              w.G == w.B),
+              "rn_bwd per_image: 16->16 / 32->32 stride-1 layers with one split-K group per image only");
   c10::DeviceGuard guard(gy.device());
   DmlcRnLayerGeom gc = g.c();
   gc.per_image = per_image ? 1 : 0;

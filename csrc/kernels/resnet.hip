@@ -764,10 +764,10 @@ struct BwdImg {
   static constexpr int HP = HIN + 2, CINP = CIN;
   static constexpr int XCH = HP * HP * CIN / 8, XIT = (XCH + RT - 1) / RT;
   static constexpr size_t XB = (size_t)HP * HP * CIN * 2;
-  static constexpr int KP = round32(9 * CIN), MT = KP / 16, MJ = (MT + 3) / 4;
+  static constexpr int KP = round32(9 * CIN), MT = KP / 16, MJ = (MT + 3) / 4, NT = COUT / 16;
   static constexpr int NPIX = HIN * HIN, KSTEPS = NPIX / 32;
   static constexpr size_t LDS = D::GB + XB + 4 * 2 * 64 * 4 + 5 * 64 * 4;
-  static_assert(COUT == 16, "per-image backward: one 16-wide c_out tile");
+  static_assert(CIN == COUT && CIN % 16 == 0 && NPIX % 32 == 0, "per-image backward: square stride-1 layers");
 };
 
 template <int CIN, int COUT, int HIN>
@@ -937,39 +937,49 @@ __global__ __launch_bounds__(RT, 2) void k_rn_bwd_img(DmlcRnDgradArgs a, DmlcRnW
   reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid, a.red_det, a.B);
 
   // ---- weight gradient of this image: C[k = (tap, ci)][co] = sum_px X[px + tap][ci] g_z[px][co] ----
-  int moff[I::MJ];
+  // m-tile m: k = 16m .. 16m+15 = tap (16m) / CIN, channels (16m) % CIN .. +15 (taps past 8: K padding)
+  int moff[I::MJ], mci[I::MJ];
   bool mok[I::MJ];
 #pragma unroll
   for (int j = 0; j < I::MJ; ++j) {
     const int m = w + 4 * j;
     mok[j] = m < I::MT;                             // wave-uniform
-    const int tap = min(m, 8);                      // CIN = 16: m-tile m = tap m (m = 9: K padding)
+    const int tap = min((16 * m) / CIN, 8);
     moff[j] = (tap / 3) * HP + tap % 3;
+    mci[j] = (16 * m) % CIN + 4 * p;
   }
   auto prow = [&](int r) { return ((r / HIN) + 1) * HPD + (r % HIN) + 1; };   // padded g_z row of pixel r
-  auto frags = [&](int s_, bf16x8& bf, bf16x8 (&af)[I::MJ]) {
+  auto frags = [&](int s_, bf16x8 (&bf)[I::NT], bf16x8 (&af)[I::MJ]) {
     const int rA = 32 * s_ + 8 * g + q, rB = rA + 4;
-    bf = tr_frag(gs + prow(rA) * COUT + 4 * p, gs + prow(rB) * COUT + 4 * p);
+#pragma unroll
+    for (int n = 0; n < I::NT; ++n)
+      bf[n] = tr_frag(gs + prow(rA) * COUT + 16 * n + 4 * p, gs + prow(rB) * COUT + 16 * n + 4 * p);
     const int pA = (rA / HIN) * HP + rA % HIN, pB = (rB / HIN) * HP + rB % HIN;
 #pragma unroll
     for (int j = 0; j < I::MJ; ++j)
-      if (mok[j]) af[j] = tr_frag(xs + (pA + moff[j]) * CIN + 4 * p, xs + (pB + moff[j]) * CIN + 4 * p);
+      if (mok[j]) af[j] = tr_frag(xs + (pA + moff[j]) * CIN + mci[j], xs + (pB + moff[j]) * CIN + mci[j]);
   };
-  f32x4 wacc[I::MJ];
+  f32x4 wacc[I::MJ][I::NT];
 #pragma unroll
-  for (int j = 0; j < I::MJ; ++j) wacc[j] = zero4();
-  bf16x8 bfr, afr[I::MJ];
+  for (int j = 0; j < I::MJ; ++j)
+#pragma unroll
+    for (int n = 0; n < I::NT; ++n) wacc[j][n] = zero4();
+  bf16x8 bfr[I::NT], afr[I::MJ];
   frags(0, bfr, afr);
   for (int s_ = 0; s_ < I::KSTEPS; ++s_) {
-    bf16x8 bn, an[I::MJ];
+    bf16x8 bn[I::NT], an[I::MJ];
     wait_lds();
     __builtin_amdgcn_sched_barrier(0);
     if (s_ + 1 < I::KSTEPS) frags(s_ + 1, bn, an);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < I::MJ; ++j)
-      if (mok[j]) wacc[j] = mfma16(afr[j], bfr, wacc[j]);
-    bfr = bn;
+      if (mok[j]) {
+#pragma unroll
+        for (int n = 0; n < I::NT; ++n) wacc[j][n] = mfma16(afr[j], bfr[n], wacc[j][n]);
+      }
+#pragma unroll
+    for (int n = 0; n < I::NT; ++n) bfr[n] = bn[n];
 #pragma unroll
     for (int j = 0; j < I::MJ; ++j) afr[j] = an[j];
   }
@@ -979,7 +989,9 @@ __global__ __launch_bounds__(RT, 2) void k_rn_bwd_img(DmlcRnDgradArgs a, DmlcRnW
     const int m = w + 4 * j;
     if (mok[j]) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) st_maybe_nt<kNtRn>(out + (16 * m + 4 * g + i) * COUT + li, wacc[j][i]);
+      for (int n = 0; n < I::NT; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st_maybe_nt<kNtRn>(out + (16 * m + 4 * g + i) * COUT + 16 * n + li, wacc[j][n][i]);
     }
   }
 }
@@ -1332,11 +1344,12 @@ hipError_t launch_bwd(const DmlcRnDgradArgs& d, const DmlcRnWgradArgs& w, hipStr
   }
 }
 
+template <int C, int H>
 hipError_t launch_bwd_img(const DmlcRnDgradArgs& d, const DmlcRnWgradArgs& w, hipStream_t s) {
-  using I = BwdImg<16, 16, 32>;
+  using I = BwdImg<C, C, H>;
   if (w.G != d.B) return hipErrorInvalidValue;   // one slab per image
-  DMLC_LDS_OPTIN((&k_rn_bwd_img<16, 16, 32>), I::LDS);
-  hipLaunchKernelGGL((k_rn_bwd_img<16, 16, 32>), dim3(d.B), dim3(RT), I::LDS, s, d, w);
+  DMLC_LDS_OPTIN((&k_rn_bwd_img<C, C, H>), I::LDS);
+  hipLaunchKernelGGL((k_rn_bwd_img<C, C, H>), dim3(d.B), dim3(RT), I::LDS, s, d, w);
   return hipGetLastError();
 }
 
@@ -1379,7 +1392,8 @@ hipError_t dmlc_rn_wgrad(const DmlcRnLayerGeom* g, const DmlcRnWgradArgs* a, hip
 hipError_t dmlc_rn_bwd(const DmlcRnLayerGeom* g, const DmlcRnDgradArgs* d, const DmlcRnWgradArgs* w, hipStream_t s) {
   if (d->B != w->B) return hipErrorInvalidValue;
   if (g->per_image) {                              // one workgroup per image: dgrad + wgrad
-    if (g->cin == 16 && g->cout == 16 && g->hin == 32 && g->stride == 1) return launch_bwd_img(*d, *w, s);
+    if (g->cin == 16 && g->cout == 16 && g->hin == 32 && g->stride == 1) return launch_bwd_img<16, 32>(*d, *w, s);
+    if (g->cin == 32 && g->cout == 32 && g->hin == 16 && g->stride == 1) return launch_bwd_img<32, 16>(*d, *w, s);
     return hipErrorInvalidValue;
   }
 #define X(CI, CO, H, ST) \

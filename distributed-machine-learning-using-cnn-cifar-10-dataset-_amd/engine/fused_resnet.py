@@ -176,7 +176,12 @@ class FusedResNetEngine:
         det = (lambda k, l: self.det[k][l]) if self.deterministic else (lambda k, l: None)
         self._det_stat = [det(0, l) for l in range(NL)]
         self._det_red = [det(1, l) for l in range(NL)]
-        self.groups = groups or [self._pick_groups(B, ci, co) for _, ci, co, _, _ in LAYERS]
+        # per-image backward (k_rn_bwd_img, merged backward only): DMLC_RN_BWD_IMG = 0 off, 1 the 16->16
+        # layers (their wgrad keeps one slab per image anyway), 2 also the 32->32 stride-1 layers (one
+        # slab per image instead of B/2 groups: more slab bytes for the SGD, fewer re-reads)
+        self.bwd_img_level = int(os.environ.get("DMLC_RN_BWD_IMG", "1") or 0)
+        self.groups = groups or [B if (self.bwd_img_level >= 2 and B <= 256 and (ci, co, h, s) == (32, 32, 16, 1))
+                                 else self._pick_groups(B, ci, co) for _, ci, co, h, s in LAYERS]
         self.part = [z(g, _kp(ci), co, dt=torch.float32) for g, (_, ci, co, _, _) in zip(self.groups, LAYERS)]
         self.fc_part = z(B, 656, dt=torch.float32)
         self.loss_img = z(B, dt=torch.float32)
@@ -209,7 +214,6 @@ class FusedResNetEngine:
             wgrad_branch = os.environ.get("DMLC_RN_WGRAD_BRANCH", "1" if B > 256 else "0") == "1"
         self.wgrad_branch = wgrad_branch
         self.merged_bwd = os.environ.get("DMLC_RN_MERGED_BWD", "1" if B <= 256 else "0") == "1"
-        self.bwd_img = os.environ.get("DMLC_RN_BWD_IMG", "1") != "0"
         # DMLC_RN_SGD_SPLIT=1 (single GPU, merged backward): the SGD of stage 3 (layers 13-18) and of
         # stage 2 (7-12) runs on a graph branch as soon as their weight gradients are complete, beside
         # the stage-2 / stage-1 backward; the main-stream SGD does the rest and publishes the step.
@@ -280,7 +284,8 @@ class FusedResNetEngine:
         layers whose weight gradient already keeps one split-K slab per image (G == B, B <= 256).
         DMLC_RN_BWD_IMG=0: the merged launch with separate wgrad blocks."""
         _, ci, co, h, s = LAYERS[l]
-        return (self.bwd_img and (ci, co, h, s) == (16, 16, 32, 1) and self.part[l].shape[0] == self.B)
+        lvl = {(16, 16, 32, 1): 1, (32, 32, 16, 1): 2}.get((ci, co, h, s))
+        return bool(lvl and self.bwd_img_level >= lvl and self.part[l].shape[0] == self.B)
 
     def _wgrad(self, l):
         _, ci, co, h, s = LAYERS[l]

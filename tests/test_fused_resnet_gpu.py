@@ -295,17 +295,20 @@ def test_any_batch_size_masked_tail(B):
     assert _rel(eng.state.cpu(), st_ref) < 2e-2
 
 
-@pytest.mark.parametrize("B", [32, 256])
-def test_per_image_backward_is_bit_identical(B, monkeypatch):
-    """The 16->16 layers' dgrad + wgrad from one workgroup per image (k_rn_bwd_img: the staged g_z and
-    layer input serve both, one weight-gradient slab per image) train exactly like the merged launch
-    with separate wgrad blocks (DMLC_RN_BWD_IMG=0): the same per-image sums in the same k-step order,
-    so parameters, BN state and stats agree bit for bit after eager and graph-replayed steps."""
+@pytest.mark.parametrize("B,level", [(32, 1), (256, 1), (64, 2), (256, 2)])
+def test_per_image_backward_is_bit_identical(B, level, monkeypatch):
+    """The stride-1 layers' dgrad + wgrad from one workgroup per image (k_rn_bwd_img: the staged g_z and
+    layer input serve both, one weight-gradient slab per image; level 1: the 16->16 layers, level 2:
+    also the 32->32 ones) train exactly like the merged launch with separate wgrad blocks over the
+    same slabs (DMLC_RN_BWD_IMG=0): the same per-image sums in the same k-step order, so parameters,
+    BN state and stats agree bit for bit after eager and graph-replayed steps."""
     data, labels = _data(4 * B, seed=31)
+    monkeypatch.setenv("DMLC_RN_BWD_IMG", str(level))
     img = FusedResNetEngine(B, data, labels, seed=30)
-    assert any(img._per_image(l) for l in range(1, 7))
+    assert all(img._per_image(l) for l in range(1, 7))
+    assert all(img._per_image(l) for l in (8, 9, 10, 11, 12)) == (level == 2)
     monkeypatch.setenv("DMLC_RN_BWD_IMG", "0")
-    ref = FusedResNetEngine(B, data, labels, seed=30)
+    ref = FusedResNetEngine(B, data, labels, seed=30, groups=list(img.groups))
     assert not any(ref._per_image(l) for l in range(1, 7))
     for eng in (ref, img):
         eng.step()
