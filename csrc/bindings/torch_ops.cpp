@@ -284,10 +284,11 @@ void conv2_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const
   CHECK_HIP(dmlc_conv2_wgrad(&a, stream_of(p1)));
 }
 
-void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
-           int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
-           const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2,
-           const c10::optional<Tensor>& xraw, bool with_conv1) {
+static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter,
+                                int64_t period, int64_t cy, int64_t cx, const Tensor& dp1, const Tensor& am1,
+                                const Tensor& part1, const Tensor& partb1, const Tensor& p1, const Tensor& dy2,
+                                const Tensor& part2, const Tensor& partb2, int64_t groups2,
+                                const c10::optional<Tensor>& xraw, bool with_conv1) {
   const int64_t B = p1.size(0), g1 = with_conv1 ? part1.size(0) : 0, g2 = groups2;
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
@@ -304,7 +305,6 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
   const int p2b = check_part2(part2, g2);
   check(partb2, "partb2", at::kFloat, {g2, 64});
-  c10::DeviceGuard guard(dp1.device());
   DmlcWgradArgs a;
   a.w1.data = data.data_ptr<uint8_t>(); a.w1.src = index_src(idx, counter, period, B);
   check_order_fits(a.w1.src, data.size(0));
@@ -314,6 +314,18 @@ void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& c
   a.w1.xraw = xraw_ptr(xraw, B);
   a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr(); a.w2.part2_bf16 = p2b;
   a.w2.partb2 = partb2.data_ptr<float>(); a.w2.g2 = (int)g2; a.w2.B = (int)B;
+  a.apply = 0; a.bar = nullptr;
+  memset(&a.sgd, 0, sizeof(a.sgd));
+  return a;
+}
+
+void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
+           int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
+           const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2,
+           const c10::optional<Tensor>& xraw, bool with_conv1) {
+  DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
+                               groups2, xraw, with_conv1);
+  c10::DeviceGuard guard(dp1.device());
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
 }
 
@@ -453,7 +465,7 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
   CHECK_HIP(dmlc_head(&a, stream_of(h1part)));
 }
 
-void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_scale, at::IntArrayRef off,
+static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_scale, at::IntArrayRef off,
          const Tensor& part1, const Tensor& partb1, const Tensor& part2, const Tensor& partb2, const Tensor& w1f,
          const Tensor& w2f, const Tensor& w2d, const Tensor& fc1n, const Tensor& fc2t, const Tensor& fc2n,
          const Tensor& fc3t, const Tensor& fc3d, const Tensor& step, double lr0, double decay, double decay_steps,
@@ -497,7 +509,6 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
                   loss_part.numel() == correct_part.numel(), "loss/correct partials mismatch");
   dev(stats, "stats");
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(1) == 4, "stats must be [R,4] fp32");
-  c10::DeviceGuard guard(master.device());
   DmlcSgdArgs a;
   a.master = master.data_ptr<float>(); a.grad = grad.data_ptr<float>();
   a.mode = (int)mode; a.grad_scale = (float)grad_scale;
@@ -545,7 +556,47 @@ void sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_sca
     TORCH_CHECK(a.next.idx_base == nullptr, "sgd: order must be the host descriptor");
     a.bidx = bidx->data_ptr<int>(); a.bidx_n = (int)bidx->numel();
   }
+  return a;
+}
+
+#define DMLC_SGD_PARAMS                                                                                  \
+  const Tensor &master, const Tensor &grad, int64_t mode, double grad_scale, at::IntArrayRef off,          \
+      const Tensor &part1, const Tensor &partb1, const Tensor &part2, const Tensor &partb2, const Tensor &w1f, \
+      const Tensor &w2f, const Tensor &w2d, const Tensor &fc1n, const Tensor &fc2t, const Tensor &fc2n,     \
+      const Tensor &fc3t, const Tensor &fc3d, const Tensor &step, double lr0, double decay, double decay_steps, \
+      bool staircase, const Tensor &ticket, const Tensor &loss_part, const Tensor &correct_part,            \
+      const Tensor &stats, const c10::optional<Tensor> &w2f8, const c10::optional<Tensor> &amax_w,          \
+      const c10::optional<Tensor> &scale_w, int64_t roles, bool finalize, int64_t batch,                    \
+      const c10::optional<Tensor> &bidx, const c10::optional<Tensor> &order, double warmup, bool fc1_fused,  \
+      const c10::optional<Tensor> &step_rd
+#define DMLC_SGD_ARGS                                                                                     \
+  master, grad, mode, grad_scale, off, part1, partb1, part2, partb2, w1f, w2f, w2d, fc1n, fc2t, fc2n, fc3t, fc3d, \
+      step, lr0, decay, decay_steps, staircase, ticket, loss_part, correct_part, stats, w2f8, amax_w, scale_w,  \
+      roles, finalize, batch, bidx, order, warmup, fc1_fused, step_rd
+
+void sgd(DMLC_SGD_PARAMS) {
+  DmlcSgdArgs a = make_sgd(DMLC_SGD_ARGS);
+  c10::DeviceGuard guard(master.device());
   CHECK_HIP(dmlc_sgd(&a, stream_of(master)));
+}
+
+// Single GPU: the weight gradients AND the whole SGD step in one launch (cnn_wgrad.hip apply mode).
+// The wgrad arguments come first (data .. xraw), then the barrier words, then sgd()'s arguments
+// (whose slab tensors must be the wgrad's).
+void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
+               int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& p1, const Tensor& dy2,
+               int64_t groups2, const Tensor& xraw, const Tensor& bar, DMLC_SGD_PARAMS) {
+  DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
+                               groups2, xraw, true);
+  TORCH_CHECK(mode == 0 && fc1_fused && step_rd.has_value() && !w2f8.has_value() && roles == 0 && finalize &&
+                  grad_scale == 1.0,
+              "wgrad_sgd: single-GPU mode-0 step with the fc1 epilogue and the head's step copy only");
+  check_numel(bar, "bar", at::kInt, DMLC_WBAR_WORDS);
+  a.sgd = make_sgd(DMLC_SGD_ARGS);
+  a.apply = 1;
+  a.bar = reinterpret_cast<unsigned int*>(bar.data_ptr<int>());
+  c10::DeviceGuard guard(dp1.device());
+  CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
 }
 
 }  // namespace
@@ -580,6 +631,15 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
         "Tensor(a!) h1, Tensor(b!) h2, Tensor(c!) dl, Tensor(d!) dh1, Tensor(e!) dh2, Tensor(f!) loss_part, "
         "Tensor(g!) correct_part, Tensor(h!)? logits_out, int nvalid=-1, Tensor? step=None, Tensor(i!)? step_copy=None) -> ()");
+  m.def("wgrad_sgd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
+        "Tensor p1, Tensor dy2, int groups2, Tensor xraw, Tensor(z!) bar, "
+        "Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor(r!) part1, Tensor(s!) partb1, "
+        "Tensor(t!) part2, Tensor(u!) partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
+        "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
+        "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
+        "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
+        "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
+        "bool fc1_fused=False, Tensor? step_rd=None) -> ()");
   m.def("sgd(Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor part1, Tensor partb1, "
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
@@ -607,4 +667,5 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("gemm_grouped", &gemm_grouped);
   m.impl("head", &head);
   m.impl("sgd", &sgd);
+  m.impl("wgrad_sgd", &wgrad_sgd);
 }

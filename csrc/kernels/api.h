@@ -118,11 +118,6 @@ struct DmlcConv2WgradArgs {
   int part2_bf16;           // slabs stored as bf16 (partial sums of g2-th of the batch, rounded once)
 };
 
-// Both weight gradients in one launch (blocks [0,g1): conv1; then 4 * g2 conv2 blocks, one slab per group).
-struct DmlcWgradArgs {
-  DmlcConv1WgradArgs w1;
-  DmlcConv2WgradArgs w2;
-};
 
 // Grouped bf16 GEMM: up to 8 independent problems in one launch, 64x64 tiles, MFMA 16x16x32.
 //   a_kmajor=1: A(m,k) = A[m*lda + k]; 0: A(m,k) = A[k*lda + m]
@@ -222,6 +217,21 @@ struct DmlcSgdArgs {
   // 0/2 write fc1n[(s+1) & 1], mode 3 fc1n[s & 1].  fc1_fused (mode 0): the fc1 WEIGHT update already
   // ran in the dW1 GEMM's epilogue (c_mode 4) -- the fc1 role covers the fc1 bias only
   int fc1_fused;
+};
+
+// Both weight gradients in one launch (blocks [0,g1): conv1; then 4 * g2 conv2 blocks, one slab per group).
+// apply = 1 (single GPU, cnn_wgrad.hip): the launch also finishes the step -- the blocks of each
+// slab family meet at a sub-grid barrier (bar: DMLC_WBAR_WORDS zeroed uints), reduce their share of
+// the slabs in the SGD kernel's order and apply the update (sgd: mode 0, fc1_fused, step_rd = the
+// head's step copy); the conv1 blocks also run the fc roles, publish the stats and bump global_step.
+// No SGD launch follows.  bar[10 * 32] is a sticky error word (a barrier that timed out).
+#define DMLC_WBAR_WORDS (11 * 32)
+struct DmlcWgradArgs {
+  DmlcConv1WgradArgs w1;
+  DmlcConv2WgradArgs w2;
+  int apply;
+  unsigned int* bar;
+  DmlcSgdArgs sgd;
 };
 
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);

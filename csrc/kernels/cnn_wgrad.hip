@@ -15,6 +15,7 @@
 //     tiles (12 accumulators) and waves 0-3 also tap 24 x co tile w: 25 MFMAs per k-step on every SIMD.
 // Both: the NEXT image's global data is prefetched into registers while the current image computes.
 #include "w1_common.h"
+#include "sgd_common.h"
 
 namespace dmlc {
 
@@ -23,7 +24,7 @@ namespace dmlc {
 constexpr size_t W1_LDS = (size_t)(W1_DYT + W1_XS + 9216) * 2 + 3072 + 9216;
 static_assert(W1_FL_BYTES <= (W1_DYT + W1_XS) * 2, "flush buffer over dY1 + planes");
 
-DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* smem) {
+DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* smem, bool coh = false) {
   bf16* dyt = reinterpret_cast<bf16*>(smem);
   bf16* xs = dyt + W1_DYT;
   bf16* dps = xs + W1_XS;
@@ -89,7 +90,7 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
   }
   __syncthreads();
   DMLC_STAMP(DMLC_TK_W1, 3);
-  w1_flush(smem, acc, a.part1 + (size_t)grp * 80 * 64, a.partb1 + grp * 64, ks, ch, lane, tid);
+  w1_flush(smem, acc, a.part1 + (size_t)grp * 80 * 64, a.partb1 + grp * 64, ks, ch, lane, tid, coh);
   DMLC_STAMP(DMLC_TK_W1, 4);
 }
 
@@ -118,13 +119,21 @@ constexpr size_t W2_LDS = W2_LDS_MAIN > W2_LDS_ST ? W2_LDS_MAIN : W2_LDS_ST;
 // group sit on one XCD (blockIdx % 8), the one whose dgrad / forward blocks wrote the group's dY2 and
 // input (placement is a speed matter only).  (Double-buffering the image operands in LDS, with or
 // without reading k-step s+1's fragments under k-step s's MFMAs, measured 0.3-1 us slower.)
-DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int base, char* smem) {
+DEV void w2_block_pos(const DmlcConv2WgradArgs& a, int blk, int base, int& c4, int& grp) {
+  const bool xcd = a.g2 % 8 == 0 && base % 8 == 0;
+  c4 = xcd ? (blk >> 3) & 3 : blk & 3;
+  grp = xcd ? (blk & 7) + 8 * (blk >> 5) : blk >> 2;
+}
+
+// coh: the slabs and bias partials are reduced by other blocks of the same launch (apply mode):
+// agent-coherent stores instead of streaming ones
+DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int base, char* smem, bool coh = false) {
   bf16* xt = reinterpret_cast<bf16*>(smem);
   bf16* dyt = xt + W2_XT;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-  const bool xcd = a.g2 % 8 == 0 && base % 8 == 0;
-  const int c4 = xcd ? (blk >> 3) & 3 : blk & 3, grp = xcd ? (blk & 7) + 8 * (blk >> 5) : blk >> 2;
+  int c4, grp;
+  w2_block_pos(a, blk, base, c4, grp);
   const int G = a.g2, b0 = grp, last = grp < a.B ? grp + (a.B - 1 - grp) / G * G : grp;
   DMLC_STAMP(DMLC_TK_W2, 0);
 
@@ -209,11 +218,13 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
   // boundary writes back from L2; each element is a partial sum over G-th of the batch, rounded once)
   const size_t slab0 = (size_t)grp * 1600 * 64;
   auto put4 = [&](size_t e, const f32x4& v) {
-    if (a.part2_bf16) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.part2) + slab0 + e) = pack4(v[0], v[1], v[2], v[3]);
+    if (coh) st_sc1(reinterpret_cast<float*>(a.part2) + slab0 + e, v);
+    else if (a.part2_bf16) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.part2) + slab0 + e) = pack4(v[0], v[1], v[2], v[3]);
     else st_maybe_nt<kNtDefault>(reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.part2) + slab0 + e), v);
   };
   auto put1 = [&](size_t e, float v) {
-    if (a.part2_bf16) reinterpret_cast<bf16*>(a.part2)[slab0 + e] = (bf16)v;
+    if (coh) st_sc1(reinterpret_cast<float*>(a.part2) + slab0 + e, v);
+    else if (a.part2_bf16) reinterpret_cast<bf16*>(a.part2)[slab0 + e] = (bf16)v;
     else reinterpret_cast<float*>(a.part2)[slab0 + e] = v;
   };
   __syncthreads();                             // every MFMA read of LDS is done: reuse it for staging
@@ -225,7 +236,8 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
       float sb = 0.f;
 #pragma unroll
       for (int k = 0; k < W2T / 64; ++k) sb += red[k * 64 + tid];
-      a.partb2[grp * 64 + tid] = sb;
+      if (coh) st_sc1(a.partb2 + grp * 64 + tid, sb);
+      else a.partb2[grp * 64 + tid] = sb;
     }
     __syncthreads();
   }
@@ -259,14 +271,151 @@ __global__ __launch_bounds__(W2T, 1) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
   conv2_wgrad_block(a, blockIdx.x, 0, smem);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Single-GPU apply mode (DmlcWgradArgs::apply): the step's SGD runs inside this launch and no SGD
+// launch follows (saves its ~7 us and the ~1.5 us dependent-launch gap).  Each slab family meets at a
+// sub-grid barrier once its coherent slab stores are acknowledged -- the 32 conv2 blocks of an
+// input-channel quarter, the g1 conv1 blocks -- and every block then reduces ITS share of the family's
+// outputs in exactly the SGD kernel's order (split_sum: split sp sums slabs sp, sp+S, ... and the S
+// partials are added in fixed order), so the weights are bit-identical to the two-launch path.
+// Deadlock freedom: conv1 blocks (lowest ids, dispatched first) only wait for conv1 blocks, conv2
+// blocks for the blocks of their quarter; one block per CU and g1, 4 * g2 <= the CU count (host
+// check) -- if the chip cannot hold every block, the conv1 family still completes and frees CUs.
+DEV unsigned* wbar(unsigned* b, int k) { return b + 32 * k; }
+
+// conv2: block (c4, grp) reduces float4 outputs [grp*per, grp*per+per) of quarter c4 (25 taps x 16 ci
+// x 16 co-float4 = 6400), two threads per output (splits {0,1} and {2,3} of the 4), + shadows.
+DEV void conv2_apply(const DmlcWgradArgs& A, int c4, int grp, char* smem, unsigned g0, int64_t step) {
+  const DmlcSgdArgs& s = A.sgd;
+  const int tid = threadIdx.x, h = tid & 1, n = A.w2.g2;
+  wait_vm_all();                               // this thread's coherent slab stores are acknowledged
+  __syncthreads();
+  if (tid == 0) {
+    bar_arrive(wbar(A.bar, 2 + c4), wbar(A.bar, 6 + c4), g0, (unsigned)n);
+    bar_wait(wbar(A.bar, 6 + c4), g0, wbar(A.bar, 10));
+  }
+  __syncthreads();
+  DMLC_STAMP(DMLC_TK_W2, 6);
+  const float lr = lr_of(s, step);
+  const float* part = reinterpret_cast<const float*>(A.w2.part2);
+  const int per = (6400 + n - 1) / n;
+  for (int f0 = 0; f0 < per; f0 += W2T / 2) {
+    const int ol = f0 + (tid >> 1), f = grp * per + ol;
+    const bool ok = ol < per && f < 6400;
+    const int fc = ok ? f : 0;
+    const int krow = (fc >> 8) * 64 + 16 * c4 + ((fc >> 4) & 15), co = 4 * (fc & 15);
+    const size_t e = (size_t)krow * 64 + co;
+    const float4 w0 = *reinterpret_cast<const float4*>(s.master + s.off[2] + e);
+    float4 sj[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int sp = 2 * h + j;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = sp; q < n; q += 8 * C2_SPLIT) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          v[u] = load_sel(reinterpret_cast<const float4*>(part + (size_t)(q + u * C2_SPLIT) * 102400 + e),
+                          reinterpret_cast<const float4*>(part + e), q + u * C2_SPLIT < n);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = add4(acc, v[u]);
+      }
+      sj[j] = acc;
+    }
+    float4 o[2];                               // the partner lane's splits 2, 3
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      o[j] = make_float4(__shfl_xor(sj[j].x, 1), __shfl_xor(sj[j].y, 1), __shfl_xor(sj[j].z, 1), __shfl_xor(sj[j].w, 1));
+    if (h == 0 && ok) {
+      const float4 t = add4(add4(add4(sj[0], sj[1]), o[0]), o[1]);
+      conv2_shadow4(s, krow, co, sgd4(s.master + s.off[2] + e, w0, t, lr, s.grad_scale, true));
+    }
+  }
+  if (c4 == 0 && grp == 0) conv_bias(s, 1, lr, reinterpret_cast<float4*>(smem), tid);
+  DMLC_STAMP(DMLC_TK_W2, 7);
+}
+
+// conv1: arrive, run the slab-independent work (fc roles, stats + global_step, next batch rows),
+// wait, then reduce float4 outputs [grp*per, grp*per+per) of the 75 x 16 (32 splits x 16 outputs
+// per round of 512 threads, the SGD kernel's split_sum<32, 5> order) + shadows; one block: the bias.
+DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, int64_t step) {
+  const DmlcSgdArgs& s = A.sgd;
+  const int tid = threadIdx.x, n = A.w1.g1;
+  float4* lds = reinterpret_cast<float4*>(smem);
+  wait_vm_all();
+  __syncthreads();                             // also: w1_flush's LDS reads are done
+  if (tid == 0) bar_arrive(wbar(A.bar, 0), wbar(A.bar, 1), g0, (unsigned)n);
+  const float lr = lr_of(s, step);
+  const int nfc = fc_role_count(s);
+  for (int r = grp; r < nfc; r += n) {
+    fc_role(s, r, lr, step, lds, tid);
+    lds_barrier();                             // the fc2 transpose tile is reused by the next role
+  }
+  if (grp == 0 && tid < 64) publish_step(s, step, lr, tid);
+  if (s.bidx) {                                // no block of this launch reads bidx (xraw is set)
+    const int r = grp * W1T + tid;
+    if (r < s.bidx_n) s.bidx[r] = order_row(s.next, step + 1, r);
+  }
+  DMLC_STAMP(DMLC_TK_SGD, 0);
+  if (tid == 0) bar_wait(wbar(A.bar, 1), g0, wbar(A.bar, 10));
+  __syncthreads();
+  DMLC_STAMP(DMLC_TK_SGD, 1);
+  const int per = (1200 + n - 1) / n, ol = tid & 15, sp = tid >> 4;
+  for (int f0 = 0; f0 < per; f0 += 16) {
+    const int oo = f0 + ol, o = grp * per + oo;
+    const bool ok = oo < per && o < 1200;
+    const int oc = ok ? o : 0, row = oc >> 4, co = 4 * (oc & 15);   // HWIO row = (kh*5+kw)*3 + ci
+    const int ci = row % 3, khw = row / 3, kh = khw / 5, kw = khw - kh * 5;
+    const float* p = A.w1.part1 + (size_t)(kh * 16 + kw * 3 + ci) * 64 + co;   // slab row k''
+    const size_t e = (size_t)row * 64 + co;
+    const float4 w0 = *reinterpret_cast<const float4*>(s.master + s.off[0] + e);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = sp; q < n; q += C1_LOADS * C1_SPLIT) {
+      float4 v[C1_LOADS];
+#pragma unroll
+      for (int u = 0; u < C1_LOADS; ++u)
+        v[u] = load_sel(reinterpret_cast<const float4*>(p + (size_t)(q + u * C1_SPLIT) * 80 * 64),
+                        reinterpret_cast<const float4*>(p), q + u * C1_SPLIT < n);
+#pragma unroll
+      for (int u = 0; u < C1_LOADS; ++u) acc = add4(acc, v[u]);
+    }
+    lds[tid] = acc;                            // [split sp][output ol]
+    lds_barrier();
+    if (tid < 16 && ok) {
+      float4 t = lds[ol];
+#pragma unroll
+      for (int k = 1; k < C1_SPLIT; ++k) t = add4(t, lds[k * 16 + ol]);
+      conv1_shadow4(s, row, co, sgd4(s.master + s.off[0] + e, w0, t, lr, s.grad_scale, true));
+    }
+    lds_barrier();
+  }
+  if (grp == (n > 1 ? 1 : 0)) conv_bias(s, 0, lr, lds, tid);
+  DMLC_STAMP(DMLC_TK_SGD, 2);
+}
+
 // Both weight gradients in ONE launch (no stream fork/join in the step graph): blocks [0, g1) run
 // the conv1 body, the next 4 * g2 the conv2 body.  One block per CU (LDS): g1 + 4 * g2 <= 256 keeps
 // every block resident in one wave of blocks.
 constexpr size_t WG_LDS = W1_LDS > W2_LDS ? W1_LDS : W2_LDS;
+static_assert(WG_LDS >= SGD_LDS4 * 16, "apply mode reuses the block's LDS for the SGD roles");
 __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if ((int)blockIdx.x < a.w1.g1) conv1_wgrad_block(a.w1, blockIdx.x, smem);
-  else conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, smem);
+  const bool conv1 = (int)blockIdx.x < a.w1.g1;
+  int c4 = 0, grp = 0;
+  if (!conv1) w2_block_pos(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, c4, grp);
+  unsigned g0 = 0;
+  int64_t step = 0;
+  if (a.apply) {                               // read before this block can arrive
+    if (threadIdx.x == 0) g0 = bar_gen(wbar(a.bar, conv1 ? 1 : 6 + c4));
+    step = *a.sgd.step_rd;
+  }
+  if (conv1) {
+    conv1_wgrad_block(a.w1, blockIdx.x, smem, a.apply != 0);
+    if (a.apply) conv1_apply(a, blockIdx.x, smem, g0, step);
+  } else {
+    conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, smem, a.apply != 0);
+    if (a.apply) conv2_apply(a, c4, grp, smem, g0, step);
+  }
 }
 static_assert(W1T == W2T, "k_wgrad runs both bodies with one block size");
 
@@ -290,6 +439,22 @@ hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s) {
 hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s) {
   DMLC_LDS_OPTIN(&k_wgrad, WG_LDS);
   const int blocks = a->w1.g1 + 4 * a->w2.g2;
+  if (a->apply) {
+    // every barrier family must fit on the chip at once (one block per CU), fp32 slabs, the step
+    // read from the head's copy (a block bumps *step while others may not have read it yet), and
+    // the forward's image copy (bidx is rewritten for the next step inside this launch)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return hipErrorInvalidValue;
+    }
+    const DmlcSgdArgs& g = a->sgd;
+    if (a->w1.g1 < 1 || a->w1.g1 > cus || 4 * a->w2.g2 > cus || a->w2.part2_bf16 || !a->bar || !a->w1.xraw ||
+        g.step_rd == g.step || g.mode != 0 || !g.fc1_fused || g.w2f8 || g.part1 != a->w1.part1 ||
+        g.part2 != a->w2.part2 || g.g1 != a->w1.g1 || g.g2 != a->w2.g2 || g.bidx_n > a->w1.g1 * W1T)
+      return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL(k_wgrad, dim3(blocks), dim3(W1T), WG_LDS, s, *a);
   return hipGetLastError();
 }

@@ -121,6 +121,38 @@ constexpr bool kNtW1 = kNtDefault;
 constexpr bool kNtDg = kNtDefault;
 constexpr bool kNtGemm = kNtDefault;
 
+// Agent-coherent stores (sc1: written through this XCD's L2, so once the store is acknowledged --
+// s_waitcnt vmcnt(0) -- every XCD reads the value).  For data that OTHER blocks of the same launch
+// read after a sub-grid barrier; readers never touched those lines earlier in the launch, and the
+// launch-start acquire dropped older copies from their L2, so plain loads see the new values.
+DEV void st_sc1(float* p, const f32x4& v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+DEV void st_sc1(float* p, float v) { asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory"); }
+DEV void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // s_waitcnt vmcnt(0)
+
+// Sub-grid barrier among the n co-resident blocks sharing (cnt, gen) (each on its own 128-B line,
+// zero-initialised; they re-arm themselves).  Thread 0 reads the generation BEFORE its block can
+// arrive (bar_gen), arrives once the block's coherent stores are acknowledged (bar_arrive) and spins
+// (bar_wait).  The spin is bounded: a block that is never scheduled (co-residency violated) sets the
+// sticky error word instead of hanging the GPU.
+DEV unsigned bar_gen(unsigned* gen) { return __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV void bar_arrive(unsigned* cnt, unsigned* gen, unsigned g0, unsigned n) {
+  if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1) {
+    __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(gen, g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+DEV void bar_wait(unsigned* gen, unsigned g0, unsigned* err) {
+  for (unsigned it = 0; bar_gen(gen) == g0; ++it) {
+    if (it > (1u << 20)) {
+      __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

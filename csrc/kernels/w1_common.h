@@ -151,8 +151,9 @@ DEV void w1_mfma(const bf16* dyt, const bf16* xs, f32x4 (&acc)[2][5], int ks, in
 // Cross-wave reduction (fixed order) through `fl` (W1_FL_BYTES of LDS no longer read by anyone), one
 // co-tile half per round, then the fp32 slab out[80 k''][64 co] and the bias-grad row outb[64]
 // (= row 15, the ones plane).  Call after a barrier that retired every wave's MFMA reads of the region.
+// coh: agent-coherent stores (st_sc1) -- the slab is reduced by other blocks of the SAME launch.
 DEV void w1_flush(char* fl_mem, const f32x4 (&acc)[2][5], float* out, float* outb, int ks, int ch, int lane,
-                  int tid) {
+                  int tid, bool coh = false) {
   f32x4* fl = reinterpret_cast<f32x4*>(fl_mem);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -164,8 +165,13 @@ DEV void w1_flush(char* fl_mem, const f32x4 (&acc)[2][5], float* out, float* out
       const f32x4 s = ((fl[e] + fl[640 + e]) + (fl[1280 + e] + fl[1920 + e]));
       const int tile = e >> 6, ln = e & 63, cp = tile / 5, t = tile - cp * 5;
       const int co = 16 * (2 * cp + h) + 4 * (ln >> 4), kk = 16 * t + (ln & 15);
-      st_maybe_nt<kNtW1>(reinterpret_cast<f32x4*>(out + kk * 64 + co), s);
-      if (kk == 15) *reinterpret_cast<f32x4*>(outb + co) = s;
+      if (coh) {
+        st_sc1(out + kk * 64 + co, s);
+        if (kk == 15) st_sc1(outb + co, s);
+      } else {
+        st_maybe_nt<kNtW1>(reinterpret_cast<f32x4*>(out + kk * 64 + co), s);
+        if (kk == 15) *reinterpret_cast<f32x4*>(outb + co) = s;
+      }
     }
   }
 }

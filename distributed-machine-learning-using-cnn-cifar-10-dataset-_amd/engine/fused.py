@@ -62,6 +62,8 @@ def head_rows(B: int) -> int:
     return int(HEAD_ROWS_ENV) if HEAD_ROWS_ENV else (2 if B <= 256 else 4)
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
+# int32 words of the wgrad apply-mode barriers (DMLC_WBAR_WORDS); the last line is the error word
+WBAR_WORDS = 11 * 32
 SEG = {M.short(s.name): s for s in M.PARAM_SPECS}
 
 
@@ -295,6 +297,15 @@ class FusedCifarEngine:
         # Bitwise the same update (same lr expression, same fp32 arithmetic); DMLC_FC1_EPILOGUE=0 off
         self.fc1_epilogue = (not self.dp and not self.fc_branch
                              and os.environ.get("DMLC_FC1_EPILOGUE", "1") != "0")
+        # single GPU + fc1 epilogue: the merged weight-gradient launch also runs the rest of the SGD
+        # (cnn_wgrad.hip apply mode: sub-grid barriers per slab family, the SGD kernel's reduction
+        # order -> bit-identical weights) and the step has no SGD launch.  DMLC_WGRAD_SGD=0 off.
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
+        self.wgrad_apply = (self.fc1_epilogue and self.merged_wgrad and not self.fused_w1 and not self.fp8
+                            and self.w2_slab == "fp32" and not self.sgd_ticket
+                            and 1 <= self.g1 <= cus and 4 * self.g2 <= cus
+                            and os.environ.get("DMLC_WGRAD_SGD", "1") != "0")
+        self.wbar = torch.zeros(WBAR_WORDS, dtype=torch.int32, device=dev)   # barrier words + error word
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
                                                                         s_par=FC1_NUMEL)
@@ -402,9 +413,10 @@ class FusedCifarEngine:
     def _fc_backward(self, fused_sgd: bool = False):
         self._gemm(self._fc_bwd_sgd if fused_sgd else self._fc_bwd, sgd=fused_sgd)
 
-    def _conv_backward(self, src=None):
+    def _conv_backward(self, src=None, apply: bool = False):
         o = self.ops
         idx, counter, period = src or (self.bidx, None, 1)
+        assert not apply or (self.wgrad_apply and src is None), "apply mode: the training step only"
         if self.fused_w1:
             o.conv2_dgrad_w1(self.dp2, self.am2, self.w2d, self.dp1 if self.keep_dp1 else None, self.dy2, self.am1,
                              self.xraw, self.cy, self.cx, self.part1, self.partb1)
@@ -418,6 +430,10 @@ class FusedCifarEngine:
             o.conv2_dgrad_split(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         else:
             o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
+        if apply:
+            o.wgrad_sgd(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1, self.p1, self.dy2,
+                        self.groups2, self.xraw, self.wbar, *self._sgd_args(mode=0, fc1_fused=True))
+            return
         if self.merged_wgrad:
             o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
                     self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw)
@@ -432,14 +448,23 @@ class FusedCifarEngine:
                       self.part1, self.partb1, self.xraw)
         main.wait_stream(self.side_stream)
 
+    def _sgd_args(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True,
+                  fc1_fused: bool = False) -> tuple:
+        return (self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.partb2,
+                self.w1f, self.w2f, self.w2d, self.fc1n, self.fc2t, self.fc2n, self.fc3t, self.fc3d,
+                self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
+                self.loss_part, self.correct_part, self.stats,
+                *((self.w2f8, self.amax_w, self.scale_w) if self.fp8 else (None, None, None)),
+                roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup, fc1_fused,
+                None if mode == 3 or self.sgd_ticket else self.step_sgd)
+
     def _sgd(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True, fc1_fused: bool = False):
-        self.ops.sgd(self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.partb2,
-                     self.w1f, self.w2f, self.w2d, self.fc1n, self.fc2t, self.fc2n, self.fc3t, self.fc3d,
-                     self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
-                     self.loss_part, self.correct_part, self.stats, *((self.w2f8, self.amax_w, self.scale_w)
-                                                                      if self.fp8 else (None, None, None)),
-                     roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup, fc1_fused,
-                     None if mode == 3 or self.sgd_ticket else self.step_sgd)
+        self.ops.sgd(*self._sgd_args(mode, scale, roles, finalize, fc1_fused))
+
+    def check_barriers(self):
+        """Raise if an apply-mode barrier of the wgrad launch timed out (sticky device error word)."""
+        if self.wgrad_apply and int(self.wbar[10 * 32].item()) != 0:
+            raise RuntimeError("wgrad apply mode: a sub-grid barrier timed out (blocks not co-resident)")
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -515,6 +540,9 @@ class FusedCifarEngine:
             if self.fc1_epilogue:
                 self._forward(self.bidx, None, 1, train=True)
                 self._fc_backward(fused_sgd=True)
+                if self.wgrad_apply:                # the SGD runs inside the wgrad launch
+                    self._conv_backward(apply=True)
+                    return
                 self._conv_backward()
                 self._sgd(mode=0, fc1_fused=True)
                 return

@@ -354,3 +354,39 @@ def test_fc1_update_in_gemm_epilogue_is_bit_identical(B, monkeypatch):
     assert torch.equal(fused.fc1n_current(), w1.to(torch.bfloat16))
     assert ref.read_stats(11) == fused.read_stats(11)
     assert torch.equal(ref.forward_logits(idx), fused.forward_logits(idx))
+
+
+@pytest.mark.parametrize("B", [16, 100, 128, 256, 1024])
+def test_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
+    """Single GPU: the merged weight-gradient launch also runs the SGD (cnn_wgrad.hip apply mode:
+    sub-grid barriers per slab family, each block reduces its share of the slabs in the SGD kernel's
+    order, the conv1 blocks run the fc roles / stats / global_step / next batch rows) and the step has
+    no SGD launch.  After eager and graph-replayed steps (a host set_step in between) the parameters,
+    every bf16 shadow, the stats, the step counter and the next batch rows equal the two-launch step
+    bit for bit, and no barrier timed out."""
+    data, labels = _synthetic(8 * B, seed=45)
+    kw = dict(seed=46, lr=1e-4, relu_logits=False)
+    fused = FusedCifarEngine(B, data, labels, **kw)
+    monkeypatch.setenv("DMLC_WGRAD_SGD", "0")
+    ref = FusedCifarEngine(B, data, labels, **kw)
+    assert fused.wgrad_apply and not ref.wgrad_apply
+    idx = torch.arange(min(B, 64), dtype=torch.int32)
+    for eng in (ref, fused):
+        eng.step()
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(5)
+        eng.set_step(eng.global_step() + 3)
+        eng.run(3)
+    torch.cuda.synchronize()
+    fused.check_barriers()
+    assert int(fused.wbar[320]) == 0
+    assert ref.global_step() == fused.global_step() == 13
+    assert torch.isfinite(ref.master).all()
+    assert torch.equal(ref.master, fused.master)
+    for name in ("w1f", "w2f", "w2d", "fc2t", "fc2n", "fc3t", "fc3d", "bidx"):
+        assert torch.equal(getattr(ref, name), getattr(fused, name)), name
+    assert torch.equal(ref.fc1n_current(), fused.fc1n_current())
+    for s in (10, 11, 12, 13):
+        assert ref.read_stats(s) == fused.read_stats(s), s
+    assert torch.equal(ref.forward_logits(idx), fused.forward_logits(idx))
