@@ -314,7 +314,7 @@ static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10
   a.w1.xraw = xraw_ptr(xraw, B);
   a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr(); a.w2.part2_bf16 = p2b;
   a.w2.partb2 = partb2.data_ptr<float>(); a.w2.g2 = (int)g2; a.w2.B = (int)B;
-  a.apply = 0; a.bar = nullptr;
+  a.apply = 0; a.bar = nullptr; a.helpers = 0;
   memset(&a.sgd, 0, sizeof(a.sgd));
   return a;
 }
@@ -595,6 +595,8 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   a.sgd = make_sgd(DMLC_SGD_ARGS);
   a.apply = 1;
   a.bar = reinterpret_cast<unsigned int*>(bar.data_ptr<int>());
+  static const bool helpers = [] { const char* e = getenv("DMLC_WGRAD_HELPERS"); return !(e && e[0] == '0'); }();
+  a.helpers = helpers ? 1 : 0;
   c10::DeviceGuard guard(dp1.device());
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
 }

@@ -224,13 +224,15 @@ struct DmlcSgdArgs {
 // slab family meet at a sub-grid barrier (bar: DMLC_WBAR_WORDS zeroed uints), reduce their share of
 // the slabs in the SGD kernel's order and apply the update (sgd: mode 0, fc1_fused, step_rd = the
 // head's step copy); the conv1 blocks also run the fc roles, publish the stats and bump global_step.
-// No SGD launch follows.  bar[10 * 32] is a sticky error word (a barrier that timed out).
-#define DMLC_WBAR_WORDS (11 * 32)
+// No SGD launch follows.  bar[10 * 32] is a sticky error word (a barrier that timed out); from
+// bar[11 * 32]: one claim word per conv2 slab chunk (the conv1 "helpers", cnn_wgrad.hip).
+#define DMLC_WBAR_WORDS (20 * 32)
 struct DmlcWgradArgs {
   DmlcConv1WgradArgs w1;
   DmlcConv2WgradArgs w2;
   int apply;
   unsigned int* bar;
+  int helpers;              // apply mode: idle conv1 blocks help reduce the conv2 slabs (DMLC_WGRAD_HELPERS=0 off)
   DmlcSgdArgs sgd;
 };
 

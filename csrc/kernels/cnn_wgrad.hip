@@ -218,12 +218,12 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
   // boundary writes back from L2; each element is a partial sum over G-th of the batch, rounded once)
   const size_t slab0 = (size_t)grp * 1600 * 64;
   auto put4 = [&](size_t e, const f32x4& v) {
-    if (coh) st_sc1(reinterpret_cast<float*>(a.part2) + slab0 + e, v);
+    if (coh) st_sc1(buf_rsrc(a.part2), (uint32_t)(slab0 + e) * 4, v);
     else if (a.part2_bf16) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.part2) + slab0 + e) = pack4(v[0], v[1], v[2], v[3]);
     else st_maybe_nt<kNtDefault>(reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.part2) + slab0 + e), v);
   };
   auto put1 = [&](size_t e, float v) {
-    if (coh) st_sc1(reinterpret_cast<float*>(a.part2) + slab0 + e, v);
+    if (coh) st_sc1(buf_rsrc(a.part2), (uint32_t)(slab0 + e) * 4, v);
     else if (a.part2_bf16) reinterpret_cast<bf16*>(a.part2)[slab0 + e] = (bf16)v;
     else reinterpret_cast<float*>(a.part2)[slab0 + e] = v;
   };
@@ -236,7 +236,7 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
       float sb = 0.f;
 #pragma unroll
       for (int k = 0; k < W2T / 64; ++k) sb += red[k * 64 + tid];
-      if (coh) st_sc1(a.partb2 + grp * 64 + tid, sb);
+      if (coh) st_sc1(buf_rsrc(a.partb2), (uint32_t)(grp * 64 + tid) * 4, sb);
       else a.partb2[grp * 64 + tid] = sb;
     }
     __syncthreads();
@@ -283,11 +283,61 @@ __global__ __launch_bounds__(W2T, 1) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
 // check) -- if the chip cannot hold every block, the conv1 family still completes and frees CUs.
 DEV unsigned* wbar(unsigned* b, int k) { return b + 32 * k; }
 
-// conv2: block (c4, grp) reduces float4 outputs [grp*per, grp*per+per) of quarter c4 (25 taps x 16 ci
-// x 16 co-float4 = 6400), two threads per output (splits {0,1} and {2,3} of the 4), + shadows.
+// conv2 slab reduction of quarter c4, float4 outputs [f_begin, f_end) of its 6400 (25 taps x 16 ci
+// x 16 co-float4), four threads per output (split sp = lane & 3 sums slabs sp, sp+4, ...: the SGD
+// kernel's split_sum<4> order, combined ((s0 + s1) + s2) + s3), + SGD + shadows.
+DEV void conv2_reduce(const DmlcWgradArgs& A, int c4, int f_begin, int f_end, float lr) {
+  const DmlcSgdArgs& s = A.sgd;
+  const int tid = threadIdx.x, sp = tid & 3, n = A.w2.g2;
+  const rsrc_t part = buf_rsrc(A.w2.part2);
+  for (int f0 = f_begin; f0 < f_end; f0 += W2T / 4) {
+    const int f = f0 + (tid >> 2);
+    const bool ok = f < f_end;
+    const int fc = ok ? f : f_begin;
+    const int krow = (fc >> 8) * 64 + 16 * c4 + ((fc >> 4) & 15), co = 4 * (fc & 15);
+    const size_t e = (size_t)krow * 64 + co;
+    const float4 w0 = *reinterpret_cast<const float4*>(s.master + s.off[2] + e);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = sp; q < n; q += 8 * C2_SPLIT) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = ld_sc1(part, (uint32_t)((size_t)(q + u * C2_SPLIT < n ? q + u * C2_SPLIT : 0) * 102400 + e) * 4);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = add4(acc, q + u * C2_SPLIT < n ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+    float4 o[3];                               // splits 1..3 from the next three lanes
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      o[j] = make_float4(__shfl_down(acc.x, j + 1), __shfl_down(acc.y, j + 1), __shfl_down(acc.z, j + 1),
+                         __shfl_down(acc.w, j + 1));
+    if (sp == 0 && ok) {
+      const float4 t = add4(add4(add4(acc, o[0]), o[1]), o[2]);
+      conv2_shadow4(s, krow, co, sgd4(s.master + s.off[2] + e, w0, t, lr, s.grad_scale, true));
+    }
+  }
+}
+
+// Chunk of conv2 block (c4, grp): outputs [grp*per, min(grp*per + per, 6400)), per = ceil(6400 / g2).
+// With helpers (g1 >= 4 * g2), conv1 block j -- its conv1 work done ~5 us before the conv2 blocks'
+// -- helps conv2 block j: the chunk's second half goes to whoever CLAIMS it first after observing
+// the quarter's barrier (atomicMax of the new generation into the chunk's claim word: the first
+// caller sees an older value).  A helper that never observes the barrier (it started after it
+// completed) just gives up; the conv2 block then claims and reduces the half itself -- no extra
+// co-residency requirement, no wrong result in any schedule.
+DEV bool w2_helpers(const DmlcWgradArgs& A) { return A.helpers && A.w1.g1 >= 4 * A.w2.g2; }
+DEV void w2_chunk(const DmlcWgradArgs& A, int grp, int& b, int& m, int& e) {
+  const int per = (6400 + A.w2.g2 - 1) / A.w2.g2;
+  b = grp * per;
+  e = min(b + per, 6400);
+  m = w2_helpers(A) ? min(b + (per + 1) / 2, e) : e;
+}
+DEV unsigned* w2_claim(const DmlcWgradArgs& A, int c4, int grp) { return A.bar + 11 * 32 + c4 * A.w2.g2 + grp; }
+
 DEV void conv2_apply(const DmlcWgradArgs& A, int c4, int grp, char* smem, unsigned g0, int64_t step) {
   const DmlcSgdArgs& s = A.sgd;
-  const int tid = threadIdx.x, h = tid & 1, n = A.w2.g2;
+  const int tid = threadIdx.x, n = A.w2.g2;
+  int* flag = reinterpret_cast<int*>(smem);
   wait_vm_all();                               // this thread's coherent slab stores are acknowledged
   __syncthreads();
   if (tid == 0) {
@@ -297,42 +347,39 @@ DEV void conv2_apply(const DmlcWgradArgs& A, int c4, int grp, char* smem, unsign
   __syncthreads();
   DMLC_STAMP(DMLC_TK_W2, 6);
   const float lr = lr_of(s, step);
-  const float* part = reinterpret_cast<const float*>(A.w2.part2);
-  const int per = (6400 + n - 1) / n;
-  for (int f0 = 0; f0 < per; f0 += W2T / 2) {
-    const int ol = f0 + (tid >> 1), f = grp * per + ol;
-    const bool ok = ol < per && f < 6400;
-    const int fc = ok ? f : 0;
-    const int krow = (fc >> 8) * 64 + 16 * c4 + ((fc >> 4) & 15), co = 4 * (fc & 15);
-    const size_t e = (size_t)krow * 64 + co;
-    const float4 w0 = *reinterpret_cast<const float4*>(s.master + s.off[2] + e);
-    float4 sj[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int sp = 2 * h + j;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int q = sp; q < n; q += 8 * C2_SPLIT) {
-        float4 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          v[u] = load_sel(reinterpret_cast<const float4*>(part + (size_t)(q + u * C2_SPLIT) * 102400 + e),
-                          reinterpret_cast<const float4*>(part + e), q + u * C2_SPLIT < n);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = add4(acc, v[u]);
-      }
-      sj[j] = acc;
-    }
-    float4 o[2];                               // the partner lane's splits 2, 3
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      o[j] = make_float4(__shfl_xor(sj[j].x, 1), __shfl_xor(sj[j].y, 1), __shfl_xor(sj[j].z, 1), __shfl_xor(sj[j].w, 1));
-    if (h == 0 && ok) {
-      const float4 t = add4(add4(add4(sj[0], sj[1]), o[0]), o[1]);
-      conv2_shadow4(s, krow, co, sgd4(s.master + s.off[2] + e, w0, t, lr, s.grad_scale, true));
-    }
+  int b, m, e;
+  w2_chunk(A, grp, b, m, e);
+  conv2_reduce(A, c4, b, m, lr);
+  if (m < e) {                                 // the second half: claim it unless the helper did
+    if (tid == 0)
+      flag[0] = __hip_atomic_fetch_max(w2_claim(A, c4, grp), g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g0 + 1u;
+    __syncthreads();
+    if (flag[0]) conv2_reduce(A, c4, m, e, lr);
+    __syncthreads();                           // flag / LDS reused by the bias below
   }
-  if (c4 == 0 && grp == 0) conv_bias(s, 1, lr, reinterpret_cast<float4*>(smem), tid);
+  if (c4 == 0 && grp == 0) conv_bias(s, 1, lr, reinterpret_cast<float4*>(smem), tid, true);
   DMLC_STAMP(DMLC_TK_W2, 7);
+}
+
+// conv1 block j < 4 * g2 helping conv2 block j (after its own work; hg0 = the quarter's generation
+// read at kernel start)
+DEV void conv2_help(const DmlcWgradArgs& A, int j, char* smem, unsigned hg0, int64_t step) {
+  int c4, grp;
+  w2_block_pos(A.w2, j, A.w1.g1, c4, grp);
+  int* flag = reinterpret_cast<int*>(smem);
+  __syncthreads();                             // the conv1 bias role may still read this LDS
+  if (threadIdx.x == 0) {
+    unsigned gen = hg0;
+    for (int it = 0; it < (1 << 12) && (gen = bar_gen(wbar(A.bar, 6 + c4))) == hg0; ++it) __builtin_amdgcn_s_sleep(2);
+    flag[0] = gen != hg0 &&
+              __hip_atomic_fetch_max(w2_claim(A, c4, grp), gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen;
+  }
+  __syncthreads();
+  if (flag[0]) {
+    int b, m, e;
+    w2_chunk(A, grp, b, m, e);
+    conv2_reduce(A, c4, m, e, lr_of(A.sgd, step));
+  }
 }
 
 // conv1: arrive, run the slab-independent work (fc roles, stats + global_step, next batch rows),
@@ -361,12 +408,13 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
   __syncthreads();
   DMLC_STAMP(DMLC_TK_SGD, 1);
   const int per = (1200 + n - 1) / n, ol = tid & 15, sp = tid >> 4;
+  const rsrc_t part1 = buf_rsrc(A.w1.part1);
   for (int f0 = 0; f0 < per; f0 += 16) {
     const int oo = f0 + ol, o = grp * per + oo;
     const bool ok = oo < per && o < 1200;
     const int oc = ok ? o : 0, row = oc >> 4, co = 4 * (oc & 15);   // HWIO row = (kh*5+kw)*3 + ci
     const int ci = row % 3, khw = row / 3, kh = khw / 5, kw = khw - kh * 5;
-    const float* p = A.w1.part1 + (size_t)(kh * 16 + kw * 3 + ci) * 64 + co;   // slab row k''
+    const uint32_t p = (uint32_t)(kh * 16 + kw * 3 + ci) * 64 + co;   // slab row k'' (elements)
     const size_t e = (size_t)row * 64 + co;
     const float4 w0 = *reinterpret_cast<const float4*>(s.master + s.off[0] + e);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -374,10 +422,9 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
       float4 v[C1_LOADS];
 #pragma unroll
       for (int u = 0; u < C1_LOADS; ++u)
-        v[u] = load_sel(reinterpret_cast<const float4*>(p + (size_t)(q + u * C1_SPLIT) * 80 * 64),
-                        reinterpret_cast<const float4*>(p), q + u * C1_SPLIT < n);
+        v[u] = ld_sc1(part1, (p + (uint32_t)(q + u * C1_SPLIT < n ? q + u * C1_SPLIT : 0) * 80 * 64) * 4);
 #pragma unroll
-      for (int u = 0; u < C1_LOADS; ++u) acc = add4(acc, v[u]);
+      for (int u = 0; u < C1_LOADS; ++u) acc = add4(acc, q + u * C1_SPLIT < n ? v[u] : make_float4(0.f, 0.f, 0.f, 0.f));
     }
     lds[tid] = acc;                            // [split sp][output ol]
     lds_barrier();
@@ -389,7 +436,7 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
     }
     lds_barrier();
   }
-  if (grp == (n > 1 ? 1 : 0)) conv_bias(s, 0, lr, lds, tid);
+  if (grp == (n > 1 ? 1 : 0)) conv_bias(s, 0, lr, lds, tid, true);
   DMLC_STAMP(DMLC_TK_SGD, 2);
 }
 
@@ -403,15 +450,22 @@ __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
   const bool conv1 = (int)blockIdx.x < a.w1.g1;
   int c4 = 0, grp = 0;
   if (!conv1) w2_block_pos(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, c4, grp);
-  unsigned g0 = 0;
+  unsigned g0 = 0, hg0 = 0;
   int64_t step = 0;
+  const bool helper = a.apply && conv1 && w2_helpers(a) && (int)blockIdx.x < 4 * a.w2.g2;
   if (a.apply) {                               // read before this block can arrive
     if (threadIdx.x == 0) g0 = bar_gen(wbar(a.bar, conv1 ? 1 : 6 + c4));
+    if (helper && threadIdx.x == 0) {
+      int hc4, hgrp;
+      w2_block_pos(a.w2, blockIdx.x, a.w1.g1, hc4, hgrp);
+      hg0 = bar_gen(wbar(a.bar, 6 + hc4));
+    }
     step = *a.sgd.step_rd;
   }
   if (conv1) {
     conv1_wgrad_block(a.w1, blockIdx.x, smem, a.apply != 0);
     if (a.apply) conv1_apply(a, blockIdx.x, smem, g0, step);
+    if (helper) conv2_help(a, blockIdx.x, smem, hg0, step);
   } else {
     conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, smem, a.apply != 0);
     if (a.apply) conv2_apply(a, c4, grp, smem, g0, step);

@@ -121,14 +121,35 @@ constexpr bool kNtW1 = kNtDefault;
 constexpr bool kNtDg = kNtDefault;
 constexpr bool kNtGemm = kNtDefault;
 
-// Agent-coherent stores (sc1: written through this XCD's L2, so once the store is acknowledged --
-// s_waitcnt vmcnt(0) -- every XCD reads the value).  For data that OTHER blocks of the same launch
-// read after a sub-grid barrier; readers never touched those lines earlier in the launch, and the
-// launch-start acquire dropped older copies from their L2, so plain loads see the new values.
-DEV void st_sc1(float* p, const f32x4& v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+// Agent-coherent (sc1) buffer stores / loads through compiler-visible builtins (aux bit 4 = sc1;
+// inline-asm memory ops are invisible to the compiler's vmcnt accounting: an asm store issued while
+// compiler loads are in flight made it wait too little -- wrong data, seen in r3).  Written through
+// this XCD's L2, so once acknowledged (s_waitcnt vmcnt(0)) every XCD reads the value; sc1 loads read
+// at agent coherence whatever this XCD's L2 holds.  For data OTHER blocks of the same launch read
+// after a sub-grid barrier.  `base` must be wave-uniform (a buffer resource lives in SGPRs), offsets
+// in bytes (< 2 GiB).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+DEV rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
 }
-DEV void st_sc1(float* p, float v) { asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory"); }
+constexpr int kSC1 = 16;
+// (the builtins take / return unsigned data: every value goes through an explicit bit cast -- an
+// implicit float -> uint conversion would convert the VALUE)
+DEV void st_sc1(rsrc_t r, uint32_t off, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, kSC1);
+}
+DEV void st_sc1(rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, kSC1);
+}
+#ifdef DMLC_RED_PLAIN_LOADS
+constexpr int kLdPol = 0;     // A/B variant: plain (non-coherent) reduction loads
+#else
+constexpr int kLdPol = kSC1;
+#endif
+DEV float4 ld_sc1(rsrc_t r, uint32_t off) {
+  const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kLdPol));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
 DEV void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // s_waitcnt vmcnt(0)
 
 // Sub-grid barrier among the n co-resident blocks sharing (cnt, gen) (each on its own 128-B line,

@@ -46,8 +46,11 @@ DEV float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a
 // S splits x (256/S) outputs; split sp sums slabs sp, sp+S, ... with up to U loads in flight, then
 // split 0 adds the S partial sums in fixed order.  Returns the total on split-0 threads (tid < 256/S).
 // Call with every thread of the block (one barrier); lds: >= 256 float4.
+// coh: the slabs were written by other blocks of the SAME launch (agent-coherent sc1 loads from the
+// wave-uniform base `cb`, p = cb + a per-lane offset); otherwise plain loads.
 template <int S, int U = 8>
-DEV float4 split_sum(const float* __restrict__ p, size_t stride, int n, float4* lds, int tid) {
+DEV float4 split_sum(const float* __restrict__ p, size_t stride, int n, float4* lds, int tid, bool coh = false,
+                     const float* cb = nullptr) {
   constexpr int T = 256 / S;
   const int sp = tid / T, idx = tid % T;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -58,8 +61,10 @@ DEV float4 split_sum(const float* __restrict__ p, size_t stride, int n, float4* 
       float4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        v[u] = load_sel(reinterpret_cast<const float4*>(p + (size_t)(q + u * S) * stride),
-                        reinterpret_cast<const float4*>(p), q + u * S < n);
+        v[u] = coh ? (q + u * S < n ? ld_sc1(buf_rsrc(cb), (uint32_t)((p - cb) + (size_t)(q + u * S) * stride) * 4)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f))
+                   : load_sel(reinterpret_cast<const float4*>(p + (size_t)(q + u * S) * stride),
+                              reinterpret_cast<const float4*>(p), q + u * S < n);
 #pragma unroll
       for (int u = 0; u < U; ++u) s = add4(s, v[u]);
     }
@@ -140,13 +145,14 @@ DEV void conv1_shadow4(const DmlcSgdArgs& a, int row, int co, const float4& w) {
 
 // conv biases: which 0 -> conv1 bias (g1 group partials), 1 -> conv2 bias (g2 group partials).
 // Every thread of the block calls (split_sum barrier).
-DEV void conv_bias(const DmlcSgdArgs& a, int which, float lr, float4* lds, int tid) {
+DEV void conv_bias(const DmlcSgdArgs& a, int which, float lr, float4* lds, int tid, bool coh = false) {
   const int c = (tid % 16) * 4;
   const int seg = which == 0 ? 1 : 3;
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f), w0 = g;
   if (a.mode != 1 && tid < 16) w0 = *reinterpret_cast<const float4*>(a.master + a.off[seg] + c);
   if (a.mode == 0 || a.mode == 1)
-    g = split_sum<16>((which == 0 ? a.partb1 : a.partb2) + c, 64, which == 0 ? a.g1 : a.g2, lds, tid);
+    g = split_sum<16>((which == 0 ? a.partb1 : a.partb2) + c, 64, which == 0 ? a.g1 : a.g2, lds, tid, coh,
+                      which == 0 ? a.partb1 : a.partb2);
   if (tid >= 16) return;
   float* gp = a.grad + a.off[seg] + c;
   if (a.mode == 1) { *reinterpret_cast<float4*>(gp) = g; return; }

@@ -166,8 +166,8 @@ DEV void w1_flush(char* fl_mem, const f32x4 (&acc)[2][5], float* out, float* out
       const int tile = e >> 6, ln = e & 63, cp = tile / 5, t = tile - cp * 5;
       const int co = 16 * (2 * cp + h) + 4 * (ln >> 4), kk = 16 * t + (ln & 15);
       if (coh) {
-        st_sc1(out + kk * 64 + co, s);
-        if (kk == 15) st_sc1(outb + co, s);
+        st_sc1(buf_rsrc(out), (uint32_t)(kk * 64 + co) * 4, s);
+        if (kk == 15) st_sc1(buf_rsrc(outb), (uint32_t)co * 4, s);
       } else {
         st_maybe_nt<kNtW1>(reinterpret_cast<f32x4*>(out + kk * 64 + co), s);
         if (kk == 15) *reinterpret_cast<f32x4*>(outb + co) = s;

@@ -1,8 +1,8 @@
 """Fused MI355X training engine for the reference CNN (hand-written HIP kernels + HIP graphs + RCCL).
 
 One training step (= one ``mon_sess.run([train_op, loss])`` of /root/reference/cifar10cnn.py:230,
-SURVEY.md §3.3) is seven kernel launches on the bf16 path (B > 128), all reading their inputs
-from device memory:
+SURVEY.md §3.3) is six kernel launches on the single-GPU bf16 path (B > 128), all reading their
+inputs from device memory:
 
   1 conv12_fwd   uint8 gather + center crop + conv1 + bias + ReLU + pool1 (+argmax), handed through
                  LDS to conv2 + bias + ReLU + pool2 (+argmax) -- one workgroup per image
@@ -12,11 +12,17 @@ from device memory:
   5 conv2_dgrad  pool2/ReLU backward (2x2-ownership gather) + conv2 input-gradient
   6 wgrad        ONE launch, two block roles: pool1/ReLU backward + conv1 weight/bias gradients,
                  and conv2 weight/bias gradients per (input-channel quarter, image group); split-K slabs
-  7 sgd          slab reduction + SGD + LR schedule + bf16 shadow refresh + global_step++ + stats
+                 ... and, on one GPU, the whole SGD (wgrad_apply, cnn_wgrad.hip): each slab family meets
+                 at a sub-grid barrier and every block reduces its share of the slabs in the SGD
+                 kernel's order and applies the update; the conv1 blocks also update fc2/fc3/biases,
+                 publish the stats and bump global_step (the fc1 weights were updated in launch 4's
+                 epilogue)
+  7 sgd          (data parallel, fp8, or DMLC_WGRAD_SGD=0) slab reduction + SGD + LR schedule + bf16
+                 shadow refresh + global_step++ + stats
 
 At B <= 128 (conv_split = 2, cnn_split.hip) launch 1 becomes conv1_fwd_split + conv2_fwd_split and
 launch 5 conv2_dgrad_split (two or four workgroups per image, so a small batch fills the 256 CUs):
-eight launches.  The fp8 path runs conv1 and conv2 forward as two launches.
+seven launches.  The fp8 path runs conv1 and conv2 forward as two launches.
 
 Every data-consuming kernel computes its batch rows from the device-resident global_step and the
 generated epoch order (data/order.py: a keyed Feistel permutation per epoch, no index buffer), so
@@ -63,7 +69,7 @@ def head_rows(B: int) -> int:
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
 # int32 words of the wgrad apply-mode barriers (DMLC_WBAR_WORDS); the last line is the error word
-WBAR_WORDS = 11 * 32
+WBAR_WORDS = 20 * 32
 SEG = {M.short(s.name): s for s in M.PARAM_SPECS}
 
 
