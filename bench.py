@@ -248,6 +248,8 @@ def main():
         assert device_step() == gs0 + args.steps, (device_step(), gs0, args.steps)
     if hasattr(eng, "check_comm"):
         eng.check_comm()
+    if hasattr(eng, "check_barriers"):
+        eng.check_barriers()             # a timed-out wgrad+SGD barrier would make the numbers invalid
     comm = dict(getattr(eng, "comm_info", None) or {})
     comm.update(backend=info.backend if seen > 1 else "none", world_size_seen=seen,
                 device_count=torch.cuda.device_count() if info.device.type == "cuda" else 0, device=str(info.device))

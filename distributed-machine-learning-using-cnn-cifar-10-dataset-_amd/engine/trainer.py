@@ -101,7 +101,15 @@ class _FusedAdapter:
         return self.eng.host_step
 
     def stats(self) -> Dict[str, float]:
-        return self.eng.read_stats(self.eng.host_step)
+        st = self.eng.read_stats(self.eng.host_step)     # (a device sync: the error word is current too)
+        if hasattr(self.eng, "check_barriers"):
+            # a sub-grid barrier of the single-GPU wgrad+SGD launch that timed out (its blocks were not
+            # co-resident) leaves wrong weights: stop loudly, DMLC_WGRAD_SGD=0 selects the SGD launch
+            try:
+                self.eng.check_barriers()
+            except RuntimeError as e:
+                raise RuntimeError(f"{e}; rerun with DMLC_WGRAD_SGD=0") from e
+        return st
 
     def tf_tensors(self) -> Dict[str, torch.Tensor]:
         return CK.model_tensors(self.eng.flat_params(), self.eng.host_step, 0, specs=self.specs)
@@ -427,6 +435,7 @@ class Session:
         # become a CommFailure (exit 75), not a rank blocked forever inside synchronize()
         self._wait_progress(pending)
         eng.sync()
+        eng.stats()                      # also checks the device error words once more
         self._check_replicas()
         self.tracer.close()
         self.save(force=True)            # CheckpointSaverHook.end
