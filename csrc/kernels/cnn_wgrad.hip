@@ -313,7 +313,8 @@ DEV void conv2_reduce(const DmlcWgradArgs& A, int c4, int f_begin, int f_end, fl
                          __shfl_down(acc.w, j + 1));
     if (sp == 0 && ok) {
       const float4 t = add4(add4(add4(acc, o[0]), o[1]), o[2]);
-      conv2_shadow4(s, krow, co, sgd4(s.master + s.off[2] + e, w0, t, lr, s.grad_scale, true));
+      if (s.mode == 1) *reinterpret_cast<float4*>(s.grad + s.off[2] + e) = t;   // reduce only (data parallel)
+      else conv2_shadow4(s, krow, co, sgd4(s.master + s.off[2] + e, w0, t, lr, s.grad_scale, true));
     }
   }
 }
@@ -393,13 +394,13 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
   __syncthreads();                             // also: w1_flush's LDS reads are done
   if (tid == 0) bar_arrive(wbar(A.bar, 0), wbar(A.bar, 1), g0, (unsigned)n);
   const float lr = lr_of(s, step);
-  const int nfc = fc_role_count(s);
+  const int nfc = s.mode == 1 ? 0 : fc_role_count(s);   // reduce-only (data parallel): conv grads only
   for (int r = grp; r < nfc; r += n) {
     fc_role(s, r, lr, step, lds, tid);
     lds_barrier();                             // the fc2 transpose tile is reused by the next role
   }
-  if (grp == 0 && tid < 64) publish_step(s, step, lr, tid);
-  if (s.bidx) {                                // no block of this launch reads bidx (xraw is set)
+  if (s.mode == 0 && grp == 0 && tid < 64) publish_step(s, step, lr, tid);
+  if (s.mode == 0 && s.bidx) {                 // no block of this launch reads bidx (xraw is set)
     const int r = grp * W1T + tid;
     if (r < s.bidx_n) s.bidx[r] = order_row(s.next, step + 1, r);
   }
@@ -432,7 +433,8 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
       float4 t = lds[ol];
 #pragma unroll
       for (int k = 1; k < C1_SPLIT; ++k) t = add4(t, lds[k * 16 + ol]);
-      conv1_shadow4(s, row, co, sgd4(s.master + s.off[0] + e, w0, t, lr, s.grad_scale, true));
+      if (s.mode == 1) *reinterpret_cast<float4*>(s.grad + s.off[0] + e) = t;   // reduce only
+      else conv1_shadow4(s, row, co, sgd4(s.master + s.off[0] + e, w0, t, lr, s.grad_scale, true));
     }
     lds_barrier();
   }
@@ -504,8 +506,10 @@ hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s) {
         return hipErrorInvalidValue;
     }
     const DmlcSgdArgs& g = a->sgd;
+    // mode 1 (data parallel): the reduced conv gradients go to the flat grad (nothing else runs)
+    const bool ok_mode = g.mode == 0 ? (g.step_rd != g.step && g.fc1_fused && !g.w2f8) : g.mode == 1;
     if (a->w1.g1 < 1 || a->w1.g1 > cus || 4 * a->w2.g2 > cus || a->w2.part2_bf16 || !a->bar || !a->w1.xraw ||
-        g.step_rd == g.step || g.mode != 0 || !g.fc1_fused || g.w2f8 || g.part1 != a->w1.part1 ||
+        !ok_mode || g.part1 != a->w1.part1 ||
         g.part2 != a->w2.part2 || g.g1 != a->w1.g1 || g.g2 != a->w2.g2 || g.bidx_n > a->w1.g1 * W1T)
       return hipErrorInvalidValue;
   }

@@ -307,10 +307,18 @@ class FusedCifarEngine:
         # (cnn_wgrad.hip apply mode: sub-grid barriers per slab family, the SGD kernel's reduction
         # order -> bit-identical weights) and the step has no SGD launch.  DMLC_WGRAD_SGD=0 off.
         cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
-        self.wgrad_apply = (self.fc1_epilogue and self.merged_wgrad and not self.fused_w1 and not self.fp8
-                            and self.w2_slab == "fp32" and not self.sgd_ticket
-                            and 1 <= self.g1 <= cus and 4 * self.g2 <= cus
-                            and os.environ.get("DMLC_WGRAD_SGD", "1") != "0")
+        in_launch = (self.merged_wgrad and not self.fused_w1 and self.w2_slab == "fp32"
+                     and 1 <= self.g1 <= cus and 4 * self.g2 <= cus
+                     and os.environ.get("DMLC_WGRAD_SGD", "1") != "0")
+        self.wgrad_apply = in_launch and self.fc1_epilogue and not self.fp8 and not self.sgd_ticket
+        # data parallel: the same launch reduces the conv slabs into the flat gradient (the reduce-only
+        # SGD launch before the all-reduce goes away).  Needs the launch's blocks co-resident, so not
+        # when several ranks share one GPU (rehearsals / tests: another rank's kernels hold CUs).
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
+        ndev = torch.cuda.device_count() if dev.type == "cuda" else 0
+        self.wgrad_reduce = in_launch and self.dp and local <= max(1, ndev)
+        # reduce-only also serves compute_gradients() on one GPU
+        self._grad_in_launch = in_launch and (self.wgrad_apply or self.wgrad_reduce)
         self.wbar = torch.zeros(WBAR_WORDS, dtype=torch.int32, device=dev)   # barrier words + error word
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
@@ -419,10 +427,13 @@ class FusedCifarEngine:
     def _fc_backward(self, fused_sgd: bool = False):
         self._gemm(self._fc_bwd_sgd if fused_sgd else self._fc_bwd, sgd=fused_sgd)
 
-    def _conv_backward(self, src=None, apply: bool = False):
+    def _conv_backward(self, src=None, apply: bool = False, reduce: bool = False):
+        """apply: + the whole SGD in the wgrad launch (single GPU); reduce: + the conv slab reduction
+        into the flat gradient (SGD mode 1) in the wgrad launch."""
         o = self.ops
         idx, counter, period = src or (self.bidx, None, 1)
         assert not apply or (self.wgrad_apply and src is None), "apply mode: the training step only"
+        assert not reduce or self._grad_in_launch
         if self.fused_w1:
             o.conv2_dgrad_w1(self.dp2, self.am2, self.w2d, self.dp1 if self.keep_dp1 else None, self.dy2, self.am1,
                              self.xraw, self.cy, self.cx, self.part1, self.partb1)
@@ -436,9 +447,10 @@ class FusedCifarEngine:
             o.conv2_dgrad_split(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         else:
             o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
-        if apply:
+        if apply or reduce:
             o.wgrad_sgd(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1, self.p1, self.dy2,
-                        self.groups2, self.xraw, self.wbar, *self._sgd_args(mode=0, fc1_fused=True))
+                        self.groups2, self.xraw, self.wbar,
+                        *(self._sgd_args(mode=0, fc1_fused=True) if apply else self._sgd_args(mode=1)))
             return
         if self.merged_wgrad:
             o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
@@ -510,6 +522,9 @@ class FusedCifarEngine:
         self._fc_backward()
 
     def _seg_compute_b(self):
+        if self.dp and self.wgrad_reduce:       # conv slabs reduced inside the wgrad launch
+            self._conv_backward(reduce=True)
+            return
         self._conv_backward()
         self._sgd(mode=1 if self.dp else 0)
 
@@ -529,11 +544,17 @@ class FusedCifarEngine:
         ``idx``: explicit dataset rows (int32 [Bv]) instead of this step's generated batch."""
         if idx is None:
             self._seg_compute_a()
+            if self._grad_in_launch:
+                self._conv_backward(reduce=True)
+                return self.grad
             self._conv_backward()
         else:
             ids = self._padded(idx)
             self._forward(ids, None, 1, train=True)
             self._fc_backward()
+            if self._grad_in_launch:
+                self._conv_backward(src=(ids, None, 1), reduce=True)
+                return self.grad
             self._conv_backward(src=(ids, None, 1))
         self._sgd(mode=1)
         return self.grad

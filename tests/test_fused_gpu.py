@@ -390,3 +390,25 @@ def test_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
     for s in (10, 11, 12, 13):
         assert ref.read_stats(s) == fused.read_stats(s), s
     assert torch.equal(ref.forward_logits(idx), fused.forward_logits(idx))
+
+
+@pytest.mark.parametrize("B", [16, 100, 256])
+def test_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B, monkeypatch):
+    """Data-parallel / compute_gradients path: the merged weight-gradient launch reduces its own conv
+    slabs into the flat gradient (SGD mode 1 inside cnn_wgrad.hip, helpers included) instead of a
+    reduce-only SGD launch.  The whole flat gradient equals the two-launch path bit for bit, for the
+    generated batch and for an explicit index list."""
+    data, labels = _synthetic(8 * B, seed=47)
+    kw = dict(seed=48, lr=1e-4, relu_logits=False)
+    fused = FusedCifarEngine(B, data, labels, **kw)
+    monkeypatch.setenv("DMLC_WGRAD_SGD", "0")
+    ref = FusedCifarEngine(B, data, labels, **kw)
+    assert fused._grad_in_launch and not ref._grad_in_launch
+    idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(3))[:B].to(torch.int32)
+    for explicit in (None, idx):
+        g_ref = ref.compute_gradients(explicit).clone()
+        g_fused = fused.compute_gradients(explicit).clone()
+        torch.cuda.synchronize()
+        assert torch.isfinite(g_ref).all() and float(g_ref.abs().max()) > 0
+        assert torch.equal(g_ref, g_fused)
+    fused.check_barriers()
