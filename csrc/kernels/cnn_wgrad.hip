@@ -371,7 +371,10 @@ DEV void conv2_help(const DmlcWgradArgs& A, int j, char* smem, unsigned hg0, int
   __syncthreads();                             // the conv1 bias role may still read this LDS
   if (threadIdx.x == 0) {
     unsigned gen = hg0;
-    for (int it = 0; it < (1 << 12) && (gen = bar_gen(wbar(A.bar, 6 + c4))) == hg0; ++it) __builtin_amdgcn_s_sleep(2);
+    // a short bound (~64 polls of ~1 us): the conv2 blocks normally pass the barrier ~3 us after the
+    // helper gets here; if they are late (e.g. a concurrent comm kernel holds CUs) the helper leaves
+    // rather than holding its CU, and the conv2 block claims the half itself
+    for (int it = 0; it < 64 && (gen = bar_gen(wbar(A.bar, 6 + c4))) == hg0; ++it) __builtin_amdgcn_s_sleep(2);
     flag[0] = gen != hg0 &&
               __hip_atomic_fetch_max(w2_claim(A, c4, grp), gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen;
   }
