@@ -588,7 +588,7 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
                int64_t groups2, const Tensor& xraw, const Tensor& bar, DMLC_SGD_PARAMS) {
   DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
                                groups2, xraw, true);
-  TORCH_CHECK((mode == 0 && fc1_fused && step_rd.has_value() && !w2f8.has_value() && roles == 0 && finalize &&
+  TORCH_CHECK((mode == 0 && fc1_fused && step_rd.has_value() && roles == 0 && finalize &&
                grad_scale == 1.0) || (mode == 1 && roles == 0),
               "wgrad_sgd: the single-GPU mode-0 step (fc1 epilogue, the head's step copy) or mode 1 (reduce only)");
   check_numel(bar, "bar", at::kInt, DMLC_WBAR_WORDS);

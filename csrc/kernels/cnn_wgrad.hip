@@ -286,9 +286,35 @@ DEV unsigned* wbar(unsigned* b, int k) { return b + 32 * k; }
 // conv2 slab reduction of quarter c4, float4 outputs [f_begin, f_end) of its 6400 (25 taps x 16 ci
 // x 16 co-float4), four threads per output (split sp = lane & 3 sums slabs sp, sp+4, ...: the SGD
 // kernel's split_sum<4> order, combined ((s0 + s1) + s2) + s3), + SGD + shadows.
-DEV void conv2_reduce(const DmlcWgradArgs& A, int c4, int f_begin, int f_end, float lr) {
+// fp8 (w2f8 set): also the e4m3 shadows (forward w2f8 and the dgrad's flipped w2d8) quantised with
+// the delayed scale sw (as the SGD kernel does) and the maximum |w| of this range, stored to
+// amax_w[nxt][slot] (every thread calls: one LDS reduction through red[8]).
+struct W2Fp8 { float sw; int nxt, slot; float* red; };
+DEV float w2_fp8_scale(const DmlcSgdArgs& s, int64_t step) {
+  const float* src = s.amax_w + (size_t)(step & 1) * C2_BLOCKS;
+  float m = 0.f;
+  for (int i = threadIdx.x & 63; i < C2_BLOCKS; i += 64) m = fmaxf(m, src[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  return 224.f / fmaxf(m, 1e-20f);              // the SGD kernel's expression (cnn_sgd.hip conv2_rows)
+}
+DEV void w2_fp8_put(const DmlcWgradArgs& A, int slot, int nxt, float m, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = red[0];
+    for (int k = 1; k < W2T / 64; ++k) t = fmaxf(t, red[k]);
+    A.sgd.amax_w[(size_t)nxt * C2_BLOCKS + slot] = t;
+  }
+  __syncthreads();
+}
+
+DEV void conv2_reduce(const DmlcWgradArgs& A, int c4, int f_begin, int f_end, float lr, const W2Fp8& f8) {
   const DmlcSgdArgs& s = A.sgd;
   const int tid = threadIdx.x, sp = tid & 3, n = A.w2.g2;
+  float wmax = 0.f;
   const rsrc_t part = buf_rsrc(A.w2.part2);
   for (int f0 = f_begin; f0 < f_end; f0 += W2T / 4) {
     const int f = f0 + (tid >> 2);
@@ -313,10 +339,25 @@ DEV void conv2_reduce(const DmlcWgradArgs& A, int c4, int f_begin, int f_end, fl
                          __shfl_down(acc.w, j + 1));
     if (sp == 0 && ok) {
       const float4 t = add4(add4(add4(acc, o[0]), o[1]), o[2]);
-      if (s.mode == 1) *reinterpret_cast<float4*>(s.grad + s.off[2] + e) = t;   // reduce only (data parallel)
-      else conv2_shadow4(s, krow, co, sgd4(s.master + s.off[2] + e, w0, t, lr, s.grad_scale, true));
+      if (s.mode == 1) {
+        *reinterpret_cast<float4*>(s.grad + s.off[2] + e) = t;   // reduce only (data parallel)
+      } else {
+        const float4 w = sgd4(s.master + s.off[2] + e, w0, t, lr, s.grad_scale, true);
+        conv2_shadow4(s, krow, co, w);
+        if (s.w2f8) {
+          const float sw = f8.sw;
+          const uint32_t q = pk_fp8x4(w.x * sw, w.y * sw, w.z * sw, w.w * sw);
+          uint8_t* w8 = s.w2f8 + krow;
+          w8[(co + 0) * 1600] = (uint8_t)q; w8[(co + 1) * 1600] = (uint8_t)(q >> 8);
+          w8[(co + 2) * 1600] = (uint8_t)(q >> 16); w8[(co + 3) * 1600] = (uint8_t)(q >> 24);
+          if (s.w2d8)
+            *reinterpret_cast<uint32_t*>(s.w2d8 + (size_t)(krow & 63) * 1600 + (24 - (krow >> 6)) * 64 + co) = q;
+          wmax = fmaxf(wmax, fmaxf(fmaxf(fabsf(w.x), fabsf(w.y)), fmaxf(fabsf(w.z), fabsf(w.w))));
+        }
+      }
     }
   }
+  if (s.w2f8 && s.mode == 0) w2_fp8_put(A, f8.slot, f8.nxt, wmax, f8.red);
 }
 
 // Chunk of conv2 block (c4, grp): outputs [grp*per, min(grp*per + per, 6400)), per = ceil(6400 / g2).
@@ -350,13 +391,24 @@ DEV void conv2_apply(const DmlcWgradArgs& A, int c4, int grp, char* smem, unsign
   const float lr = lr_of(s, step);
   int b, m, e;
   w2_chunk(A, grp, b, m, e);
-  conv2_reduce(A, c4, b, m, lr);
+  // fp8: amax slots 2k / 2k+1 for the halves of chunk k = c4 * g2 + grp (whoever reduces a half
+  // writes its slot); block (0, 0) also zeroes the unused slots and publishes the scale
+  const int slot = 2 * (c4 * n + grp), nxt = (int)((step & 1) ^ 1);
+  W2Fp8 f8 = {s.w2f8 ? w2_fp8_scale(s, step) : 0.f, nxt, slot, reinterpret_cast<float*>(smem + 64)};
+  if (s.w2f8 && c4 == 0 && grp == 0) {
+    for (int i = 8 * n + tid; i < C2_BLOCKS; i += W2T) s.amax_w[(size_t)nxt * C2_BLOCKS + i] = 0.f;
+    if (tid == 0) { s.scale_w[0] = f8.sw; s.scale_w[1] = f8.sw; }
+  }
+  conv2_reduce(A, c4, b, m, lr, f8);
   if (m < e) {                                 // the second half: claim it unless the helper did
     if (tid == 0)
       flag[0] = __hip_atomic_fetch_max(w2_claim(A, c4, grp), g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g0 + 1u;
     __syncthreads();
-    if (flag[0]) conv2_reduce(A, c4, m, e, lr);
+    f8.slot = slot + 1;
+    if (flag[0]) conv2_reduce(A, c4, m, e, lr, f8);
     __syncthreads();                           // flag / LDS reused by the bias below
+  } else if (s.w2f8 && tid == 0) {
+    s.amax_w[(size_t)nxt * C2_BLOCKS + slot + 1] = 0.f;   // no second half
   }
   if (c4 == 0 && grp == 0) conv_bias(s, 1, lr, reinterpret_cast<float4*>(smem), tid, true);
   DMLC_STAMP(DMLC_TK_W2, 7);
@@ -382,7 +434,9 @@ DEV void conv2_help(const DmlcWgradArgs& A, int j, char* smem, unsigned hg0, int
   if (flag[0]) {
     int b, m, e;
     w2_chunk(A, grp, b, m, e);
-    conv2_reduce(A, c4, m, e, lr_of(A.sgd, step));
+    const W2Fp8 f8 = {A.sgd.w2f8 ? w2_fp8_scale(A.sgd, step) : 0.f, (int)((step & 1) ^ 1),
+                      2 * (c4 * A.w2.g2 + grp) + 1, reinterpret_cast<float*>(smem + 64)};
+    conv2_reduce(A, c4, m, e, lr_of(A.sgd, step), f8);
   }
 }
 
@@ -510,7 +564,9 @@ hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s) {
     }
     const DmlcSgdArgs& g = a->sgd;
     // mode 1 (data parallel): the reduced conv gradients go to the flat grad (nothing else runs)
-    const bool ok_mode = g.mode == 0 ? (g.step_rd != g.step && g.fc1_fused && !g.w2f8) : g.mode == 1;
+    const bool ok_mode = g.mode == 0 ? (g.step_rd != g.step && g.fc1_fused && (!g.w2f8 || (g.amax_w && g.scale_w) ) &&
+                                        8 * a->w2.g2 <= 400)
+                                     : g.mode == 1;
     if (a->w1.g1 < 1 || a->w1.g1 > cus || 4 * a->w2.g2 > cus || a->w2.part2_bf16 || !a->bar || !a->w1.xraw ||
         !ok_mode || g.part1 != a->w1.part1 ||
         g.part2 != a->w2.part2 || g.g1 != a->w1.g1 || g.g2 != a->w2.g2 || g.bidx_n > a->w1.g1 * W1T)

@@ -310,7 +310,10 @@ class FusedCifarEngine:
         in_launch = (self.merged_wgrad and not self.fused_w1 and self.w2_slab == "fp32"
                      and 1 <= self.g1 <= cus and 4 * self.g2 <= cus
                      and os.environ.get("DMLC_WGRAD_SGD", "1") != "0")
-        self.wgrad_apply = in_launch and self.fc1_epilogue and not self.fp8 and not self.sgd_ticket
+        # fp8: bit-identical too (the e4m3 shadows + amax slots in-launch), but measured slower at
+        # B=1024 (207.5 vs 204.7 us, profiles/r3_fp8_wgrad_sgd_ab.txt): opt-in DMLC_WGRAD_SGD_FP8=1
+        self.wgrad_apply = (in_launch and self.fc1_epilogue and not self.sgd_ticket
+                            and (not self.fp8 or os.environ.get("DMLC_WGRAD_SGD_FP8", "0") == "1"))
         # data parallel: the same launch reduces the conv slabs into the flat gradient (the reduce-only
         # SGD launch before the all-reduce goes away).  Needs the launch's blocks co-resident, so not
         # when several ranks share one GPU (rehearsals / tests: another rank's kernels hold CUs).
@@ -318,7 +321,7 @@ class FusedCifarEngine:
         ndev = torch.cuda.device_count() if dev.type == "cuda" else 0
         self.wgrad_reduce = in_launch and self.dp and local <= max(1, ndev)
         # reduce-only also serves compute_gradients() on one GPU
-        self._grad_in_launch = in_launch and (self.wgrad_apply or self.wgrad_reduce)
+        self._grad_in_launch = in_launch and (self.wgrad_apply or self.wgrad_reduce) and not (self.fp8 and not self.wgrad_apply)
         self.wbar = torch.zeros(WBAR_WORDS, dtype=torch.int32, device=dev)   # barrier words + error word
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,

@@ -139,3 +139,32 @@ def test_lr_warmup_and_linear_scaling_on_device():
     torch.cuda.synchronize()
     want = [0.4 * 0.5 ** (s // 3) * (min(s + 1, 4) / 4) for s in range(8)]
     assert [eng.read_stats(s)["lr"] for s in range(1, 9)] == pytest.approx(want, rel=1e-6)
+
+
+@pytest.mark.parametrize("B", [100, 1024])
+def test_fp8_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
+    """fp8 (BASELINE config 5) on one GPU: the SGD inside the wgrad launch also writes the e4m3
+    shadows (forward w2f8, the dgrad's flipped copy) with the delayed per-tensor scale and the new
+    weights' amax slots.  After eager + graph-replayed steps the parameters, both fp8 shadows, the
+    scales and the stats equal the SGD-launch path bit for bit."""
+    data, labels = _synthetic(8 * B, seed=51)
+    kw = dict(seed=52, lr=1e-4, relu_logits=False, dtype="fp8")
+    monkeypatch.setenv("DMLC_WGRAD_SGD_FP8", "1")             # opt-in for fp8 (measured slower)
+    fused = FusedCifarEngine(B, data, labels, **kw)
+    monkeypatch.setenv("DMLC_WGRAD_SGD", "0")
+    ref = FusedCifarEngine(B, data, labels, **kw)
+    assert fused.wgrad_apply and not ref.wgrad_apply and fused.fp8
+    for eng in (ref, fused):
+        eng.step()
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(5)
+    torch.cuda.synchronize()
+    fused.check_barriers()
+    assert ref.global_step() == fused.global_step() == 7
+    assert torch.isfinite(ref.master).all()
+    assert torch.equal(ref.master, fused.master)
+    assert torch.equal(ref.w2f8, fused.w2f8)
+    assert torch.equal(ref.scale_w, fused.scale_w)
+    assert float(ref.amax_w[1].max()) == float(fused.amax_w[1].max())   # step 7: slot 1 holds the new amax
+    assert ref.read_stats(7) == fused.read_stats(7)
