@@ -280,7 +280,10 @@ __global__ __launch_bounds__(W2T, 1) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
 // partials are added in fixed order), so the weights are bit-identical to the two-launch path.
 // Deadlock freedom: conv1 blocks (lowest ids, dispatched first) only wait for conv1 blocks, conv2
 // blocks for the blocks of their quarter; one block per CU and g1, 4 * g2 <= the CU count (host
-// check) -- if the chip cannot hold every block, the conv1 family still completes and frees CUs.
+// check) -- if the chip cannot hold every block, the conv1 family still completes and frees CUs
+// (the conv1 "helpers" of the conv2 reduction only ever join work they saw become ready, w2_chunk).
+// sgd.mode 1 (data parallel, before the all-reduce): the same reductions write the flat gradient
+// instead (the SGD kernel's mode 1); no update, no fc roles, stats or step counter.
 DEV unsigned* wbar(unsigned* b, int k) { return b + 32 * k; }
 
 // conv2 slab reduction of quarter c4, float4 outputs [f_begin, f_end) of its 6400 (25 taps x 16 ci
