@@ -528,6 +528,12 @@ class FusedCifarEngine:
         if self.dp and self.wgrad_reduce:       # conv slabs reduced inside the wgrad launch
             self._conv_backward(reduce=True)
             return
+        self._seg_compute_b_launch()
+
+    def _seg_compute_b_launch(self):
+        """conv backward + the slab reduction as its own SGD launch.  The overlap schedule always uses
+        it: its wgrad launch runs beside comm-stream kernels, so the in-launch sub-grid barriers would
+        not have the co-residency they assume (a wait on another GPU's progress could close a cycle)."""
         self._conv_backward()
         self._sgd(mode=1 if self.dp else 0)
 
@@ -582,7 +588,7 @@ class FusedCifarEngine:
         if self.dp_schedule == "serial":
             self._serial_dp_step([self._seg_compute_ab, self._seg_apply])
             return
-        self._dp_step([self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv])
+        self._dp_step([self._seg_compute_a, self._seg_compute_b_launch, self._seg_apply_fc, self._seg_apply_conv])
 
     def _branched_step(self):
         """Single-GPU step on two graph branches (fc_branch): the fc weight gradients and the fc SGD
@@ -658,7 +664,7 @@ class FusedCifarEngine:
         elif self.dp_schedule == "serial":
             segs = [self._seg_compute_ab, self._seg_apply]
         else:
-            segs = [self._seg_compute_a, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv]
+            segs = [self._seg_compute_a, self._seg_compute_b_launch, self._seg_apply_fc, self._seg_apply_conv]
         self._captured_schedule = self.dp_schedule
         # a capture records launches without running them: the step counter and weights are
         # identical before and after
