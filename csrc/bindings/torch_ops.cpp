@@ -344,6 +344,8 @@ void gemm_grouped(at::TensorList A, at::TensorList Bm, at::TensorList C, const c
   DmlcGemmGroup G;
   memset(&G, 0, sizeof(G));
   G.nprob = n;
+  static const int xcd_map = getenv("DMLC_GEMM_XCD") ? atoi(getenv("DMLC_GEMM_XCD")) : 1;
+  G.xcd_map = xcd_map;
   if (step.has_value()) {
     check_numel(*step, "step", at::kLong, 1);
     G.step = step->data_ptr<int64_t>();

@@ -148,6 +148,10 @@ struct DmlcGemmGroup {
   const int64_t* step;
   float lr0, decay, decay_steps, warmup, grad_scale;
   int staircase;
+  // XCD-aware tile order: every problem's block range is padded to a multiple of 8 and XCD x
+  // (= blockIdx % 8 under round-robin dispatch) takes a contiguous 1/8 of its tiles, so the blocks
+  // that share the larger operand's tiles (or, split-K, one K slice) share an L2 (speed only)
+  int xcd_map;
 };
 
 // MLP head, rows-parallel (rows = 2 or 4 per workgroup; B / rows workgroups): fc1 split-K reduce + bias + ReLU, fc2, fc3,

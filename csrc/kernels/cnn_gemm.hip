@@ -102,8 +102,21 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int g = lane >> 4, li = lane & 15;
   const int per_split = P.tiles_m * P.tiles_n;
-  const int split = local / per_split, t = local - split * per_split;
-  const int m0 = (t / P.tiles_n) * 64, n0 = (t % P.tiles_n) * 64;
+  // XCD-aware order (G.xcd_map): the problem's blocks are padded to 8 * per_x; block local runs on
+  // XCD local % 8 (round-robin dispatch, block_start % 8 == 0) and takes tile (local % 8) * per_x +
+  // local / 8, so each XCD owns a contiguous run of tiles -- split-major, then along the LARGER
+  // operand (n-major when B = N x K outweighs A = M x K) -- and reads that operand's tiles into its
+  // own L2 once instead of every XCD pulling all of it through the fabric.  Placement is a speed
+  // matter only: any block->XCD assignment computes the same tiles.
+  int lin = local;
+  if (G.xcd_map) {
+    const int nb = per_split * P.ksplit, per_x = (nb + 7) >> 3;
+    lin = (local & 7) * per_x + (local >> 3);
+    if (lin >= nb) return;                     // padding block
+  }
+  const int split = lin / per_split, t = lin - split * per_split;
+  const bool nmaj = G.xcd_map && P.N > P.M;
+  const int m0 = (nmaj ? t % P.tiles_m : t / P.tiles_n) * 64, n0 = (nmaj ? t / P.tiles_m : t % P.tiles_n) * 64;
   const int ksteps = (P.K + 31) >> 5;
   const int per = (ksteps + P.ksplit - 1) / P.ksplit;
   const int kbeg = split * per * 32, kend = min(P.K, (split * per + per) * 32);
@@ -117,34 +130,65 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) { acc[i][0] = zero4(); acc[i][1] = zero4(); }
 
+  // fused SGD (c_mode 4): this tile's fp32 master weights are loaded NOW, under the mainloop, not
+  // after it (the epilogue's one dependent memory round trip was ~1 us of every dW1 block)
+  float4 wv[4];
+  int ok[4];
+  if (P.c_mode == 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + u * 256, rr = e >> 4, cc = (e & 15) * 4;
+      const int m = m0 + rr, n = n0 + cc;
+      ok[u] = m < P.M && n < P.nvalid;
+      wv[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.C) + (ok[u] ? (size_t)m * P.ldc + n : 0));
+    }
+  }
+
+  // Two chunks of operand loads in flight (64 KB per block): the loads of chunk i+2 are issued as
+  // soon as chunk i's registers are in LDS.  With one chunk in flight every 128-deep chunk paid a
+  // whole memory latency under load (~1.6-2 us per chunk, in-kernel stamps); a K slice of up to two
+  // chunks (fc1 forward, dW1) now pays one.  Unrolled by two so the register sets stay static.
+  auto mma = [&](const bf16* a_s, const bf16* b_s, int nk) {
+    for (int kk = 0; kk < nk; ++kk) {
+      const bf16x8 a0 = frag(a_s, P.a_kmajor, 32 * wm, kk, g, li);
+      const bf16x8 a1 = frag(a_s, P.a_kmajor, 32 * wm + 16, kk, g, li);
+      const bf16x8 b0 = frag(b_s, P.b_kmajor, 32 * wn, kk, g, li);
+      const bf16x8 b1 = frag(b_s, P.b_kmajor, 32 * wn + 16, kk, g, li);
+      acc[0][0] = mfma16(a0, b0, acc[0][0]);
+      acc[0][1] = mfma16(a0, b1, acc[0][1]);
+      acc[1][0] = mfma16(a1, b0, acc[1][0]);
+      acc[1][1] = mfma16(a1, b1, acc[1][1]);
+    }
+  };
   if (kbeg < kend) {
-    Chunk ca, cb;
-    ca.load(A, P.lda, P.a_kmajor, P.M, kend, m0, kbeg, tid);
-    cb.load(B, P.ldb, P.b_kmajor, P.N, kend, n0, kbeg, tid);
-    int buf = 0;
-    for (int k0 = kbeg; k0 < kend; k0 += KC) {
-      bf16* a_s = sA + buf * TILE_ELEMS;
-      bf16* b_s = sB + buf * TILE_ELEMS;
-      ca.store(a_s, P.a_kmajor, tid);
-      cb.store(b_s, P.b_kmajor, tid);
-      if (k0 + KC < kend) {                    // next chunk in flight during this chunk's MFMAs
-        ca.load(A, P.lda, P.a_kmajor, P.M, kend, m0, k0 + KC, tid);
-        cb.load(B, P.ldb, P.b_kmajor, P.N, kend, n0, k0 + KC, tid);
+    Chunk ca0, cb0, ca1, cb1;
+    ca0.load(A, P.lda, P.a_kmajor, P.M, kend, m0, kbeg, tid);
+    cb0.load(B, P.ldb, P.b_kmajor, P.N, kend, n0, kbeg, tid);
+    if (kbeg + KC < kend) {
+      ca1.load(A, P.lda, P.a_kmajor, P.M, kend, m0, kbeg + KC, tid);
+      cb1.load(B, P.ldb, P.b_kmajor, P.N, kend, n0, kbeg + KC, tid);
+    }
+    // buffer b was last read by the MFMAs two chunks ago, which every wave finished before the
+    // barrier of the chunk in between
+    for (int k0 = kbeg; k0 < kend; k0 += 2 * KC) {
+      ca0.store(sA, P.a_kmajor, tid);
+      cb0.store(sB, P.b_kmajor, tid);
+      if (k0 + 2 * KC < kend) {
+        ca0.load(A, P.lda, P.a_kmajor, P.M, kend, m0, k0 + 2 * KC, tid);
+        cb0.load(B, P.ldb, P.b_kmajor, P.N, kend, n0, k0 + 2 * KC, tid);
       }
       __syncthreads();
-      const int nk = min(KC, kend - k0 + 31) >> 5;
-      for (int kk = 0; kk < nk; ++kk) {
-        const bf16x8 a0 = frag(a_s, P.a_kmajor, 32 * wm, kk, g, li);
-        const bf16x8 a1 = frag(a_s, P.a_kmajor, 32 * wm + 16, kk, g, li);
-        const bf16x8 b0 = frag(b_s, P.b_kmajor, 32 * wn, kk, g, li);
-        const bf16x8 b1 = frag(b_s, P.b_kmajor, 32 * wn + 16, kk, g, li);
-        acc[0][0] = mfma16(a0, b0, acc[0][0]);
-        acc[0][1] = mfma16(a0, b1, acc[0][1]);
-        acc[1][0] = mfma16(a1, b0, acc[1][0]);
-        acc[1][1] = mfma16(a1, b1, acc[1][1]);
+      mma(sA, sB, min(KC, kend - k0 + 31) >> 5);
+      if (k0 + KC >= kend) break;
+      ca1.store(sA + TILE_ELEMS, P.a_kmajor, tid);
+      cb1.store(sB + TILE_ELEMS, P.b_kmajor, tid);
+      if (k0 + 3 * KC < kend) {
+        ca1.load(A, P.lda, P.a_kmajor, P.M, kend, m0, k0 + 3 * KC, tid);
+        cb1.load(B, P.ldb, P.b_kmajor, P.N, kend, n0, k0 + 3 * KC, tid);
       }
-      buf ^= 1;                                 // the other buffer was last read two chunks ago,
-    }                                           // behind this chunk's barrier
+      __syncthreads();
+      mma(sA + TILE_ELEMS, sB + TILE_ELEMS, min(KC, kend - k0 - KC + 31) >> 5);
+    }
   }
   DMLC_STAMP(DMLC_TK_GEMM, 1);
 
@@ -168,16 +212,6 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
     // nvalid == N, checked by the binding)
     const float f = lr_sched(G.lr0, G.decay, G.decay_steps, G.staircase, G.warmup, st) * G.grad_scale;
     bf16* S = reinterpret_cast<bf16*>(P.S) + (((st + 1) & 1) ? P.s_par : 0);
-    float4 wv[4];
-    int ok[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {                   // master loads first: one latency for all four
-      const int e = tid + u * 256, rr = e >> 4, cc = (e & 15) * 4;
-      const int m = m0 + rr, n = n0 + cc;
-      ok[u] = m < P.M && n < P.nvalid;
-      const size_t q = ok[u] ? (size_t)m * P.ldc + n : 0;
-      wv[u] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(P.C) + q);
-    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (!ok[u]) continue;
@@ -239,7 +273,8 @@ extern "C" hipError_t dmlc_gemm_grouped(DmlcGemmGroup* G, hipStream_t s) {
     if (P.ksplit < 1) P.ksplit = 1;
     if (P.c_mode == 3) P.ksplit = 1;
     P.block_start = blocks;
-    blocks += P.tiles_m * P.tiles_n * P.ksplit;
+    const int nb = P.tiles_m * P.tiles_n * P.ksplit;
+    blocks += G->xcd_map ? (nb + 7) / 8 * 8 : nb;
   }
   G->nblocks = blocks;
   if (blocks == 0) return hipSuccess;

@@ -319,10 +319,17 @@ class FusedCifarEngine:
         # when several ranks share one GPU (rehearsals / tests: another rank's kernels hold CUs).
         local = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
         ndev = torch.cuda.device_count() if dev.type == "cuda" else 0
-        self.wgrad_reduce = in_launch and self.dp and local <= max(1, ndev)
+        reduce_ok = in_launch and self.dp and local <= max(1, ndev)
         # reduce-only also serves compute_gradients() on one GPU
-        self._grad_in_launch = in_launch and (self.wgrad_apply or self.wgrad_reduce) and not (self.fp8 and not self.wgrad_apply)
+        self._grad_in_launch = in_launch and (self.wgrad_apply or reduce_ok) and not (self.fp8 and not self.wgrad_apply)
+        # the data-parallel step takes the in-launch reduction exactly when compute_gradients() does
+        # (one predicate: the DP step and _conv_backward's assertion can never disagree)
+        self.wgrad_reduce = self.dp and self._grad_in_launch
         self.wbar = torch.zeros(WBAR_WORDS, dtype=torch.int32, device=dev)   # barrier words + error word
+        # pinned host copy of the barrier error word, refreshed by queue_error_copy() behind each
+        # chunk of steps (the trainer checks it at every progress point without a device sync)
+        self._err_host = (torch.zeros(1, dtype=torch.int32).pin_memory() if dev.type == "cuda"
+                          else torch.zeros(1, dtype=torch.int32))
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
                                                                         s_par=FC1_NUMEL)
@@ -354,7 +361,10 @@ class FusedCifarEngine:
         # profiles/r2_v26_fc1_split_sweep.jsonl): B=256 9 -> 82.2 vs 8 -> 83.0 us, B=512 9 best,
         # B=1024 4 -> 208.7 vs 2 -> 211.5 / 9 -> 211.7 us
         tiles = max(1, math.ceil(B / 64)) * 6
-        for s in (9, 6, 4, 3, 2):
+        # XCD-aware GEMM order (cnn_gemm.hip, default): a power-of-two split gives every XCD its own
+        # K slice of p2 and W1 (split 8: one slice per XCD)
+        cands = (8, 4, 2) if os.environ.get("DMLC_GEMM_XCD", "1") != "0" else (9, 6, 4, 3, 2)
+        for s in cands:
             if tiles * s <= 450:
                 return s
         return 1
@@ -482,10 +492,30 @@ class FusedCifarEngine:
     def _sgd(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True, fc1_fused: bool = False):
         self.ops.sgd(*self._sgd_args(mode, scale, roles, finalize, fc1_fused))
 
-    def check_barriers(self):
-        """Raise if an apply-mode barrier of the wgrad launch timed out (sticky device error word)."""
-        if self.wgrad_apply and int(self.wbar[10 * 32].item()) != 0:
-            raise RuntimeError("wgrad apply mode: a sub-grid barrier timed out (blocks not co-resident)")
+    @property
+    def barriers_in_use(self) -> bool:
+        """The wgrad launch meets at sub-grid barriers: apply mode (single-GPU SGD) or the in-launch
+        conv-slab reduction (data parallel / compute_gradients)."""
+        return bool(self.wgrad_apply or self._grad_in_launch)
+
+    def queue_error_copy(self):
+        """Enqueue a copy of the barrier error word into pinned host memory (stream-ordered: valid once
+        an event recorded after this call has completed)."""
+        if self.barriers_in_use:
+            self._err_host.copy_(self.wbar[10 * 32:10 * 32 + 1], non_blocking=True)
+
+    def check_barriers(self, cached: bool = False):
+        """Raise if a sub-grid barrier of the wgrad launch timed out (sticky device error word): apply
+        mode would have updated the weights, the reduce mode would have reduced (and all-reduced)
+        partial conv gradients -- every replica would agree on them, so the replica check cannot see
+        it.  ``cached``: read the pinned copy of :meth:`queue_error_copy` (no device sync)."""
+        if not self.barriers_in_use:
+            return
+        e = int(self._err_host[0]) if cached else int(self.wbar[10 * 32].item())
+        if e != 0:
+            mode = "apply" if self.wgrad_apply else "reduce"
+            raise RuntimeError(f"wgrad {mode} mode: a sub-grid barrier timed out (blocks not co-resident, "
+                               f"error word {e})")
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -504,7 +534,10 @@ class FusedCifarEngine:
             self._allreduce(self.grad[off:off + n])
 
     def check_comm(self):
-        """Raise if the xGMI all-reduce saw a peer stop participating (sticky device error word)."""
+        """Raise if the xGMI all-reduce saw a peer stop participating (sticky device error word) or a
+        wgrad sub-grid barrier timed out (device read: callers that must not sync use
+        ``check_barriers(cached=True)``)."""
+        self.check_barriers()
         if self.xgmi is not None:
             self.xgmi.check()
 
@@ -525,7 +558,7 @@ class FusedCifarEngine:
         self._fc_backward()
 
     def _seg_compute_b(self):
-        if self.dp and self.wgrad_reduce:       # conv slabs reduced inside the wgrad launch
+        if self.wgrad_reduce:                   # conv slabs reduced inside the wgrad launch
             self._conv_backward(reduce=True)
             return
         self._seg_compute_b_launch()

@@ -86,13 +86,24 @@ class _FusedAdapter:
         self.run(1)
 
     def device_event(self):
+        # the wgrad barrier error word rides along with every chunk (pinned copy, no sync)
+        if hasattr(self.eng, "queue_error_copy"):
+            self.eng.queue_error_copy()
         ev = torch.cuda.Event()
         ev.record()
         return ev
 
     def check_comm(self):
+        # a timed-out wgrad sub-grid barrier is not a peer failure (a restart would repeat it): a plain
+        # RuntimeError, raised before anything (e.g. a checkpoint) can use the step's weights
+        if hasattr(self.eng, "check_barriers"):
+            try:
+                self.eng.check_barriers(cached=True)
+            except RuntimeError as e:
+                raise RuntimeError(f"{e}; rerun with DMLC_WGRAD_SGD=0") from e
         try:
-            self.eng.check_comm()
+            if getattr(self.eng, "xgmi", None) is not None:
+                self.eng.xgmi.check()
         except RuntimeError as e:
             raise CommFailure(str(e)) from e
 
@@ -296,6 +307,7 @@ class Session:
     def __init__(self, cfg: C.TrainConfig, info: D.DistInfo, log=print):
         self.cfg, self.info, self.log = cfg, info, log
         self.chief = info.rank == 0
+        self._replica_checks = 0
         tr_x, tr_y, te_x, te_y = _load_data(cfg, info)
         self.test = (te_x, te_y)
         impl = pick_impl(cfg, info.device)
@@ -363,15 +375,21 @@ class Session:
             time.sleep(0.0002)
         self.engine.check_comm()
 
+    def _allreduce_path(self) -> str:
+        info = getattr(getattr(self.engine, "eng", None), "comm_info", None) or {}
+        return str(info.get("allreduce", self.info.backend))
+
     def _check_replicas(self):
         """Every synchronous replica must hold bit-identical parameters (parallel/health.py)."""
         if self.info.world_size <= 1 or not self.cfg.check_replicas or not hasattr(self.engine, "param_checksum"):
             return
         cs = self.engine.param_checksum()
         dev = self.info.device if self.info.backend == "nccl" else torch.device("cpu")
+        self._replica_checks += 1
         if not H.replicas_agree(cs, device=dev):
+            # the all-reduce this run actually used (xgmi / rccl / gloo ...), not the flag value
             marker = H.mark_divergence(self.cfg.log_dir, f"rank {self.info.rank} global_step {self.engine.global_step} "
-                                                        f"allreduce={self.cfg.allreduce}")
+                                                        f"allreduce={self._allreduce_path()}")
             raise CommFailure(f"replica divergence at global_step {self.engine.global_step} "
                               f"(marker {marker}: the next start uses --allreduce=rccl)")
 
@@ -437,6 +455,8 @@ class Session:
         eng.sync()
         eng.stats()                      # also checks the device error words once more
         self._check_replicas()
+        if self._replica_checks and self.info.rank == 0 and self._allreduce_path() == "xgmi":
+            H.clear_divergence(self.cfg.log_dir)   # the xGMI path passed every replica check again
         self.tracer.close()
         self.save(force=True)            # CheckpointSaverHook.end
         result["global_step"] = eng.global_step

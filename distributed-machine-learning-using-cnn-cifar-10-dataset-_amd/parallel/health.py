@@ -93,6 +93,11 @@ class Heartbeat:
             except Exception as e:                      # store host gone / unreachable
                 if self._stop.is_set() or not self.active:
                     return
+                if 0 in done or self.rank == 0:
+                    # the store lives in rank 0's process (reference-CLI worlds) or beside it: rank 0
+                    # marked itself finished, so its store going away is its clean exit, not a failure
+                    # (this rank is about to finish too: its own collectives completed with rank 0's)
+                    return
                 self._fail(f"rendezvous store unreachable ({type(e).__name__}: {e})")
                 return
 
@@ -102,19 +107,35 @@ class Heartbeat:
         self.failure = why
         self.on_failure(f"rank {self.rank}: {why}")
 
-    def stop(self, done: bool = True):
-        """Stop beating; ``done`` marks this rank finished so peers stop watching it."""
+    def stop(self, done: bool = True, wait_peers_s: Optional[float] = None):
+        """Stop beating; ``done`` marks this rank finished so peers stop watching it.  Rank 0 then
+        waits (bounded by ``wait_peers_s``, default the heartbeat timeout) until every peer has marked
+        itself finished too: in reference-CLI worlds rank 0's process hosts the rendezvous store, and
+        tearing it down under a slower peer's heartbeat would make that peer report a failure (exit
+        75) for a run that succeeded."""
         if not self.active:
             return
         self.active = False
         self._stop.set()
-        if done and self._store is not None:
-            try:
-                self._store.add(self._key("hb_done", self.rank), 1)
-            except Exception:
-                pass
         if self._thread is not None:
             self._thread.join(timeout=2 * self.interval + 1.0)
+        if not done or self._store is None:
+            return
+        try:
+            self._store.add(self._key("hb_done", self.rank), 1)
+        except Exception:
+            return
+        if self.rank != 0:
+            return
+        deadline = time.monotonic() + (self.timeout if wait_peers_s is None else float(wait_peers_s))
+        pending = set(range(1, self.world))
+        while pending and time.monotonic() < deadline:
+            try:
+                pending = {r for r in pending if self._store.add(self._key("hb_done", r), 0) == 0}
+            except Exception:
+                return
+            if pending:
+                time.sleep(min(0.05, self.interval))
 
 
 def _exit_comm_failure(msg: str):
@@ -129,14 +150,16 @@ _WEIGHTS = {}
 
 def replica_checksum(t: torch.Tensor) -> torch.Tensor:
     """int64 [2] = (sum of the fp32 bit patterns, position-weighted sum) of ``t`` -- exact integer
-    arithmetic (no overflow for <= 2^20 elements at weights <= 4093), so equal only for replicas
-    that agree bit for bit up to an astronomically unlikely collision; catches value AND position
-    (e.g. a shifted bucket) differences."""
+    arithmetic: |bits| < 2^31 and position weights <= 2039 < 2^11 keep every product below 2^42,
+    so the sums cannot overflow for up to 2^21 elements (the CNN has 1,068,298 parameters; past
+    2^21 they wrap, identically on every rank, so equality still compares replicas).  Equal only
+    for replicas that agree bit for bit up to an astronomically unlikely collision; catches value
+    AND position (e.g. a shifted bucket) differences."""
     v = t.detach().contiguous().view(-1).view(torch.int32).to(torch.int64)
     key = (v.numel(), v.device)
     w = _WEIGHTS.get(key)
     if w is None:
-        w = _WEIGHTS[key] = torch.arange(v.numel(), device=v.device, dtype=torch.int64) % 4093 + 1
+        w = _WEIGHTS[key] = torch.arange(v.numel(), device=v.device, dtype=torch.int64) % 2039 + 1
     return torch.stack([v.sum(), (v * w).sum()])
 
 
@@ -162,4 +185,22 @@ def mark_divergence(log_dir: str, info: str) -> Optional[str]:
 
 
 def divergence_marked(log_dir: str) -> bool:
-    return bool(log_dir) and os.path.exists(os.path.join(log_dir, DIVERGENCE_MARKER))
+    """True when an earlier run in ``log_dir`` saw replicas diverge WHILE using the custom xGMI
+    all-reduce (the one component a downgrade to RCCL can rule out).  Divergence under RCCL, the
+    eager engine or fault injection is recorded too but forces nothing."""
+    if not log_dir:
+        return False
+    p = os.path.join(log_dir, DIVERGENCE_MARKER)
+    if not os.path.exists(p):
+        return False
+    with open(p) as f:
+        return any("allreduce=xgmi" in line.split() for line in f)
+
+
+def clear_divergence(log_dir: str) -> bool:
+    """Remove the marker (a later xGMI run completed its replica checks cleanly)."""
+    p = os.path.join(log_dir, DIVERGENCE_MARKER) if log_dir else ""
+    if p and os.path.exists(p):
+        os.remove(p)
+        return True
+    return False

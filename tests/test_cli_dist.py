@@ -306,15 +306,24 @@ def test_heartbeat_detection_time_is_bounded(tmp_path):
 @pytest.mark.timeout(300)
 def test_replica_divergence_is_detected_and_forces_rccl(tmp_path):
     """A replica that stops matching the others (here: perturbed on rank 1) is caught at the next
-    output point on EVERY rank (exit 75), a marker is left in log_dir and the next start falls back
-    from the custom all-reduce to RCCL."""
+    output point on EVERY rank (exit 75) and a marker naming the all-reduce the run really used is
+    left in log_dir.  Only a divergence under the custom xGMI all-reduce makes the next start fall
+    back to RCCL (this CPU world all-reduces over gloo: its marker forces nothing)."""
     ws = _two_workers(tmp_path, dict(DMLC_FAULT_STEP="3", DMLC_FAULT_RANK="1", DMLC_FAULT_MODE="diverge"),
                       ["--generations=50", "--output_every=5", "--eval_every=100000"])
     outs = [w.communicate(timeout=240)[0] for w in ws]
     assert [w.returncode for w in ws] == [75, 75], outs
     assert all("replica divergence at global_step 5" in o for o in outs), outs
-    assert os.path.exists(tmp_path / ".dmlc_replica_divergence")
+    marker = tmp_path / ".dmlc_replica_divergence"
+    assert marker.exists() and "allreduce=gloo" in marker.read_text(), marker.read_text()
     ws = _two_workers(tmp_path, {}, ["--generations=6", "--output_every=5", "--eval_every=100000"])
     outs = [w.communicate(timeout=240)[0] for w in ws]
     assert [w.returncode for w in ws] == [0, 0], outs
+    assert "using --allreduce=rccl" not in outs[0]
+    with open(marker, "a") as f:                   # as a divergence under the xGMI path records it
+        f.write("2026-01-01T00:00:00 rank 0 global_step 5 allreduce=xgmi\n")
+    ws = _two_workers(tmp_path, {}, ["--generations=12", "--output_every=5", "--eval_every=100000"])
+    outs = [w.communicate(timeout=240)[0] for w in ws]
+    assert [w.returncode for w in ws] == [0, 0], outs
     assert "using --allreduce=rccl" in outs[0]
+    assert marker.exists()                         # an RCCL run does not clear an xGMI marker
