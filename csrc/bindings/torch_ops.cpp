@@ -467,6 +467,77 @@ void head(const Tensor& h1part, const Tensor& b1, const Tensor& w2t, const Tenso
   CHECK_HIP(dmlc_head(&a, stream_of(h1part)));
 }
 
+// the whole fc chain of a training step, one persistent launch (cnn_fc.hip)
+void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const Tensor& b1, const Tensor& w2t,
+              const Tensor& b2, const Tensor& w3t, const Tensor& b3, const Tensor& w3d, const Tensor& labels,
+              const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, double inv_batch,
+              bool relu_logits, const Tensor& h1, const Tensor& h2, const Tensor& dl, const Tensor& dh1,
+              const Tensor& dh2, const Tensor& loss_part, const Tensor& correct_part, const Tensor& dp2,
+              const Tensor& gw1, const Tensor& gw2, const Tensor& gw3, const Tensor& gb1, const Tensor& gb2,
+              const Tensor& gb3, bool fuse_sgd, at::ArrayRef<double> sched, int64_t nvalid, const Tensor& step,
+              const c10::optional<Tensor>& step_copy, const Tensor& sync, const Tensor& err) {
+  const int64_t B = p2.size(0);
+  TORCH_CHECK(B >= 16 && B <= 256 && B % 16 == 0, "fc_chain: batch must be a multiple of 16 in [16, 256]");
+  check(p2, "p2", at::kBFloat16, {B, 2304});
+  check(fc1n, "fc1n", at::kBFloat16, {2, 2304, 384});
+  check(h1part, "h1part", at::kFloat, {8, B, 384});
+  check_numel(b1, "b1", at::kFloat, 384);
+  check(w2t, "w2t", at::kBFloat16, {192, 384});
+  check_numel(b2, "b2", at::kFloat, 192);
+  check(w3t, "w3t", at::kBFloat16, {16, 192});
+  check_numel(b3, "b3", at::kFloat, 10);
+  check(w3d, "w3d", at::kBFloat16, {192, 32});
+  dev(labels, "labels");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.dim() == 1, "labels must be int32 [N]");
+  check(h1, "h1", at::kBFloat16, {B, 384});
+  check(h2, "h2", at::kBFloat16, {B, 192});
+  check(dl, "dl", at::kBFloat16, {B, 16});
+  check(dh1, "dh1", at::kBFloat16, {B, 384});
+  check(dh2, "dh2", at::kBFloat16, {B, 192});
+  check(loss_part, "loss_part", at::kFloat, {B / 4});
+  check(correct_part, "correct_part", at::kInt, {B / 4});
+  check(dp2, "dp2", at::kBFloat16, {B, 2304});
+  check_numel(gw1, "gw1", at::kFloat, 2304 * 384);
+  check_numel(gw2, "gw2", at::kFloat, 384 * 192);
+  check_numel(gw3, "gw3", at::kFloat, 192 * 10);
+  check_numel(gb1, "gb1", at::kFloat, 384);
+  check_numel(gb2, "gb2", at::kFloat, 192);
+  check_numel(gb3, "gb3", at::kFloat, 10);
+  check_numel(step, "step", at::kLong, 1);
+  check_min(sync, "sync", at::kInt, 19 * 32);
+  check_min(err, "err", at::kInt, 1);
+  TORCH_CHECK(sched.size() == 6, "fc_chain: sched = {lr0, decay, decay_steps, staircase, warmup, grad_scale}");
+  if (nvalid < 0) nvalid = B;
+  TORCH_CHECK(nvalid >= 1 && nvalid <= B, "fc_chain: nvalid must be in [1, B]");
+  c10::DeviceGuard guard(p2.device());
+  DmlcFcArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = (int)B; a.nvalid = (int)nvalid; a.mtiles = (int)((B + 63) / 64);
+  a.p2 = p2.data_ptr(); a.w1 = fc1n.data_ptr(); a.h1part = h1part.data_ptr<float>();
+  a.b1 = b1.data_ptr<float>(); a.w2t = w2t.data_ptr(); a.b2 = b2.data_ptr<float>();
+  a.w3t = w3t.data_ptr(); a.b3 = b3.data_ptr<float>(); a.w3d = w3d.data_ptr();
+  a.labels = labels.data_ptr<int>(); a.src = index_src(idx, counter, period, B);
+  check_order_fits(a.src, labels.size(0));
+  a.inv_batch = (float)inv_batch; a.relu_logits = relu_logits;
+  a.h1 = h1.data_ptr(); a.h2 = h2.data_ptr(); a.dl = dl.data_ptr(); a.dh1 = dh1.data_ptr(); a.dh2 = dh2.data_ptr();
+  a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
+  a.dp2 = dp2.data_ptr();
+  a.gw1 = gw1.data_ptr<float>(); a.gw2 = gw2.data_ptr<float>(); a.gw3 = gw3.data_ptr<float>();
+  a.gb1 = gb1.data_ptr<float>(); a.gb2 = gb2.data_ptr<float>(); a.gb3 = gb3.data_ptr<float>();
+  a.fuse_sgd = fuse_sgd;
+  a.lr0 = (float)sched[0]; a.decay = (float)sched[1]; a.decay_steps = (float)sched[2];
+  a.staircase = sched[3] != 0.0; a.warmup = (float)sched[4]; a.grad_scale = (float)sched[5];
+  a.step = step.data_ptr<int64_t>();
+  a.step_copy = nullptr;
+  if (step_copy.has_value()) {
+    check_numel(*step_copy, "step_copy", at::kLong, 1);
+    a.step_copy = step_copy->data_ptr<int64_t>();
+  }
+  a.sync = reinterpret_cast<unsigned int*>(sync.data_ptr<int>());
+  a.err = reinterpret_cast<unsigned int*>(err.data_ptr<int>());
+  CHECK_HIP(dmlc_fc_chain(&a, stream_of(p2)));
+}
+
 static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_scale, at::IntArrayRef off,
          const Tensor& part1, const Tensor& partb1, const Tensor& part2, const Tensor& partb2, const Tensor& w1f,
          const Tensor& w2f, const Tensor& w2d, const Tensor& fc1n, const Tensor& fc2t, const Tensor& fc2n,
@@ -635,6 +706,12 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, bool relu_logits, bool train, "
         "Tensor(a!) h1, Tensor(b!) h2, Tensor(c!) dl, Tensor(d!) dh1, Tensor(e!) dh2, Tensor(f!) loss_part, "
         "Tensor(g!) correct_part, Tensor(h!)? logits_out, int nvalid=-1, Tensor? step=None, Tensor(i!)? step_copy=None) -> ()");
+  m.def("fc_chain(Tensor p2, Tensor(a!) fc1n, Tensor(b!) h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, "
+        "Tensor b3, Tensor w3d, Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, "
+        "bool relu_logits, Tensor(c!) h1, Tensor(d!) h2, Tensor(e!) dl, Tensor(f!) dh1, Tensor(g!) dh2, "
+        "Tensor(h!) loss_part, Tensor(i!) correct_part, Tensor(j!) dp2, Tensor(k!) gw1, Tensor(l!) gw2, "
+        "Tensor(m!) gw3, Tensor(n!) gb1, Tensor(o!) gb2, Tensor(p!) gb3, bool fuse_sgd, float[] sched, "
+        "int nvalid, Tensor step, Tensor(q!)? step_copy, Tensor(r!) sync, Tensor(s!) err) -> ()");
   m.def("wgrad_sgd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor p1, Tensor dy2, int groups2, Tensor xraw, Tensor(z!) bar, "
         "Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor(r!) part1, Tensor(s!) partb1, "
@@ -670,6 +747,7 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("wgrad", &wgrad);
   m.impl("gemm_grouped", &gemm_grouped);
   m.impl("head", &head);
+  m.impl("fc_chain", &fc_chain);
   m.impl("sgd", &sgd);
   m.impl("wgrad_sgd", &wgrad_sgd);
 }

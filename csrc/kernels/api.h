@@ -175,6 +175,33 @@ struct DmlcHeadArgs {
   const int64_t* step; int64_t* step_copy;
 };
 
+// The fully-connected part of a training step in ONE persistent launch (cnn_fc.hip; B <= 256,
+// B % 16 == 0; 256 co-resident workgroups): fc1 forward (split-K), the MLP head (loss, accuracy,
+// dlogits -> dh2 -> dh1), and the fc backward (dp2 = dh1 W1^T, dW1 [+ fused fc1 SGD], dW2, dW3, db).
+struct DmlcFcArgs {
+  int B, nvalid, mtiles;             // padded batch, real rows, ceil(B / 64)
+  const void* p2;                    // bf16 [B][2304] pooled conv2 output (NHWC flatten)
+  void* w1;                          // bf16 [2][2304][384] fc1 shadow (step parity; fused SGD writes the other)
+  float* h1part;                     // fp32 [8][B][384] fc1 split-K partials (workspace)
+  const float* b1;
+  const void* w2t; const float* b2;  // bf16 [192][384]
+  const void* w3t; const float* b3;  // bf16 [16][192]
+  const void* w3d;                   // bf16 [192][32]
+  const int* labels;
+  DmlcIndexSrc src;
+  float inv_batch; int relu_logits;
+  void* h1; void* h2; void* dl; void* dh1; void* dh2;   // bf16 hand-off rows (as DmlcHeadArgs)
+  float* loss_part; int* correct_part;                  // [B / 4]
+  void* dp2;                         // bf16 [B][2304] out: the conv backward's input
+  float* gw1;                        // fuse_sgd: fc1 fp32 master (updated); else the fc1 weight gradient
+  float* gw2; float* gw3; float* gb1; float* gb2; float* gb3;   // gradients (flat grad views)
+  int fuse_sgd;
+  float lr0, decay, decay_steps, warmup, grad_scale; int staircase;
+  const int64_t* step; int64_t* step_copy;             // device step counter; copy for the SGD reader
+  unsigned int* sync;                // >= 19 * 32 zeroed uints (counters re-arm themselves)
+  unsigned int* err;                 // sticky error word (bit 2: a seam wait timed out)
+};
+
 // Fused SGD over the flat fp32 parameter buffer (+ split-K partial reduction, LR schedule from the
 // device step counter, bf16 shadow-weight refresh, step++ by the last workgroup, stats ring).
 struct DmlcSgdArgs {
@@ -259,6 +286,7 @@ hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s);
 hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s);
 hipError_t dmlc_gemm_grouped(DmlcGemmGroup* g, hipStream_t s);
+hipError_t dmlc_fc_chain(const DmlcFcArgs* a, hipStream_t s);
 hipError_t dmlc_head(const DmlcHeadArgs* a, hipStream_t s);
 hipError_t dmlc_sgd(DmlcSgdArgs* a, hipStream_t s);
 

@@ -398,7 +398,7 @@ DEV void conv2_apply(const DmlcWgradArgs& A, int c4, int grp, char* smem, unsign
   // writes its slot); block (0, 0) also zeroes the unused slots and publishes the scale
   const int slot = 2 * (c4 * n + grp), nxt = (int)((step & 1) ^ 1);
   W2Fp8 f8 = {s.w2f8 ? w2_fp8_scale(s, step) : 0.f, nxt, slot, reinterpret_cast<float*>(smem + 64)};
-  if (s.w2f8 && c4 == 0 && grp == 0) {
+  if (s.w2f8 && s.mode == 0 && c4 == 0 && grp == 0) {   // (reduce-only mode 1 touches no fp8 state)
     for (int i = 8 * n + tid; i < C2_BLOCKS; i += W2T) s.amax_w[(size_t)nxt * C2_BLOCKS + i] = 0.f;
     if (tid == 0) { s.scale_w[0] = f8.sw; s.scale_w[1] = f8.sw; }
   }
@@ -410,7 +410,7 @@ DEV void conv2_apply(const DmlcWgradArgs& A, int c4, int grp, char* smem, unsign
     f8.slot = slot + 1;
     if (flag[0]) conv2_reduce(A, c4, m, e, lr, f8);
     __syncthreads();                           // flag / LDS reused by the bias below
-  } else if (s.w2f8 && tid == 0) {
+  } else if (s.w2f8 && s.mode == 0 && tid == 0) {
     s.amax_w[(size_t)nxt * C2_BLOCKS + slot + 1] = 0.f;   // no second half
   }
   if (c4 == 0 && grp == 0) conv_bias(s, 1, lr, reinterpret_cast<float4*>(smem), tid, true);

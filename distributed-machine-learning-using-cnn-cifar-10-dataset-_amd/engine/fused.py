@@ -257,9 +257,23 @@ class FusedCifarEngine:
         sdt = torch.bfloat16 if self.w2_slab == "bf16" else torch.float32
         self.part2, self.partb2 = z(self.g2, 1600, 64, dt=sdt), z(self.g2, 64, dt=torch.float32)
         self.part1, self.partb1 = z(self.g1, 80, 64, dt=torch.float32), z(self.g1, 64, dt=torch.float32)
-        # head: head_rows(B) batch rows per workgroup (B / rows workgroups share the fc2 weight reads)
-        self.loss_part = z(B // head_rows(B), dt=torch.float32)
-        self.correct_part = z(B // head_rows(B), dt=torch.int32)
+        # the whole fc chain of a training step (fc1 forward, head, fc backward) as ONE persistent
+        # launch (cnn_fc.hip) instead of three: B <= 256, 256 co-resident workgroups (one per CU, so
+        # not when several ranks share a GPU), not beside the fc-branch graph.  DMLC_FC_FUSED=1 on.
+        local_ = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
+        ndev_ = torch.cuda.device_count() if dev.type == "cuda" else 0
+        cus_ = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
+        self.fc_fused = (B <= 256 and cus_ >= 256 and local_ <= max(1, ndev_)
+                         and os.environ.get("DMLC_FC_BRANCH", "0") != "1"
+                         and os.environ.get("DMLC_FC_FUSED", "0") == "1")
+        self.h1part8 = z(8, B, 384, dt=torch.float32) if self.fc_fused else None
+        self.fc_sync = torch.zeros(20 * 32, dtype=torch.int32, device=dev)
+        self._fc_src = None
+        # head: head_rows(B) batch rows per workgroup (B / rows workgroups share the fc2 weight reads);
+        # the fused fc chain's head takes 4 rows per workgroup
+        hr = 4 if self.fc_fused else head_rows(B)
+        self.loss_part = z(B // hr, dt=torch.float32)
+        self.correct_part = z(B // hr, dt=torch.int32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
         # the head kernel copies the step counter here; the SGD launch reads the copy, so one of its
         # workgroups can bump step_t without an arrival ticket (cnn_sgd.hip)
@@ -320,8 +334,11 @@ class FusedCifarEngine:
         local = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
         ndev = torch.cuda.device_count() if dev.type == "cuda" else 0
         reduce_ok = in_launch and self.dp and local <= max(1, ndev)
-        # reduce-only also serves compute_gradients() on one GPU
-        self._grad_in_launch = in_launch and (self.wgrad_apply or reduce_ok) and not (self.fp8 and not self.wgrad_apply)
+        # reduce-only also serves compute_gradients() on one GPU.  fp8 included: the round-3 report of a
+        # wrong conv1 gradient under the in-launch reduction (cosine 0.24 at B=64) came from an
+        # intermediate build; on this one tools/dbg_race.py 64 fp8 finds 0/5 mismatches against the
+        # two-launch path and test_fp8_gpu.py covers reduce mode at B=64/100/1024 bit for bit
+        self._grad_in_launch = in_launch and (self.wgrad_apply or reduce_ok)
         # the data-parallel step takes the in-launch reduction exactly when compute_gradients() does
         # (one predicate: the DP step and _conv_backward's assertion can never disagree)
         self.wgrad_reduce = self.dp and self._grad_in_launch
@@ -424,6 +441,9 @@ class FusedCifarEngine:
             o.conv2_fwd_fp8(self.p1, self.w2f8[0], p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
         elif not self.fused_fwd and self.conv_split == 1:
             o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
+        if train and self.fc_fused:
+            self._fc_src = (idx, counter, period)    # fc forward + head run in _fc_backward's launch
+            return
         self._gemm(self._fc1_fwd)
         o.head(self.h1part, p["full_bias_1"], self.fc2t, p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d,
                self.fc2n, self.labels, idx, counter, period, 1.0 / (self.Bv * self.world_size), self.relu_logits,
@@ -438,7 +458,27 @@ class FusedCifarEngine:
             self.ops.gemm_grouped(f["A"], f["B"], f["C"], f["bias"], f["params"], self.step_t)
 
     def _fc_backward(self, fused_sgd: bool = False):
+        if self.fc_fused:
+            self._fc_chain(fused_sgd)
+            return
         self._gemm(self._fc_bwd_sgd if fused_sgd else self._fc_bwd, sgd=fused_sgd)
+
+    def _fc_chain(self, fused_sgd: bool):
+        """fc1 forward + head + fc backward in one persistent launch (cnn_fc.hip), for the batch of
+        the preceding _forward(train=True).  fused_sgd: the fc1 weights are updated in the dW1
+        epilogue (single GPU), else the fc1 weight gradient goes to the flat gradient."""
+        assert self._fc_src is not None, "_fc_chain follows a training _forward"
+        idx, counter, period = self._fc_src
+        self._fc_src = None
+        p, gv = self.pv, self.gv
+        sched = [self.lr0, self.decay, self.decay_steps, 1.0 if self.staircase else 0.0, self.warmup, 1.0]
+        self.ops.fc_chain(self.p2.view(self.B, 2304), self.fc1n, self.h1part8, p["full_bias_1"], self.fc2t,
+                          p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d, self.labels, idx, counter, period,
+                          1.0 / (self.Bv * self.world_size), self.relu_logits, self.h1, self.h2, self.dl, self.dh1,
+                          self.dh2, self.loss_part, self.correct_part, self.dp2.view(self.B, 2304),
+                          p["full_weight_1"] if fused_sgd else gv["full_weight_1"], gv["full_weight_2"],
+                          gv["full_weight_3"], gv["full_bias_1"], gv["full_bias_2"], gv["full_bias_3"], fused_sgd,
+                          sched, self.Bv, self.step_t, self.step_sgd, self.fc_sync, self.wbar[10 * 32:10 * 32 + 1])
 
     def _conv_backward(self, src=None, apply: bool = False, reduce: bool = False):
         """apply: + the whole SGD in the wgrad launch (single GPU); reduce: + the conv slab reduction
@@ -496,7 +536,7 @@ class FusedCifarEngine:
     def barriers_in_use(self) -> bool:
         """The wgrad launch meets at sub-grid barriers: apply mode (single-GPU SGD) or the in-launch
         conv-slab reduction (data parallel / compute_gradients)."""
-        return bool(self.wgrad_apply or self._grad_in_launch)
+        return bool(self.wgrad_apply or self._grad_in_launch or self.fc_fused)
 
     def queue_error_copy(self):
         """Enqueue a copy of the barrier error word into pinned host memory (stream-ordered: valid once
@@ -514,8 +554,8 @@ class FusedCifarEngine:
         e = int(self._err_host[0]) if cached else int(self.wbar[10 * 32].item())
         if e != 0:
             mode = "apply" if self.wgrad_apply else "reduce"
-            raise RuntimeError(f"wgrad {mode} mode: a sub-grid barrier timed out (blocks not co-resident, "
-                               f"error word {e})")
+            where = "fc chain" if e & 2 and not e & 1 else f"wgrad {mode} mode"
+            raise RuntimeError(f"{where}: a sub-grid barrier timed out (blocks not co-resident, error word {e})")
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist

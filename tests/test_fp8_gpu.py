@@ -141,7 +141,7 @@ def test_lr_warmup_and_linear_scaling_on_device():
     assert [eng.read_stats(s)["lr"] for s in range(1, 9)] == pytest.approx(want, rel=1e-6)
 
 
-@pytest.mark.parametrize("B", [100, 1024])
+@pytest.mark.parametrize("B", [64, 100, 1024])
 def test_fp8_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
     """fp8 (BASELINE config 5) on one GPU: the SGD inside the wgrad launch also writes the e4m3
     shadows (forward w2f8, the dgrad's flipped copy) with the delayed per-tensor scale and the new
@@ -168,3 +168,47 @@ def test_fp8_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
     assert torch.equal(ref.scale_w, fused.scale_w)
     assert float(ref.amax_w[1].max()) == float(fused.amax_w[1].max())   # step 7: slot 1 holds the new amax
     assert ref.read_stats(7) == fused.read_stats(7)
+
+
+@pytest.mark.parametrize("B", [64, 100, 1024])
+def test_fp8_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B, monkeypatch):
+    """fp8 compute_gradients() through the in-launch conv-slab reduction (reduce mode, the data-parallel
+    path; helpers included at B=64) against the reduce-only SGD launch, bit for bit over the whole flat
+    gradient, for the generated batch and an explicit index list -- the case round 3 excluded after a
+    wrong conv1 gradient (cosine 0.24 at B=64) on an intermediate build."""
+    data, labels = _synthetic(8 * B, seed=47)
+    kw = dict(seed=48, lr=1e-4, relu_logits=False, dtype="fp8")
+    monkeypatch.setenv("DMLC_WGRAD_SGD_FP8", "1")             # single GPU: in-launch mode needs the opt-in
+    fused = FusedCifarEngine(B, data, labels, **kw)
+    monkeypatch.setenv("DMLC_WGRAD_SGD", "0")
+    ref = FusedCifarEngine(B, data, labels, **kw)
+    assert fused._grad_in_launch and not ref._grad_in_launch and fused.fp8
+    idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(3))[:B].to(torch.int32)
+    for explicit in (None, idx, None):
+        g_ref = ref.compute_gradients(explicit).clone()
+        g_fused = fused.compute_gradients(explicit).clone()
+        torch.cuda.synchronize()
+        assert torch.isfinite(g_ref).all() and float(g_ref.abs().max()) > 0
+        assert torch.equal(g_ref, g_fused)
+    assert torch.equal(ref.scale_w, fused.scale_w)            # reduce mode leaves the fp8 state alone
+    fused.check_barriers()
+
+
+def test_check_barriers_raises_in_reduce_mode():
+    """The sticky error word of the wgrad sub-grid barriers is checked in reduce mode too (a timed-out
+    barrier there would all-reduce partial conv gradients that every replica agrees on), through the
+    device read and through the pinned copy the trainer reads at every progress point."""
+    data, labels = _synthetic(512, seed=5)
+    eng = FusedCifarEngine(64, data, labels, seed=6, dp_force=True, allreduce="rccl")   # no step taken
+    assert eng.wgrad_reduce and not eng.wgrad_apply and eng.barriers_in_use
+    eng.wbar[320] = 1                                         # as bar_wait's give-up path sets it
+    with pytest.raises(RuntimeError, match="sub-grid barrier timed out"):
+        eng.check_barriers()
+    eng.queue_error_copy()
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="sub-grid barrier timed out"):
+        eng.check_barriers(cached=True)
+    with pytest.raises(RuntimeError):
+        eng.check_comm()
+    eng.wbar[320] = 0
+    eng.check_barriers()

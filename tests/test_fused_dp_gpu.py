@@ -154,7 +154,7 @@ def test_dp2_tune_schedule_agrees_across_ranks(tmp_path, allreduce):
     assert torch.isfinite(t0["flat"]).all()
 
 
-def _nccl1_rank(rank, world, port, out, steps):
+def _nccl1_rank(rank, world, port, out, steps, dtype="bf16"):
     sys.path.insert(0, REPO)
     import datetime
     import torch.distributed as dist
@@ -167,34 +167,44 @@ def _nccl1_rank(rank, world, port, out, steps):
     res = {}
     for sched in ("serial", "overlap"):
         eng = FusedCifarEngine(32, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dp_force=True,
-                               dp_schedule=sched, allreduce="rccl")
+                               dp_schedule=sched, allreduce="rccl", dtype=dtype)
         assert eng.dp and eng.capture_comm and eng.single_graph, (eng.dp, eng.capture_comm)
+        # the DP step reduces the conv slabs inside the wgrad launch (fp8 too: round 3 asserted here)
+        assert eng.wgrad_reduce == eng._grad_in_launch
+        assert eng.wgrad_reduce or sched == "overlap", sched
         eng.step()
         eng.capture(steps_per_graph=4)
         eng.run(steps - 1)
         torch.cuda.synchronize()
         res[sched] = {"flat": eng.flat_params(), "step": eng.global_step(), "info": dict(eng.comm_info)}
+    if dtype == "fp8":
+        res["fp8_state"] = {"w2f8": eng.w2f8.cpu(), "scale_w": eng.scale_w.cpu()}
     torch.save(res, os.path.join(out, "nccl1.pt"))
     dist.destroy_process_group()
 
 
 @pytest.mark.timeout(240)
-def test_captured_rccl_allreduce_world1_equals_single_gpu(tmp_path):
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_captured_rccl_allreduce_world1_equals_single_gpu(tmp_path, dtype):
     """The RCCL path with the all-reduce captured inside the step graph (capture_comm) and chained
-    steps, on a 1-rank nccl group (dp_force: the DP step -- reduce-only SGD, all-reduce, apply-only
-    SGD -- runs at world size 1).  A 1-rank sum is the identity, so it must equal the plain
-    single-GPU step bit for bit, for both step schedules."""
+    steps, on a 1-rank nccl group (dp_force: the DP step -- conv slabs reduced in the wgrad launch,
+    all-reduce, apply-only SGD -- runs at world size 1).  A 1-rank sum is the identity, so it must
+    equal the plain single-GPU step bit for bit, for both step schedules; fp8 (BASELINE config 5)
+    also compares the e4m3 weight shadows and the delayed scales."""
     import torch.multiprocessing as mp
     from dmlc.cli import free_port
     from dmlc.engine.fused import FusedCifarEngine
     steps = 11
-    mp.spawn(_nccl1_rank, args=(1, free_port(), str(tmp_path), steps), nprocs=1, join=True)
+    mp.spawn(_nccl1_rank, args=(1, free_port(), str(tmp_path), steps, dtype), nprocs=1, join=True)
     res = torch.load(tmp_path / "nccl1.pt", weights_only=True)
     x, y = _data()
-    ref = FusedCifarEngine(32, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False)
+    ref = FusedCifarEngine(32, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dtype=dtype)
     for _ in range(steps):
         ref.step()
     torch.cuda.synchronize()
+    f8 = res.pop("fp8_state", None)
+    if dtype == "fp8":
+        assert torch.equal(f8["w2f8"], ref.w2f8.cpu()) and torch.equal(f8["scale_w"], ref.scale_w.cpu())
     for sched, r in res.items():
         assert r["step"] == steps, sched
         assert r["info"]["captured_comm"] and r["info"]["backend"] == "nccl", r["info"]

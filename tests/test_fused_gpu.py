@@ -310,6 +310,7 @@ def test_fc_branch_step_is_bit_identical(B, monkeypatch):
     the parameters, step counter and stats equal the one-branch step bit for bit."""
     data, labels = _synthetic(8 * B, seed=41)
     kw = dict(seed=40, lr=1e-4, relu_logits=False)     # (lr 1e-2 on raw pixels diverges to NaN in ~4 steps)
+    monkeypatch.setenv("DMLC_FC_FUSED", "0")           # the branch runs the three-launch fc kernels
     ref = FusedCifarEngine(B, data, labels, **kw)
     monkeypatch.setenv("DMLC_FC_BRANCH", "1")
     br = FusedCifarEngine(B, data, labels, **kw)
@@ -412,3 +413,56 @@ def test_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B, monkeypatch):
         assert torch.isfinite(g_ref).all() and float(g_ref.abs().max()) > 0
         assert torch.equal(g_ref, g_fused)
     fused.check_barriers()
+
+
+@pytest.mark.parametrize("B", [16, 100, 128, 256])
+def test_fc_chain_launch_matches_three_launch_path(B, monkeypatch):
+    """The persistent fc-chain launch (cnn_fc.hip: fc1 forward + head + fc backward, 256 co-resident
+    workgroups, in-launch hand-offs) against the three-launch path (grouped GEMM, head, grouped
+    GEMM) on the same weights and batch: loss, accuracy, the conv backward's input dp2 and every
+    gradient segment agree to bf16 rounding (the fc1 split-K order differs: 8 slices, not 9)."""
+    data, labels = _synthetic(8 * B, seed=61)
+    kw = dict(seed=62, lr=1e-4, relu_logits=False)
+    monkeypatch.setenv("DMLC_FC_FUSED", "1")
+    fused = FusedCifarEngine(B, data, labels, **kw)
+    monkeypatch.setenv("DMLC_FC_FUSED", "0")
+    ref = FusedCifarEngine(B, data, labels, **kw)
+    assert fused.fc_fused and not ref.fc_fused
+    idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(5))[:B].to(torch.int32)
+    for explicit in (None, idx):
+        g_ref = ref.compute_gradients(explicit).clone()
+        g_fus = fused.compute_gradients(explicit).clone()
+        torch.cuda.synchronize()
+        fused.check_barriers()
+        n = B // 4
+        assert abs(float(fused.loss_part[:n].sum()) - float(ref.loss_part.sum())) <= 1e-3 * max(1.0, float(ref.loss_part.sum()))
+        assert int(fused.correct_part[:n].sum()) == int(ref.correct_part.sum())
+        assert _rel(fused.dp2[:fused.Bv], ref.dp2[:ref.Bv]) < 2e-2
+        for spec in M.PARAM_SPECS:
+            sl = slice(spec.offset, spec.offset + spec.numel)
+            assert _rel(g_fus[sl], g_ref[sl]) < 2e-2, spec.name
+    # counters re-arm: many launches (eager and graph-replayed) keep giving the eager step's weights
+    for eng in (fused, ref):
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(9)
+    torch.cuda.synchronize()
+    fused.check_barriers()
+    assert _rel(fused.master, ref.master) < 1e-3
+    assert abs(fused.read_stats(10)["loss"] - ref.read_stats(10)["loss"]) < 1e-2 * max(1.0, abs(ref.read_stats(10)["loss"]))
+
+
+def test_fc_chain_graph_replay_is_deterministic(monkeypatch):
+    """Two engines, same seed, same steps through the persistent fc chain: bit-identical weights
+    (fixed-order split-K sums, no atomics on data)."""
+    monkeypatch.setenv("DMLC_FC_FUSED", "1")
+    data, labels = _synthetic(2048, seed=71)
+    engs = [FusedCifarEngine(256, data, labels, seed=72, lr=1e-3) for _ in range(2)]
+    for eng in engs:
+        assert eng.fc_fused
+        eng.step()
+        eng.capture(steps_per_graph=8)
+        eng.run(23)
+    torch.cuda.synchronize()
+    assert torch.equal(engs[0].master, engs[1].master)
+    assert engs[0].read_stats(24) == engs[1].read_stats(24)
