@@ -237,7 +237,6 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
   bf16* h2s = reinterpret_cast<bf16*>(smem + HL::H2);
   bf16* dh2s = reinterpret_cast<bf16*>(smem + HL::DH2);
   bf16* dls = reinterpret_cast<bf16*>(smem + HL::DL);
-  float (*lg)[17] = reinterpret_cast<float (*)[17]>(smem + HL::LG);
   const int lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   constexpr int RB = FC_RB;
   const int r0 = hb * RB, mt = r0 >> 6;
@@ -287,6 +286,8 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
   else if (tid < 144) *reinterpret_cast<bf16x4*>(h2s + RB * H2_LD + (tid - 96) * 4) = pack4(0.f, 0.f, 0.f, 0.f);
   else if (tid < 192) *reinterpret_cast<bf16x4*>(dh2s + RB * H2_LD + (tid - 144) * 4) = pack4(0.f, 0.f, 0.f, 0.f);
   else if (tid < 200) *reinterpret_cast<bf16x4*>(dls + RB * DL_LD + (tid - 192) * 4) = pack4(0.f, 0.f, 0.f, 0.f);
+  else if (tid < 200 + 2 * RB)                 // dlogit columns 16..31 of the real rows (K pad)
+    *reinterpret_cast<uint4*>(dls + ((tid - 200) >> 1) * DL_LD + 16 + 8 * ((tid - 200) & 1)) = make_uint4(0, 0, 0, 0);
 
   // --- seam 1: every fc1 forward task of this 64-row tile
   DMLC_STAMP(DMLC_TK_HEAD, 1);
@@ -324,54 +325,60 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
   }
   lds_barrier();
 
-  // (c) logits = [relu](h2 W3 + b3): wave 7, one 16x16 tile, K = 192
+  // (c)+(d) wave 7, in registers: logits = [relu](h2 W3 + b3) as one 16x16 tile (K = 192), lane
+  //   (g, li) holding classes 4g..4g+3 of row li; the row max / argmax / exp-sum meet across the
+  //   four lane groups by two xor shuffles -- softmax cross-entropy, accuracy and dlogits without an
+  //   LDS round trip or a barrier in between (fixed shuffle order: deterministic)
   if (w == 7) {
     f32x4 acc = zero4();
 #pragma unroll
     for (int ks = 0; ks < 6; ++ks) acc = mfma16(w3f[ks], lds_b128(h2s + rr * H2_LD + ks * 32 + 8 * g), acc);
+    float v[4];
+    float m = -INFINITY;
+    int am = 16;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int nn = 4 * g + i;
-      if (nn < 10) {
-        float v = acc[i] + b3v[i];
-        if (a.relu_logits) v = fmaxf(v, 0.f);
-        lg[li][nn] = v;
-      }
+      v[i] = acc[i] + b3v[i];
+      if (a.relu_logits) v[i] = fmaxf(v[i], 0.f);
+      if (4 * g + i < 10 && v[i] > m) { m = v[i]; am = 4 * g + i; }   // first maximum within the lane
     }
-  }
-  lds_barrier();
-
-  // (d) softmax cross-entropy, accuracy, dlogits (wave 7, lanes 0..RB-1 = rows)
-  if (w == 7) {
-    float loss = 0.f, corr = 0.f;
-    if (lane < RB) {
-      const int b = r0 + lane;
-      const float vr = b < a.nvalid ? 1.f : 0.f;
-      float m = lg[lane][0];
-      int am = 0;
 #pragma unroll
-      for (int j = 1; j < 10; ++j) if (lg[lane][j] > m) { m = lg[lane][j]; am = j; }
-      float se = 0.f;
+    for (int o = 16; o <= 32; o <<= 1) {       // larger value wins, ties go to the smaller class
+      const float m2 = __shfl_xor(m, o);
+      const int a2 = __shfl_xor(am, o);
+      if (m2 > m || (m2 == m && a2 < am)) { m = m2; am = a2; }
+    }
+    float se = 0.f;
 #pragma unroll
-      for (int j = 0; j < 10; ++j) se += __expf(lg[lane][j] - m);
-      const float lse = m + __logf(se);
-      loss = vr * (lse - lg[lane][label]);
-      corr = vr * (am == label ? 1.f : 0.f);
+    for (int i = 0; i < 4; ++i) se += 4 * g + i < 10 ? __expf(v[i] - m) : 0.f;
+    se += __shfl_xor(se, 16);
+    se += __shfl_xor(se, 32);
+    const float lse = m + __logf(se);
+    const int lab = __shfl(label, li);          // wave 7 lane r < RB loaded row r's label
+    const bool rowok = li < RB;
+    const float vr = rowok && r0 + li < a.nvalid ? 1.f : 0.f;
+    float loss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
+    for (int i = 0; i < 4; ++i) if (4 * g + i == lab) loss = vr * (lse - v[i]);
+    const float corr = g == 0 ? vr * (am == lab ? 1.f : 0.f) : 0.f;
+    if (rowok) {
+      bf16x4 d4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 4 * g + i;
         float d = 0.f;
-        if (j < 10) {
-          d = (__expf(lg[lane][j] - lse) - (j == label ? 1.f : 0.f)) * a.inv_batch * vr;
-          if (a.relu_logits && !(lg[lane][j] > 0.f)) d = 0.f;
+        if (c < 10) {
+          d = (__expf(v[i] - lse) - (c == lab ? 1.f : 0.f)) * a.inv_batch * vr;
+          if (a.relu_logits && !(v[i] > 0.f)) d = 0.f;
         }
-        dls[lane * DL_LD + j] = (bf16)d;
+        d4[i] = (bf16)d;
       }
+      *reinterpret_cast<bf16x4*>(dls + li * DL_LD + 4 * g) = d4;
     }
-    loss = wave_sum(loss);
-    corr = wave_sum(corr);
+    const float ls = wave_sum(rowok ? loss : 0.f), cs = wave_sum(corr);
     if (lane == 0) {
-      a.loss_part[hb] = loss;
-      a.correct_part[hb] = (int)(corr + 0.5f);
+      a.loss_part[hb] = ls;
+      a.correct_part[hb] = (int)(cs + 0.5f);
     }
   }
   lds_barrier();

@@ -259,13 +259,13 @@ class FusedCifarEngine:
         self.part1, self.partb1 = z(self.g1, 80, 64, dt=torch.float32), z(self.g1, 64, dt=torch.float32)
         # the whole fc chain of a training step (fc1 forward, head, fc backward) as ONE persistent
         # launch (cnn_fc.hip) instead of three: B <= 256, 256 co-resident workgroups (one per CU, so
-        # not when several ranks share a GPU), not beside the fc-branch graph.  DMLC_FC_FUSED=1 on.
+        # not when several ranks share a GPU), not beside the fc-branch graph.  DMLC_FC_FUSED=0 off.
         local_ = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
         ndev_ = torch.cuda.device_count() if dev.type == "cuda" else 0
         cus_ = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
         self.fc_fused = (B <= 256 and cus_ >= 256 and local_ <= max(1, ndev_)
                          and os.environ.get("DMLC_FC_BRANCH", "0") != "1"
-                         and os.environ.get("DMLC_FC_FUSED", "0") == "1")
+                         and os.environ.get("DMLC_FC_FUSED", "1") != "0")
         self.h1part8 = z(8, B, 384, dt=torch.float32) if self.fc_fused else None
         self.fc_sync = torch.zeros(20 * 32, dtype=torch.int32, device=dev)
         self._fc_src = None
