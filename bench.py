@@ -123,6 +123,14 @@ def parse():
     ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
                     help="fp8 = OCP e4m3 MFMA conv2 forward with delayed per-tensor scaling (config 5)")
     ap.add_argument("--dataset-size", type=int, default=50000)
+    # The timed steps must train a LIVE network.  With the reference's lr 0.1 on raw 0..255 pixels and
+    # random labels the weights are NaN within ~300 steps (every activation zero: profiles/
+    # r4_settle_probe.jsonl), and with the reference's ReLU on the logits (D4) the logits die and every
+    # gradient is exactly zero.  lr 1e-4 without the logit ReLU keeps activations AND gradients live
+    # (loss 2.71 -> 2.46 over 2k steps).  The step time is the same in all of these regimes (80.5-82 us
+    # at B=256 in every window of the probe): the number does not depend on it, but the run is valid.
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--relu-logits", action="store_true", help="the reference's ReLU on the logits (D4)")
     return ap.parse_args()
 
 
@@ -137,12 +145,13 @@ def build_fused(args, info, data, labels):
     if args.model == "resnet20":
         from dmlc.engine.fused_resnet import FusedResNetEngine
         eng = FusedResNetEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
-                                rank=info.rank, seed=0, lr=0.01, comm_dtype=args.comm_dtype,
+                                rank=info.rank, seed=0, lr=min(args.lr, 0.01), comm_dtype=args.comm_dtype,
                                 allreduce=args.allreduce, capture_comm=_capture_comm(args))
         return eng, eng.step, (None if args.no_graph else lambda: eng.capture(args.steps_per_graph))
     from dmlc.engine.fused import FusedCifarEngine
     eng = FusedCifarEngine(args.batch, data, labels, device=info.device, world_size=info.world_size,
-                           rank=info.rank, seed=0, comm_dtype=args.comm_dtype, dtype=args.dtype,
+                           rank=info.rank, seed=0, lr=args.lr, relu_logits=args.relu_logits,
+                           comm_dtype=args.comm_dtype, dtype=args.dtype,
                            allreduce=args.allreduce, capture_comm=_capture_comm(args),
                            dp_schedule="serial" if args.dp_schedule == "auto" else args.dp_schedule)
     step = eng.step
@@ -158,7 +167,7 @@ def build_eager(args, info, data, labels):
     hipf32 = args.impl == "hipf32"
     tr = EagerTrainer(args.model, args.batch, data, labels, device=info.device, world_size=info.world_size,
                       rank=info.rank, dtype="fp32" if hipf32 or args.dtype == "fp32" else "bf16", crop=args.crop,
-                      lr=0.01 if args.model == "resnet20" else 0.1, graph=args.eager_graph or hipf32,
+                      lr=min(args.lr, 0.01), relu_logits=args.relu_logits, graph=args.eager_graph or hipf32,
                       backend="hip_f32" if hipf32 else "torch")
     return tr, tr.step, None
 
@@ -256,6 +265,18 @@ def main():
     if info.backend == "nccl" and seen > 1:
         comm["rccl_env"] = D.rccl_env()
 
+    # the network the timed steps trained: finite weights, the last step's loss (device stats ring)
+    net = {"lr": args.lr, "relu_logits": bool(args.relu_logits)}
+    master = getattr(eng, "master", None)
+    if master is not None:
+        net["finite"] = bool(torch.isfinite(master).all())
+        if not net["finite"]:
+            raise SystemExit("bench: the weights went non-finite during the run (invalid measurement)")
+    if hasattr(eng, "read_stats") and gs0 is not None:
+        try:
+            net["loss_last_step"] = round(float(eng.read_stats(device_step())["loss"]), 4)
+        except Exception:
+            pass
     n = info.world_size
     ms = elapsed * 1000.0 / args.steps
     gbatch = args.batch * n
@@ -287,6 +308,7 @@ def main():
                 "comm_dtype": args.comm_dtype,
                 "comm": comm,
                 "graph_warmup_steps": graph_warm,
+                "network": net,
                 "steps_per_graph": args.steps_per_graph if capture is not None else None,
             },
         }

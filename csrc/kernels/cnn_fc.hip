@@ -243,6 +243,7 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
   const bool rv = li < RB;
   const int rr = rv ? li : RB;
   DMLC_STAMP(DMLC_TK_HEAD, 0);
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 0);
 
   // --- everything the seam does not gate, issued first: fc2 weights (18 x 16 B per thread), the
   //     small operands, the labels
@@ -325,6 +326,7 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
   }
   lds_barrier();
 
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 1);            // (head-internal phase stamps: the conv2_fwd row)
   // (c)+(d) wave 7, in registers: logits = [relu](h2 W3 + b3) as one 16x16 tile (K = 192), lane
   //   (g, li) holding classes 4g..4g+3 of row li; the row max / argmax / exp-sum meet across the
   //   four lane groups by two xor shuffles -- softmax cross-entropy, accuracy and dlogits without an
@@ -383,6 +385,7 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
   }
   lds_barrier();
 
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 2);
   // (e) dh2 = (dl W3^T) * (h2 > 0), K = 32 (one MFMA)
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -395,6 +398,7 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
   }
   lds_barrier();
 
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 3);
   // (f) dh1 = (dh2 W2^T) * (h1 > 0): 24 k tiles, 3 per wave, K = 192 (transposed fc2 fragments);
   //     the rows go through LDS over the dead W2 image to the write-through stores below
   f32x4 dacc[3];

@@ -65,7 +65,8 @@ def cnn_local_errors(eng, data, labels, idx):
 
     # fc1 forward (split-K partial slabs, summed by the head)
     p2 = eng.p2[:B].reshape(B, 2304).float()
-    h1pre = eng.h1part[:, :B].sum(0)
+    # fc1 split-K partials: the persistent fc chain's (8 slices) or the grouped GEMM's
+    h1pre = (eng.h1part8 if eng.fc_fused else eng.h1part)[:, :B].sum(0)
     out["fc1_fwd"] = _rel(h1pre, p2 @ bfw["full_weight_1"])
 
     # head: fc1 bias+ReLU, fc2, fc3 (+ReLU logits), softmax-xent, dlogits, dh2, dh1

@@ -29,6 +29,8 @@ NK, NB, NS = 8, 1024, 8
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--raw", default="", help="comma list of kernel names whose per-block stamps (us since "
+                    "the step's first stamp, -1 = not stamped) are dumped too, as raw_<name>")
     ap.add_argument("--graph", action="store_true",
                     help="time the second step of a 2-step graph chain (kernels back to back, as in bench.py)")
     a = ap.parse_args()
@@ -99,6 +101,10 @@ def main():
                     rec[f"role_{name}_work_by_xcd"] = [round(float(d[(ids % 8) == x].mean()), 2) if ((ids % 8) == x).any()
                                                        else None for x in range(8)]
         out[NAMES[k]] = rec
+        if NAMES[k] in a.raw.split(","):
+            raw = t[k]
+            out["raw_" + NAMES[k]] = [[round(float((x - base) / 100.0), 2) if x > 0 else -1 for x in row]
+                                      for row in raw[: int(np.nonzero(raw[:, 0] > 0)[0].max()) + 1]]
     print(json.dumps(out, indent=1))
 
 

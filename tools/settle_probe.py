@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--learnable", action="store_true", help="learnable synthetic labels instead of random")
+    ap.add_argument("--no-relu-logits", action="store_true", help="no ReLU on the logits (reference D4 off)")
     a = ap.parse_args()
     g = torch.Generator().manual_seed(0)
     if a.learnable:
@@ -39,7 +40,8 @@ def main():
     else:
         data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
         labels = torch.randint(0, 10, (50000,), dtype=torch.int32, generator=g)
-    eng = FusedCifarEngine(a.batch, data.cuda(), labels.cuda(), device="cuda", seed=0, lr=a.lr)
+    eng = FusedCifarEngine(a.batch, data.cuda(), labels.cuda(), device="cuda", seed=0, lr=a.lr,
+                           relu_logits=not a.no_relu_logits)
     for _ in range(3):
         eng.step()
     eng.capture(32)
@@ -59,6 +61,9 @@ def main():
                "loss": st["loss"], "acc": st["accuracy"], "lr": st["lr"],
                "p2_zero": round(float((eng.p2 == 0).float().mean()), 4),
                "p1_zero": round(float((eng.p1 == 0).float().mean()), 4),
+               "dl_nonzero": round(float((eng.dl[:, :10] != 0).float().mean()), 4),
+               "dp2_nonzero": round(float((eng.dp2 != 0).float().mean()), 4),
+               "dy2_nonzero": round(float((eng.dy2 != 0).float().mean()), 4),
                "w_absmax": float(eng.master.abs().max()), "finite": bool(torch.isfinite(eng.master).all())}
         print(json.dumps(rec), flush=True)
 
