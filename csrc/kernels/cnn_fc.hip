@@ -447,7 +447,14 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
 // db1 / db2 / db3.
 // =================================================================================================
 struct CTask { int kind, i, j; };   // kind 0 dp2, 1 dW1, 2 dW2, 3 dW3
+DEV CTask ctask_(const DmlcFcArgs& a, int t);
+// (wave-uniform fields: held in SGPRs, so the task branches are uniform and no kernel argument has
+// to live in divergent-code VGPRs -- without this hipcc copied the argument block to scratch)
 DEV CTask ctask(const DmlcFcArgs& a, int t) {
+  const CTask T = ctask_(a, t);
+  return {__builtin_amdgcn_readfirstlane(T.kind), __builtin_amdgcn_readfirstlane(T.i), __builtin_amdgcn_readfirstlane(T.j)};
+}
+DEV CTask ctask_(const DmlcFcArgs& a, int t) {
   const int ndp2 = a.mtiles * 18;
   if (t < ndp2) return {0, t / 18, t % 18};
   t -= ndp2;
@@ -586,28 +593,74 @@ DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid) {
 }
 
 // dW1 / dW2 / dW3: 128 x 64 tile of A^T B over the batch (A, B: bf16 [B][lda], [B][ldb])
+// One 16-B chunk per thread of a 64-row tile of an m-major hand-off operand: rows 64 m + (tid >> 3),
+// columns c0 + 8 (tid & 7) of a bf16 [B][ld] matrix (sc1; rows >= B / columns >= ncol read as zero)
+// a pointer the compiler cannot prove wave-uniform, made so (buffer descriptors live in SGPRs; a
+// VGPR descriptor makes hipcc wrap every buffer op in a waterfall loop -- guide T20)
+DEV const void* uni(const void* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo);
+}
+DEV uint4 ld_mtile(const void* base, int ld, int c0, int ncol, int B, int m, int tid) {
+  const int rw = 64 * m + (tid >> 3), col = c0 + 8 * (tid & 7);
+  const bool ok = rw < B && col < ncol;
+  const uint4 v = ld16(buf_rsrc(base), ok ? (uint32_t)(rw * ld + col) * 2 : 0u);
+  return ok ? v : make_uint4(0, 0, 0, 0);
+}
+DEV void st_mtile(bf16* img, int m, const uint4& v, int tid) {
+  *reinterpret_cast<uint4*>(img + mz(64 * m + (tid >> 3), 8 * (tid & 7))) = v;
+}
+
 DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t step, char* smem, int tid) {
   bf16* sa = reinterpret_cast<bf16*>(smem + L_W1_A);
   bf16* sb = reinterpret_cast<bf16*>(smem + L_W1_B);
   const int Kpad = (a.B + 31) & ~31;
-  consume(cntBall(a), (unsigned)(a.B / FC_RB), a.err);
+  const int m0 = 128 * T.i, n0 = 64 * T.j;
+  // dW1 = p2^T dh1 (A staged before the seam), dW2 = h1^T dh2, dW3 = h2^T dl (10 columns)
+  const int M = T.kind == 1 ? 2304 : T.kind == 2 ? 384 : 192;
+  const int N = T.kind == 1 ? 384 : T.kind == 2 ? 192 : 10;
+  const int ldc = N;
+  // The K (= batch) range arrives one 64-row tile at a time: wait for that tile's head blocks only
+  // (its own counter: the polls spread over mtiles words instead of all hitting the total) and
+  // issue its operand loads before waiting for the next tile.  The barrier between is an s_barrier
+  // (lds_barrier), not __syncthreads: that would drain the loads already in flight.
+  // (the operand of each kind, selected branch-free: the same three loads per tile for every kind)
+  // (every candidate made opaque BEFORE the select: a select between two argument fields becomes a
+  // load through a selected address into the argument block, and hipcc then copies the whole block
+  // to scratch)
+  const void* pa = T.kind == 2 ? uni(a.h1) : uni(a.h2);
+  const void* pb = T.kind == 1 ? uni(a.dh1) : T.kind == 2 ? uni(a.dh2) : uni(a.dl);
+  const int lda = __builtin_amdgcn_readfirstlane(T.kind == 2 ? 384 : 192);
+  const int ldb = __builtin_amdgcn_readfirstlane(T.kind == 1 ? 384 : T.kind == 2 ? 192 : 16);
+  const int cb = T.kind == 3 ? 0 : n0;
+  const bool need_a = T.kind != 1;
+  // (written out per tile: with the spin inside, a loop over the tiles stayed rolled and its register
+  // arrays went to scratch)
+  struct T3 { uint4 a0, a1, b; };
+  auto tile = [&](int m) __attribute__((always_inline)) {
+    const bool on = m < a.mtiles;
+    if (on && tid == 0) wait_ge(cntB(a, m), (unsigned)(min(64, a.B - 64 * m) / FC_RB), a.err);
+    lds_barrier();
+    const int Bm = on ? a.B : 0;            // a tile past the batch reads nothing (zeros)
+    T3 r;
+    r.b = ld_mtile(pb, ldb, cb, ldb, Bm, m, tid);
+    r.a0 = ld_mtile(pa, lda, m0, need_a ? lda : 0, Bm, m, tid);
+    r.a1 = ld_mtile(pa, lda, m0 + 64, need_a ? lda : 0, Bm, m, tid);
+    return r;
+  };
+  auto put = [&](int m, const T3& r) __attribute__((always_inline)) {
+    if (64 * m + (tid >> 3) < Kpad) {
+      st_mtile(sb, m, r.b, tid);
+      if (need_a) {
+        st_mtile(sa, m, r.a0, tid);
+        st_mtile(sa + 256 * 64, m, r.a1, tid);
+      }
+    }
+  };
+  const T3 t0 = tile(0), t1 = tile(1), t2 = tile(2), t3 = tile(3);
   DMLC_STAMP(DMLC_TK_GEMM, 3);
-  int M, N, ldc, m0 = 128 * T.i, n0 = 64 * T.j;
-  float* C;
-  if (T.kind == 1) {                           // dW1 = p2^T dh1 (A staged before the seam)
-    stage_m_sc1(a.dh1, 384, n0, 384, a.B, sb, Kpad, tid);
-    M = 2304; N = 384; ldc = 384; C = a.gw1;
-  } else if (T.kind == 2) {                    // dW2 = h1^T dh2
-    stage_m_sc1(a.h1, 384, m0, 384, a.B, sa, Kpad, tid);
-    stage_m_sc1(a.h1, 384, m0 + 64, 384, a.B, sa + 256 * 64, Kpad, tid);
-    stage_m_sc1(a.dh2, 192, n0, 192, a.B, sb, Kpad, tid);
-    M = 384; N = 192; ldc = 192; C = a.gw2;
-  } else {                                     // dW3 = h2^T dl (10 valid columns)
-    stage_m_sc1(a.h2, 192, m0, 192, a.B, sa, Kpad, tid);
-    stage_m_sc1(a.h2, 192, m0 + 64, 192, a.B, sa + 256 * 64, Kpad, tid);
-    stage_m_sc1(a.dl, 16, 0, 16, a.B, sb, Kpad, tid);
-    M = 192; N = 10; ldc = 10; C = a.gw3;
-  }
+  put(0, t0); put(1, t1); put(2, t2); put(3, t3);
   __syncthreads();
   const int w = wave_id(), lane = tid & 63, g = lane >> 4, li = lane & 15;
   // bias gradient of the B columns (first M tile only): 8 row groups x 64 columns, fixed order
@@ -628,7 +681,7 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
     float sum = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) sum += red[k * 64 + tid];
-    (T.kind == 1 ? a.gb1 : T.kind == 2 ? a.gb2 : a.gb3)[n0 + tid] = sum;
+    ((float*)(T.kind == 1 ? uni(a.gb1) : T.kind == 2 ? uni(a.gb2) : uni(a.gb3)))[n0 + tid] = sum;
   }
   float* ct = reinterpret_cast<float*>(smem);  // [128][68]
   acc.to_lds(ct, CT_LD, 32 * (w >> 1), 32 * (w & 1), g, li);
@@ -657,6 +710,7 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
     const int m = m0 + rr, n = n0 + cc;
     if (m >= M || n >= N) continue;
     const float4 v = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
+    float* C = (float*)(T.kind == 1 ? uni(a.gw1) : T.kind == 2 ? uni(a.gw2) : uni(a.gw3));
     if (ldc % 4 == 0 && n + 4 <= N) {
       *reinterpret_cast<float4*>(C + (size_t)m * ldc + n) = v;
     } else {
