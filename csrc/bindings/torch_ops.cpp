@@ -306,6 +306,7 @@ static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10
   const int p2b = check_part2(part2, g2);
   check(partb2, "partb2", at::kFloat, {g2, 64});
   DmlcWgradArgs a;
+  memset(&a, 0, sizeof(a));                      // (fc_in_launch off unless wgrad_sgd sets it)
   a.w1.data = data.data_ptr<uint8_t>(); a.w1.src = index_src(idx, counter, period, B);
   check_order_fits(a.w1.src, data.size(0));
   a.w1.cy = (int)cy; a.w1.cx = (int)cx;
@@ -475,7 +476,7 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
               const Tensor& dh2, const Tensor& loss_part, const Tensor& correct_part, const Tensor& dp2,
               const Tensor& gw1, const Tensor& gw2, const Tensor& gw3, const Tensor& gb1, const Tensor& gb2,
               const Tensor& gb3, bool fuse_sgd, at::ArrayRef<double> sched, int64_t nvalid, const Tensor& step,
-              const c10::optional<Tensor>& step_copy, const Tensor& sync, const Tensor& err) {
+              const c10::optional<Tensor>& step_copy, const Tensor& sync, const Tensor& err, bool dw_tasks) {
   const int64_t B = p2.size(0);
   TORCH_CHECK(B >= 16 && B <= 256 && B % 16 == 0, "fc_chain: batch must be a multiple of 16 in [16, 256]");
   check(p2, "p2", at::kBFloat16, {B, 2304});
@@ -524,7 +525,8 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
   a.dp2 = dp2.data_ptr();
   a.gw1 = gw1.data_ptr<float>(); a.gw2 = gw2.data_ptr<float>(); a.gw3 = gw3.data_ptr<float>();
   a.gb1 = gb1.data_ptr<float>(); a.gb2 = gb2.data_ptr<float>(); a.gb3 = gb3.data_ptr<float>();
-  a.fuse_sgd = fuse_sgd;
+  a.fuse_sgd = fuse_sgd ? 1 : 0;
+  a.dw_tasks = dw_tasks ? 1 : 0;
   a.lr0 = (float)sched[0]; a.decay = (float)sched[1]; a.decay_steps = (float)sched[2];
   a.staircase = sched[3] != 0.0; a.warmup = (float)sched[4]; a.grad_scale = (float)sched[5];
   a.step = step.data_ptr<int64_t>();
@@ -658,7 +660,8 @@ void sgd(DMLC_SGD_PARAMS) {
 // (whose slab tensors must be the wgrad's).
 void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
                int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& p1, const Tensor& dy2,
-               int64_t groups2, const Tensor& xraw, const Tensor& bar, DMLC_SGD_PARAMS) {
+               int64_t groups2, const Tensor& xraw, const Tensor& bar, DMLC_SGD_PARAMS,
+               const c10::optional<at::TensorList> fc_acts) {
   DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
                                groups2, xraw, true);
   TORCH_CHECK((mode == 0 && fc1_fused && step_rd.has_value() && roles == 0 && finalize &&
@@ -670,6 +673,38 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   a.bar = reinterpret_cast<unsigned int*>(bar.data_ptr<int>());
   static const bool helpers = [] { const char* e = getenv("DMLC_WGRAD_HELPERS"); return !(e && e[0] == '0'); }();
   a.helpers = helpers ? 1 : 0;
+  a.fc_in_launch = 0;
+  memset(&a.fc, 0, sizeof(a.fc));
+  if (fc_acts.has_value()) {
+    // the fc weight-gradient tiles + every fc SGD run in this launch (fc_common.h): fc_acts = the fc
+    // chain's activations {p2 [B][2304], h1, h2, dl, dh1, dh2}; masters / shadows from the SGD args
+    const at::TensorList t = *fc_acts;
+    TORCH_CHECK(t.size() == 6 && mode == 0 && fc1_fused, "wgrad_sgd: fc_acts = {p2, h1, h2, dl, dh1, dh2} in mode 0");
+    const int64_t B = t[0].size(0);
+    TORCH_CHECK(B >= 16 && B <= 256 && B % 16 == 0, "wgrad_sgd: fc tiles need a batch in [16, 256]");
+    check(t[0], "p2", at::kBFloat16, {B, 2304});
+    check(t[1], "h1", at::kBFloat16, {B, 384});
+    check(t[2], "h2", at::kBFloat16, {B, 192});
+    check(t[3], "dl", at::kBFloat16, {B, 16});
+    check(t[4], "dh1", at::kBFloat16, {B, 384});
+    check(t[5], "dh2", at::kBFloat16, {B, 192});
+    check(fc2n, "fc2n", at::kBFloat16, {384, 192});
+    check(fc2t, "fc2t", at::kBFloat16, {192, 384});
+    DmlcFcArgs& f = a.fc;
+    f.B = (int)B; f.nvalid = (int)B; f.mtiles = (int)((B + 63) / 64);
+    f.p2 = t[0].data_ptr(); f.w1 = fc1n.data_ptr();
+    f.h1 = t[1].data_ptr(); f.h2 = t[2].data_ptr(); f.dl = t[3].data_ptr(); f.dh1 = t[4].data_ptr();
+    f.dh2 = t[5].data_ptr();
+    float* m = master.data_ptr<float>();
+    f.gw1 = m + off[4]; f.mb1 = m + off[5]; f.mw2 = m + off[6]; f.mb2 = m + off[7]; f.mw3 = m + off[8];
+    f.mb3 = m + off[9];
+    f.fc2n = fc2n.data_ptr(); f.fc2t = fc2t.data_ptr(); f.fc3t = fc3t.data_ptr(); f.fc3d = fc3d.data_ptr();
+    f.fuse_sgd = 2; f.dw_tasks = 1;
+    f.lr0 = (float)lr0; f.decay = (float)decay; f.decay_steps = (float)decay_steps; f.staircase = staircase;
+    f.warmup = (float)warmup; f.grad_scale = (float)grad_scale;
+    f.err = a.bar + 10 * 32;
+    a.fc_in_launch = 1;
+  }
   c10::DeviceGuard guard(dp1.device());
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
 }
@@ -711,7 +746,7 @@ TORCH_LIBRARY(dmlc, m) {
         "bool relu_logits, Tensor(c!) h1, Tensor(d!) h2, Tensor(e!) dl, Tensor(f!) dh1, Tensor(g!) dh2, "
         "Tensor(h!) loss_part, Tensor(i!) correct_part, Tensor(j!) dp2, Tensor(k!) gw1, Tensor(l!) gw2, "
         "Tensor(m!) gw3, Tensor(n!) gb1, Tensor(o!) gb2, Tensor(p!) gb3, bool fuse_sgd, float[] sched, "
-        "int nvalid, Tensor step, Tensor(q!)? step_copy, Tensor(r!) sync, Tensor(s!) err) -> ()");
+        "int nvalid, Tensor step, Tensor(q!)? step_copy, Tensor(r!) sync, Tensor(s!) err, bool dw_tasks=True) -> ()");
   m.def("wgrad_sgd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor p1, Tensor dy2, int groups2, Tensor xraw, Tensor(z!) bar, "
         "Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor(r!) part1, Tensor(s!) partb1, "
@@ -720,7 +755,7 @@ TORCH_LIBRARY(dmlc, m) {
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
         "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
-        "bool fc1_fused=False, Tensor? step_rd=None) -> ()");
+        "bool fc1_fused=False, Tensor? step_rd=None, Tensor[]? fc_acts=None) -> ()");
   m.def("sgd(Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor part1, Tensor partb1, "
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "

@@ -195,7 +195,13 @@ struct DmlcFcArgs {
   void* dp2;                         // bf16 [B][2304] out: the conv backward's input
   float* gw1;                        // fuse_sgd: fc1 fp32 master (updated); else the fc1 weight gradient
   float* gw2; float* gw3; float* gb1; float* gb2; float* gb3;   // gradients (flat grad views)
+  // fuse_sgd: 0 every fc gradient to the flat gradient; 1 the fc1 weights updated in the dW1 epilogue
+  // (gw1 = master), the rest gradients; 2 (the weight-gradient launch's apply mode) every fc
+  // parameter updated in its dW epilogue: masters mw2 / mw3 / mb1..3 and the bf16 shadows below
   int fuse_sgd;
+  float* mw2; float* mw3; float* mb1; float* mb2; float* mb3;
+  void* fc2n; void* fc2t; void* fc3t; void* fc3d;   // bf16 [384][192], [192][384], [16][192], [192][32]
+  int dw_tasks;                      // the fc-chain launch runs the dW tasks (0: the wgrad launch does)
   float lr0, decay, decay_steps, warmup, grad_scale; int staircase;
   const int64_t* step; int64_t* step_copy;             // device step counter; copy for the SGD reader
   unsigned int* sync;                // >= 19 * 32 zeroed uints (counters re-arm themselves)
@@ -265,6 +271,11 @@ struct DmlcWgradArgs {
   unsigned int* bar;
   int helpers;              // apply mode: idle conv1 blocks help reduce the conv2 slabs (DMLC_WGRAD_HELPERS=0 off)
   DmlcSgdArgs sgd;
+  // apply mode with the fc chain (fc_in_launch): the conv1 blocks, whose conv1 work ends ~8 us before
+  // the conv2 blocks', also run the fc weight-gradient tiles (dW1 / dW2 / dW3 + bias gradients,
+  // fc_common.h) with every fc parameter's SGD in their epilogues (fc.fuse_sgd = 2): no fc SGD roles
+  int fc_in_launch;
+  DmlcFcArgs fc;
 };
 
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);

@@ -24,39 +24,9 @@
 // outputs (cntB) plus a total; the last block to finish re-arms them (zero) for the next launch.
 // Every spin is bounded and sets the sticky error word (the engine's wgrad barrier error word) --
 // all 256 blocks must be co-resident (one per CU: ~150 KB of LDS each; host-checked).
-#include "common.h"
-#include "api.h"
+#include "fc_common.h"
 
 namespace dmlc {
-
-// typed views of the DmlcFcArgs pointers
-DEV const bf16* P2(const DmlcFcArgs& a) { return reinterpret_cast<const bf16*>(a.p2); }
-DEV bf16* W1S(const DmlcFcArgs& a) { return reinterpret_cast<bf16*>(a.w1); }
-DEV bf16* DP2(const DmlcFcArgs& a) { return reinterpret_cast<bf16*>(a.dp2); }
-
-constexpr int FT = 512;                        // 8 waves
-constexpr int FC_BLOCKS = 256;
-constexpr int FC_S = 8;                        // fc1 forward K split (288 = 9 k-steps each)
-constexpr int FC_KS = 2304 / FC_S;
-constexpr int FC_RB = 4;                       // head rows per block
-
-// ---- LDS images ---------------------------------------------------------------------------------
-// k-major [rows][stride] bf16 with stride = 16 (mod 128) elements: a row is 8 banks further on, so
-// the 16 lanes of every ds_read_b128 lane group hit 64 distinct banks (as cnn_gemm.hip's KC_LD)
-constexpr int KST_A = 400;                     // K <= 384 (fc1 forward slice 288, dp2 384)
-// m-major [k rows][64 cols] bf16, unpadded 128-B rows, 16-B chunk index XORed by row bits 1 and 3
-// (cnn_gemm.hip mswz: conflict-free ds_read_b64_tr_b16 and conflict-free 16-B stores)
-DEV int mz(int row, int col) {
-  const int f = 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
-  return row * 64 + (((col >> 3) ^ f) << 3) + (col & 7);
-}
-DEV bf16x8 kfrag(const bf16* img, int stride, int r0, int kk, int g, int li) {
-  return lds_b128(img + (r0 + li) * stride + kk * 32 + 8 * g);
-}
-DEV bf16x8 mfrag(const bf16* img, int c0, int kk, int g, int li) {
-  const int q = li >> 2, p = li & 3;
-  return tr_frag(img + mz(kk * 32 + 8 * g + q, c0 + 4 * p), img + mz(kk * 32 + 8 * g + 4 + q, c0 + 4 * p));
-}
 
 // head LDS (cnn_head.hip layouts): fc2 weights [192 n][384 k] swizzled, activations of RB rows + a
 // zero row
@@ -73,88 +43,9 @@ struct HL {
   static constexpr int LG = DL + (FC_RB + 1) * DL_LD * 2;
   static constexpr int BYTES = LG + 16 * 17 * 4;
 };
-// GEMM task LDS: dp2 = dh1 rows [64][400] + W1 rows [128][400]; dW1 = p2 columns 2 x [256][64] +
-// dh1 columns [256][64]; fc1 forward = p2 rows [64][400] + W1 slice [288][64]
-constexpr int L_DP2_A = 0, L_DP2_B = 64 * KST_A * 2;
-constexpr int L_DP2_END = L_DP2_B + 128 * KST_A * 2;
-constexpr int L_W1_A = 0, L_W1_B = 2 * 256 * 64 * 2;
-constexpr int L_FWD_A = 0, L_FWD_B = 64 * KST_A * 2;
-constexpr int L_RED = L_W1_B + 256 * 64 * 2;   // [8][64] fp32 bias-gradient partials (dW tasks)
 constexpr int FC_LDS = L_DP2_END > HL::BYTES ? L_DP2_END : HL::BYTES;
 static_assert(FC_LDS <= 160 * 1024, "fc chain LDS exceeds a CU");
 static_assert(L_FWD_B + FC_KS * 64 * 2 <= FC_LDS && L_RED + 8 * 64 * 4 <= FC_LDS, "task images");
-
-// ---- sync words (DmlcFcArgs::sync, uints, each counter on its own 128-B line) --------------------
-DEV unsigned* cntA(const DmlcFcArgs& a, int m) { return a.sync + 32 * m; }          // m < 4
-DEV unsigned* cntB(const DmlcFcArgs& a, int m) { return a.sync + 32 * (4 + m); }    // m < 4
-DEV unsigned* cntBall(const DmlcFcArgs& a) { return a.sync + 32 * 8; }
-// a.sync + 32 * 10 .. + 32 * 19: the two-level end-of-launch ticket (common.h last_arrival)
-
-DEV unsigned ld_relaxed(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-// one lane: spin until *p >= target (bounded; on give-up the sticky error word is set)
-DEV void wait_ge(unsigned* p, unsigned target, unsigned* err) {
-  for (unsigned it = 0; ld_relaxed(p) < target; ++it) {
-    if (it > (1u << 20)) {
-      __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-// every storing wave drains its write-through stores, the workgroup meets, one lane signals
-DEV void publish(unsigned* c1, unsigned* c2) {
-  wait_vm_all();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(c1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c2) __hip_atomic_fetch_add(c2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-// one lane waits, then the workgroup meets (every later load of the handed-off bytes is sc1)
-DEV void consume(unsigned* c, unsigned target, unsigned* err) {
-  if (threadIdx.x == 0) wait_ge(c, target, err);
-  __syncthreads();
-}
-
-DEV uint4 ld16(rsrc_t r, uint32_t off) {      // sc1 16-B load (hand-off bytes)
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSC1));
-}
-DEV void st16(rsrc_t r, uint32_t off, const uint4& v) {   // sc1 16-B store (hand-off bytes)
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, kSC1);
-}
-
-// ---- one MFMA k-step accumulate of a 32x32 wave tile --------------------------------------------
-struct Acc {
-  f32x4 c[2][2];
-  MDEV void zero() {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) { c[i][0] = zero4(); c[i][1] = zero4(); }
-  }
-  MDEV void mma(const bf16x8& a0, const bf16x8& a1, const bf16x8& b0, const bf16x8& b1) {
-    c[0][0] = mfma16(a0, b0, c[0][0]);
-    c[0][1] = mfma16(a0, b1, c[0][1]);
-    c[1][0] = mfma16(a1, b0, c[1][0]);
-    c[1][1] = mfma16(a1, b1, c[1][1]);
-  }
-  // into an fp32 LDS tile [rows][ld]: acc[i][j][r] = C[r0 + 16i + 4g + r][c0 + 16j + li]
-  MDEV void to_lds(float* t, int ld, int r0, int c0, int g, int li) const {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) t[(r0 + 16 * i + 4 * g + r) * ld + c0 + 16 * j + li] = c[i][j][r];
-  }
-  MDEV void add_lds(float* t, int ld, int r0, int c0, int g, int li) const {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) t[(r0 + 16 * i + 4 * g + r) * ld + c0 + 16 * j + li] += c[i][j][r];
-  }
-};
-constexpr int CT_LD = 68;                     // fp32 staging rows (64 + 4): conflict-free 4-B writes
 
 // =================================================================================================
 // Phase A: fc1 forward task t = (mt, nt, s): h1part[s][64 mt .. +64][64 nt .. +64] =
@@ -440,291 +331,6 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
   DMLC_STAMP(DMLC_TK_HEAD, 5);
 }
 
-// =================================================================================================
-// Phase C tasks.  Types (in task order): dp2 (64 rows x 128 k1 of dp2 = dh1 W1^T, K = 384),
-// dW1 (128 k1 x 64 n of p2^T dh1, K = B; fused SGD or gradient), dW2 (128 x 64 of h1^T dh2),
-// dW3 (128 x 16 of h2^T dl); the first M tile of each dW also sums its dh1 / dh2 / dl columns into
-// db1 / db2 / db3.
-// =================================================================================================
-struct CTask { int kind, i, j; };   // kind 0 dp2, 1 dW1, 2 dW2, 3 dW3
-DEV CTask ctask_(const DmlcFcArgs& a, int t);
-// (wave-uniform fields: held in SGPRs, so the task branches are uniform and no kernel argument has
-// to live in divergent-code VGPRs -- without this hipcc copied the argument block to scratch)
-DEV CTask ctask(const DmlcFcArgs& a, int t) {
-  const CTask T = ctask_(a, t);
-  return {__builtin_amdgcn_readfirstlane(T.kind), __builtin_amdgcn_readfirstlane(T.i), __builtin_amdgcn_readfirstlane(T.j)};
-}
-DEV CTask ctask_(const DmlcFcArgs& a, int t) {
-  const int ndp2 = a.mtiles * 18;
-  if (t < ndp2) return {0, t / 18, t % 18};
-  t -= ndp2;
-  if (t < 108) return {1, t / 6, t % 6};
-  t -= 108;
-  if (t < 9) return {2, t / 3, t % 3};
-  t -= 9;
-  if (t < 2) return {3, t, 0};
-  return {-1, 0, 0};
-}
-// (the bias gradients ride along: the i == 0 tiles of dW1 / dW2 / dW3 hold dh1 / dh2 / dl columns in
-// LDS and sum them -- three column-sum tasks of their own were each a chain of dependent row loads)
-DEV int ctask_count(const DmlcFcArgs& a) { return a.mtiles * 18 + 108 + 9 + 2; }
-
-// what a dp2 / dW1 task stages before its seam: 12 x 16 B (W1 rows, or p2 columns) + 4 float4 of
-// the fp32 master (dW1 with the fused SGD); always the same number of loads (static vmcnt counts)
-struct PreRegs { uint4 v[12]; float4 m[4]; };
-// branch-free: every block issues the same 16 loads whatever its task (others read valid dummy
-// addresses and discard), so the forward task's waits count them statically
-DEV void pre_issue(const DmlcFcArgs& a, const CTask& T, int parity, PreRegs& R, int tid) {
-  const bf16* W1 = W1S(a) + (parity ? 884736 : 0);
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const int c = tid + i * FT;
-    const int rw0 = c / 48, kc0 = c - rw0 * 48;          // dp2: W1 rows [128 j .. +128][384]
-    const int rw1 = c >> 4, cc1 = c & 15;                // dW1: p2 columns [B rows][128 i .. +128]
-    const bool ok1 = T.kind == 1 && rw1 < a.B;
-    const bf16* p = T.kind == 0 ? W1 + (size_t)(128 * T.j + rw0) * 384 + 8 * kc0
-                                : ok1 ? P2(a) + (size_t)rw1 * 2304 + 128 * T.i + 8 * cc1 : P2(a);
-    R.v[i] = load_sel(reinterpret_cast<const uint4*>(p), reinterpret_cast<const uint4*>(P2(a)), T.kind == 0 || ok1);
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {                // master tile [128][64] fp32 of dW1 (fused SGD)
-    const int e = tid + u * FT, rr = e >> 4, cc = (e & 15) * 4;
-    const bool ok = T.kind == 1 && a.fuse_sgd;
-    R.m[u] = load_sel(reinterpret_cast<const float4*>(a.gw1 + (size_t)(128 * T.i + rr) * 384 + 64 * T.j + cc),
-                      reinterpret_cast<const float4*>(a.gw1), ok);
-  }
-}
-DEV void pre_store(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, char* smem, int tid) {
-  if (T.kind == 0) {
-    bf16* sb = reinterpret_cast<bf16*>(smem + L_DP2_B);
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      const int c = tid + i * FT, rw = c / 48, kc = c - rw * 48;
-      *reinterpret_cast<uint4*>(sb + rw * KST_A + 8 * kc) = R.v[i];
-    }
-  } else if (T.kind == 1) {
-    bf16* sa = reinterpret_cast<bf16*>(smem + L_W1_A);
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      const int c = tid + i * FT, rw = c >> 4, cc = c & 15;
-      if (rw < 256) *reinterpret_cast<uint4*>(sa + (cc >> 3) * 256 * 64 + mz(rw, 8 * (cc & 7))) = R.v[i];
-    }
-  }
-}
-
-// m-major hand-off operand [K = B rows][64 cols c0 ..] of a bf16 [B][ld] matrix (sc1 loads; columns
-// >= ncol and rows >= B read as zero) into the image at `img`
-// (all of a thread's loads in flight at once: Kpad <= 256 rows x 8 chunks = at most 4 per thread)
-DEV void stage_m_sc1(const void* base, int ld, int c0, int ncol, int B, bf16* img, int Kpad, int tid) {
-  const rsrc_t r = buf_rsrc(base);
-  uint4 v[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + i * FT, rw = c >> 3, col = c0 + 8 * (c & 7);
-    const bool ok = rw < B && col < ncol;
-    v[i] = ld16(r, ok ? (uint32_t)(rw * ld + col) * 2 : 0u);
-    if (!ok) v[i] = make_uint4(0, 0, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = tid + i * FT, rw = c >> 3;
-    if (rw < Kpad) *reinterpret_cast<uint4*>(img + mz(rw, 8 * (c & 7))) = v[i];
-  }
-}
-
-// 128 (M) x 64 (N) x K=Kpad product of two m-major images: A = na 64-col images (cols 64 x img),
-// B one 64-col image; waves: wm = w >> 1 (32-row quarter), wn = w & 1
-DEV void mma_128x64(const bf16* sa, const bf16* sb, int ksteps, Acc& acc, int w, int g, int li) {
-  const int wm = w >> 1, wn = w & 1;
-  const bf16* ia = sa + (wm >> 1) * 256 * 64;
-  const int ca = 32 * (wm & 1);
-  for (int kk = 0; kk < ksteps; ++kk)
-    acc.mma(mfrag(ia, ca, kk, g, li), mfrag(ia, ca + 16, kk, g, li), mfrag(sb, 32 * wn, kk, g, li),
-            mfrag(sb, 32 * wn + 16, kk, g, li));
-}
-
-DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid) {
-  bf16* sa = reinterpret_cast<bf16*>(smem + L_DP2_A);
-  bf16* sb = reinterpret_cast<bf16*>(smem + L_DP2_B);
-  const int mt = T.i, n0 = 128 * T.j;
-  const int rows = min(64, a.B - 64 * mt);
-  consume(cntB(a, mt), (unsigned)(rows / FC_RB), a.err);
-  DMLC_STAMP(DMLC_TK_GEMM, 3);
-  {
-    const rsrc_t r = buf_rsrc(a.dh1);
-    uint4 v[6];                                // dh1 rows [64][384]: 6 x 16 B per thread, all in flight
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int c = tid + i * FT, rw = c / 48, kc = c - rw * 48;
-      const bool ok = rw < rows;
-      v[i] = ld16(r, ok ? (uint32_t)((64 * mt + rw) * 384 + 8 * kc) * 2 : 0u);
-      if (!ok) v[i] = make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int c = tid + i * FT, rw = c / 48, kc = c - rw * 48;
-      *reinterpret_cast<uint4*>(sa + rw * KST_A + 8 * kc) = v[i];
-    }
-  }
-  __syncthreads();
-  const int w = wave_id(), lane = tid & 63, g = lane >> 4, li = lane & 15;
-  const int wm = w & 1, wn = w >> 1;
-  Acc acc;
-  acc.zero();
-#pragma unroll 4
-  for (int kk = 0; kk < 12; ++kk)
-    acc.mma(kfrag(sa, KST_A, 32 * wm, kk, g, li), kfrag(sa, KST_A, 32 * wm + 16, kk, g, li),
-            kfrag(sb, KST_A, 32 * wn, kk, g, li), kfrag(sb, KST_A, 32 * wn + 16, kk, g, li));
-  __syncthreads();
-  DMLC_STAMP(DMLC_TK_GEMM, 4);
-  float* ct = reinterpret_cast<float*>(smem);  // [64][132]
-  constexpr int LD = 132;
-  acc.to_lds(ct, LD, 32 * wm, 32 * wn, g, li);
-  __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {                // 64 x 128 bf16 = 2048 x 8-B pieces
-    const int e = tid + u * FT, rr = e >> 5, cc = (e & 31) * 4;
-    if (rr < rows) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(ct + rr * LD + cc);
-      st_maybe_nt<kNtGemm>(reinterpret_cast<bf16x4*>(DP2(a) + (size_t)(64 * mt + rr) * 2304 + n0 + cc),
-                           pack4(v[0], v[1], v[2], v[3]));
-    }
-  }
-}
-
-// dW1 / dW2 / dW3: 128 x 64 tile of A^T B over the batch (A, B: bf16 [B][lda], [B][ldb])
-// One 16-B chunk per thread of a 64-row tile of an m-major hand-off operand: rows 64 m + (tid >> 3),
-// columns c0 + 8 (tid & 7) of a bf16 [B][ld] matrix (sc1; rows >= B / columns >= ncol read as zero)
-// a pointer the compiler cannot prove wave-uniform, made so (buffer descriptors live in SGPRs; a
-// VGPR descriptor makes hipcc wrap every buffer op in a waterfall loop -- guide T20)
-DEV const void* uni(const void* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo);
-}
-DEV uint4 ld_mtile(const void* base, int ld, int c0, int ncol, int B, int m, int tid) {
-  const int rw = 64 * m + (tid >> 3), col = c0 + 8 * (tid & 7);
-  const bool ok = rw < B && col < ncol;
-  const uint4 v = ld16(buf_rsrc(base), ok ? (uint32_t)(rw * ld + col) * 2 : 0u);
-  return ok ? v : make_uint4(0, 0, 0, 0);
-}
-DEV void st_mtile(bf16* img, int m, const uint4& v, int tid) {
-  *reinterpret_cast<uint4*>(img + mz(64 * m + (tid >> 3), 8 * (tid & 7))) = v;
-}
-
-DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t step, char* smem, int tid) {
-  bf16* sa = reinterpret_cast<bf16*>(smem + L_W1_A);
-  bf16* sb = reinterpret_cast<bf16*>(smem + L_W1_B);
-  const int Kpad = (a.B + 31) & ~31;
-  const int m0 = 128 * T.i, n0 = 64 * T.j;
-  // dW1 = p2^T dh1 (A staged before the seam), dW2 = h1^T dh2, dW3 = h2^T dl (10 columns)
-  const int M = T.kind == 1 ? 2304 : T.kind == 2 ? 384 : 192;
-  const int N = T.kind == 1 ? 384 : T.kind == 2 ? 192 : 10;
-  const int ldc = N;
-  // The K (= batch) range arrives one 64-row tile at a time: wait for that tile's head blocks only
-  // (its own counter: the polls spread over mtiles words instead of all hitting the total) and
-  // issue its operand loads before waiting for the next tile.  The barrier between is an s_barrier
-  // (lds_barrier), not __syncthreads: that would drain the loads already in flight.
-  // (the operand of each kind, selected branch-free: the same three loads per tile for every kind)
-  // (every candidate made opaque BEFORE the select: a select between two argument fields becomes a
-  // load through a selected address into the argument block, and hipcc then copies the whole block
-  // to scratch)
-  const void* pa = T.kind == 2 ? uni(a.h1) : uni(a.h2);
-  const void* pb = T.kind == 1 ? uni(a.dh1) : T.kind == 2 ? uni(a.dh2) : uni(a.dl);
-  const int lda = __builtin_amdgcn_readfirstlane(T.kind == 2 ? 384 : 192);
-  const int ldb = __builtin_amdgcn_readfirstlane(T.kind == 1 ? 384 : T.kind == 2 ? 192 : 16);
-  const int cb = T.kind == 3 ? 0 : n0;
-  const bool need_a = T.kind != 1;
-  // (written out per tile: with the spin inside, a loop over the tiles stayed rolled and its register
-  // arrays went to scratch)
-  struct T3 { uint4 a0, a1, b; };
-  auto tile = [&](int m) __attribute__((always_inline)) {
-    const bool on = m < a.mtiles;
-    if (on && tid == 0) wait_ge(cntB(a, m), (unsigned)(min(64, a.B - 64 * m) / FC_RB), a.err);
-    lds_barrier();
-    const int Bm = on ? a.B : 0;            // a tile past the batch reads nothing (zeros)
-    T3 r;
-    r.b = ld_mtile(pb, ldb, cb, ldb, Bm, m, tid);
-    r.a0 = ld_mtile(pa, lda, m0, need_a ? lda : 0, Bm, m, tid);
-    r.a1 = ld_mtile(pa, lda, m0 + 64, need_a ? lda : 0, Bm, m, tid);
-    return r;
-  };
-  auto put = [&](int m, const T3& r) __attribute__((always_inline)) {
-    if (64 * m + (tid >> 3) < Kpad) {
-      st_mtile(sb, m, r.b, tid);
-      if (need_a) {
-        st_mtile(sa, m, r.a0, tid);
-        st_mtile(sa + 256 * 64, m, r.a1, tid);
-      }
-    }
-  };
-  const T3 t0 = tile(0), t1 = tile(1), t2 = tile(2), t3 = tile(3);
-  DMLC_STAMP(DMLC_TK_GEMM, 3);
-  put(0, t0); put(1, t1); put(2, t2); put(3, t3);
-  __syncthreads();
-  const int w = wave_id(), lane = tid & 63, g = lane >> 4, li = lane & 15;
-  // bias gradient of the B columns (first M tile only): 8 row groups x 64 columns, fixed order
-  float* red = reinterpret_cast<float*>(smem + L_RED);
-  const bool bias = T.i == 0;
-  if (bias) {
-    const int col = tid & 63, rg = tid >> 6;
-    float sum = 0.f;
-    for (int rw = rg; rw < Kpad; rw += 8) sum += (float)sb[mz(rw, col)];
-    red[rg * 64 + col] = sum;
-  }
-  Acc acc;
-  acc.zero();
-  mma_128x64(sa, sb, Kpad >> 5, acc, w, g, li);
-  __syncthreads();
-  DMLC_STAMP(DMLC_TK_GEMM, 4);
-  if (bias && tid < 64 && n0 + tid < N) {
-    float sum = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sum += red[k * 64 + tid];
-    ((float*)(T.kind == 1 ? uni(a.gb1) : T.kind == 2 ? uni(a.gb2) : uni(a.gb3)))[n0 + tid] = sum;
-  }
-  float* ct = reinterpret_cast<float*>(smem);  // [128][68]
-  acc.to_lds(ct, CT_LD, 32 * (w >> 1), 32 * (w & 1), g, li);
-  __syncthreads();
-  if (T.kind == 1 && a.fuse_sgd) {
-    // fused SGD (single GPU): the complete dW1 tile; master update + the NEXT step's bf16 shadow
-    // (the expression of cnn_gemm.hip's c_mode 4 and the SGD kernel: bit-identical weights)
-    const float f = lr_sched(a.lr0, a.decay, a.decay_steps, a.staircase, a.warmup, step) * a.grad_scale;
-    bf16* S = W1S(a) + ((step & 1) ? 0 : 884736);    // the shadow the NEXT step reads
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + u * FT, rr = e >> 4, cc = (e & 15) * 4;
-      const size_t q = (size_t)(m0 + rr) * 384 + n0 + cc;
-      const float4 gv = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
-      float4 v = R.m[u];
-      v.x -= f * gv.x; v.y -= f * gv.y; v.z -= f * gv.z; v.w -= f * gv.w;
-      const f32x4 vo = {v.x, v.y, v.z, v.w};
-      st_maybe_nt<kNtX>(reinterpret_cast<f32x4*>(a.gw1 + q), vo);
-      st_maybe_nt<kNtX>(reinterpret_cast<bf16x4*>(S + q), pack4(v.x, v.y, v.z, v.w));
-    }
-    return;
-  }
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int e = tid + u * FT, rr = e >> 4, cc = (e & 15) * 4;
-    const int m = m0 + rr, n = n0 + cc;
-    if (m >= M || n >= N) continue;
-    const float4 v = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
-    float* C = (float*)(T.kind == 1 ? uni(a.gw1) : T.kind == 2 ? uni(a.gw2) : uni(a.gw3));
-    if (ldc % 4 == 0 && n + 4 <= N) {
-      *reinterpret_cast<float4*>(C + (size_t)m * ldc + n) = v;
-    } else {
-      const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) if (n + k < N) C[(size_t)m * ldc + n + k] = vv[k];
-    }
-  }
-}
-
-DEV void c_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t step, char* smem, int tid) {
-  if (T.kind == 0) dp2_task(a, T, smem, tid);
-  else dw_task(a, T, R, step, smem, tid);
-}
 
 __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];

@@ -16,6 +16,7 @@
 // Both: the NEXT image's global data is prefetched into registers while the current image computes.
 #include "w1_common.h"
 #include "sgd_common.h"
+#include "fc_common.h"
 
 namespace dmlc {
 
@@ -446,15 +447,22 @@ DEV void conv2_help(const DmlcWgradArgs& A, int j, char* smem, unsigned hg0, int
 // conv1: arrive, run the slab-independent work (fc roles, stats + global_step, next batch rows),
 // wait, then reduce float4 outputs [grp*per, grp*per+per) of the 75 x 16 (32 splits x 16 outputs
 // per round of 512 threads, the SGD kernel's split_sum<32, 5> order) + shadows; one block: the bias.
-DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, int64_t step) {
+DEV void conv1_arrive(const DmlcWgradArgs& A, unsigned g0) {
+  wait_vm_all();
+  __syncthreads();                             // also: w1_flush's LDS reads are done
+  if (threadIdx.x == 0) bar_arrive(wbar(A.bar, 0), wbar(A.bar, 1), g0, (unsigned)A.w1.g1);
+}
+// arrived: the block already arrived at the conv1 barrier (conv1_arrive) and did other work since
+DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, int64_t step, bool arrived = false) {
   const DmlcSgdArgs& s = A.sgd;
   const int tid = threadIdx.x, n = A.w1.g1;
   float4* lds = reinterpret_cast<float4*>(smem);
-  wait_vm_all();
-  __syncthreads();                             // also: w1_flush's LDS reads are done
-  if (tid == 0) bar_arrive(wbar(A.bar, 0), wbar(A.bar, 1), g0, (unsigned)n);
+  if (!arrived) conv1_arrive(A, g0);
+  else __syncthreads();                        // the previous role's LDS reads are done
   const float lr = lr_of(s, step);
-  const int nfc = s.mode == 1 ? 0 : fc_role_count(s);   // reduce-only (data parallel): conv grads only
+  // reduce-only (data parallel): conv grads only; fc_in_launch: the fc parameters are updated in
+  // the dW tiles' epilogues (below, after this function)
+  const int nfc = s.mode == 1 || A.fc_in_launch ? 0 : fc_role_count(s);
   for (int r = grp; r < nfc; r += n) {
     fc_role(s, r, lr, step, lds, tid);
     lds_barrier();                             // the fc2 transpose tile is reused by the next role
@@ -506,6 +514,9 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
 // the conv1 body, the next 4 * g2 the conv2 body.  One block per CU (LDS): g1 + 4 * g2 <= 256 keeps
 // every block resident in one wave of blocks.
 constexpr size_t WG_LDS = W1_LDS > W2_LDS ? W1_LDS : W2_LDS;
+static_assert(WG_LDS >= (size_t)L_RED + 8 * 64 * 4 && WG_LDS >= 40960 + 64 * 136 * 2,
+              "the fc dW tiles reuse the weight-gradient launch's LDS");
+static_assert(W1T == FT, "the fc dW tiles run with the weight-gradient launch's block size");
 static_assert(WG_LDS >= SGD_LDS4 * 16, "apply mode reuses the block's LDS for the SGD roles");
 __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -526,7 +537,25 @@ __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
   }
   if (conv1) {
     conv1_wgrad_block(a.w1, blockIdx.x, smem, a.apply != 0);
-    if (a.apply) conv1_apply(a, blockIdx.x, smem, g0, step);
+    if (a.apply && a.fc_in_launch) {
+      // arrive at the conv1 barrier, then the fc weight gradients + their SGD (inputs from earlier
+      // launches: no waits) while the rest of the family arrives, then the conv1 reduction + SGD;
+      // the conv2 help comes last, when the conv2 slabs are ready anyway (running the fc tiles
+      // after the help instead made the helpers late: the conv2 tail grew by ~3 us)
+      conv1_arrive(a, g0);
+      const int parity = (int)(step & 1);
+      for (int d = blockIdx.x; d < FC_DW_TASKS; d += a.w1.g1) {
+        const CTask T = dw_ctask(d);
+        PreRegs R;
+        pre_issue(a.fc, T, parity, R, threadIdx.x);
+        __syncthreads();                       // the previous role's LDS reads are done
+        pre_store(a.fc, T, R, smem, threadIdx.x);
+        dw_task<false>(a.fc, T, R, step, smem, threadIdx.x);
+      }
+      conv1_apply(a, blockIdx.x, smem, g0, step, true);
+    } else if (a.apply) {
+      conv1_apply(a, blockIdx.x, smem, g0, step);
+    }
     if (helper) conv2_help(a, blockIdx.x, smem, hg0, step);
   } else {
     conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, smem, a.apply != 0);
@@ -570,6 +599,9 @@ hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s) {
     const bool ok_mode = g.mode == 0 ? (g.step_rd != g.step && g.fc1_fused && (!g.w2f8 || (g.amax_w && g.scale_w) ) &&
                                         8 * a->w2.g2 <= 400)
                                      : g.mode == 1;
+    if (a->fc_in_launch && (g.mode != 0 || !g.fc1_fused || a->fc.fuse_sgd != 2 || a->fc.B < 16 || a->fc.B > 256 ||
+                            !a->fc.p2 || !a->fc.dh1 || !a->fc.mw2 || !a->fc.fc2t))
+      return hipErrorInvalidValue;
     if (a->w1.g1 < 1 || a->w1.g1 > cus || 4 * a->w2.g2 > cus || a->w2.part2_bf16 || !a->bar || !a->w1.xraw ||
         !ok_mode || g.part1 != a->w1.part1 ||
         g.part2 != a->w2.part2 || g.g1 != a->w1.g1 || g.g2 != a->w2.g2 || g.bidx_n > a->w1.g1 * W1T)

@@ -347,6 +347,11 @@ class FusedCifarEngine:
         # chunk of steps (the trainer checks it at every progress point without a device sync)
         self._err_host = (torch.zeros(1, dtype=torch.int32).pin_memory() if dev.type == "cuda"
                           else torch.zeros(1, dtype=torch.int32))
+        # single GPU, fused fc chain + apply mode: the fc weight-gradient tiles and every fc SGD run in
+        # the wgrad launch's conv1 blocks (idle ~8 us there while the conv2 blocks finish), so the fc
+        # chain launch ends with its dp2 tiles.  DMLC_FC_DW_WGRAD=0: the dW tiles stay in the chain.
+        self.fc_dw_in_wgrad = (self.fc_fused and self.wgrad_apply
+                               and os.environ.get("DMLC_FC_DW_WGRAD", "1") != "0")
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
                                                                         s_par=FC1_NUMEL)
@@ -478,7 +483,8 @@ class FusedCifarEngine:
                           self.dh2, self.loss_part, self.correct_part, self.dp2.view(self.B, 2304),
                           p["full_weight_1"] if fused_sgd else gv["full_weight_1"], gv["full_weight_2"],
                           gv["full_weight_3"], gv["full_bias_1"], gv["full_bias_2"], gv["full_bias_3"], fused_sgd,
-                          sched, self.Bv, self.step_t, self.step_sgd, self.fc_sync, self.wbar[10 * 32:10 * 32 + 1])
+                          sched, self.Bv, self.step_t, self.step_sgd, self.fc_sync, self.wbar[10 * 32:10 * 32 + 1],
+                          not (fused_sgd and self.fc_dw_in_wgrad))
 
     def _conv_backward(self, src=None, apply: bool = False, reduce: bool = False):
         """apply: + the whole SGD in the wgrad launch (single GPU); reduce: + the conv slab reduction
@@ -501,9 +507,13 @@ class FusedCifarEngine:
         else:
             o.conv2_dgrad(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         if apply or reduce:
+            fc_acts = None
+            if apply and self.fc_dw_in_wgrad:
+                fc_acts = [self.p2.view(self.B, 2304), self.h1, self.h2, self.dl, self.dh1, self.dh2]
             o.wgrad_sgd(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1, self.p1, self.dy2,
                         self.groups2, self.xraw, self.wbar,
-                        *(self._sgd_args(mode=0, fc1_fused=True) if apply else self._sgd_args(mode=1)))
+                        *(self._sgd_args(mode=0, fc1_fused=True) if apply else self._sgd_args(mode=1)),
+                        fc_acts=fc_acts)
             return
         if self.merged_wgrad:
             o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
