@@ -41,12 +41,12 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedu
     for _ in range(steps - 1):
         eng.step()
     torch.cuda.synchronize()
-    torch.save({"flat": eng.flat_params(), "step": eng.global_step(),
+    torch.save({"flat": eng.flat_params(), "step": eng.global_step(), "fc_fused": eng.fc_fused,
                 "batches": [eng.batch_indices(s) for s in range(steps)]}, os.path.join(out, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
-def _dp_reference(world, B, steps, batches, comm_dtype, allreduce):
+def _dp_reference(world, B, steps, batches, comm_dtype, allreduce, fc_fused=False):
     """Replays the data-parallel run on ONE world-1 engine: at every step each rank's gradient on its
     own batch from the shared weights (the DP kernels compute exactly it / world: the loss scale
     1/(B*world) is a power-of-two multiple of 1/B here, which commutes with every rounding), summed in
@@ -54,7 +54,18 @@ def _dp_reference(world, B, steps, batches, comm_dtype, allreduce):
     apply-only SGD kernel.  Returns (initial, final) flat parameters."""
     from dmlc.engine.fused import FusedCifarEngine
     x, y = _data()
-    ref = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, staircase=False)
+    # the fc kernels the ranks ran (ranks sharing one GPU run the three-launch fc path, not the
+    # persistent fc chain, whose 256 workgroups must own the chip)
+    old = os.environ.get("DMLC_FC_FUSED")
+    os.environ["DMLC_FC_FUSED"] = "1" if fc_fused else "0"
+    try:
+        ref = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, staircase=False)
+    finally:
+        if old is None:
+            del os.environ["DMLC_FC_FUSED"]
+        else:
+            os.environ["DMLC_FC_FUSED"] = old
+    assert ref.fc_fused == fc_fused
     init = ref.flat_params().clone()
     bf = (lambda t: t.to(torch.bfloat16).float()) if comm_dtype == "bf16" else (lambda t: t)
     for s in range(steps):
@@ -92,7 +103,7 @@ def test_dp_matches_mean_of_rank_gradients(tmp_path, world, graph, comm_dtype, a
     assert all(r["step"] == steps for r in rs)
     for r in rs[1:]:
         assert torch.equal(rs[0]["flat"], r["flat"])      # replicas identical
-    init, want = _dp_reference(world, B, steps, [r["batches"] for r in rs], comm_dtype, allreduce)
+    init, want = _dp_reference(world, B, steps, [r["batches"] for r in rs], comm_dtype, allreduce, rs[0]["fc_fused"])
     d_dp, d_ref = rs[0]["flat"] - init, want - init
     rel = float((d_dp - d_ref).norm() / d_ref.norm())
     tol = 1e-2 if (comm_dtype == "bf16" and allreduce == "rccl") else 1e-5
