@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Fixed cost of a timed region: how long do k chained training steps take when bracketed exactly as
+bench.py brackets them (synchronize -> t0 -> one graph replay of k steps -> synchronize -> t1)?
+A linear fit over k separates the per-step time (slope) from the per-region overhead (intercept:
+graph launch submission, the first kernel's dispatch after an idle queue, the final sync).
+
+  python tools/region_probe.py [--batch 256] [--reps 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import dmlc  # noqa: E402,F401
+from dmlc.engine.fused import FusedCifarEngine  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    g = torch.Generator().manual_seed(0)
+    data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g).cuda()
+    labels = torch.randint(0, 10, (50000,), dtype=torch.int32, generator=g).cuda()
+    eng = FusedCifarEngine(a.batch, data, labels, device="cuda", seed=0, lr=1e-4, relu_logits=False)
+    for _ in range(3):
+        eng.step()
+    eng.capture(32)
+    ks = [1, 2, 4, 8, 16, 20, 32, 40, 64]
+    for k in ks:
+        eng.add_chain(k)
+    for k in sorted(eng.chains):
+        eng.run(k)
+    eng.run(256)
+    torch.cuda.synchronize()
+    res = {}
+    for k in ks:
+        ts = []
+        for _ in range(a.reps):
+            eng.run(64)                          # busy before, as after bench.py's warm-up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.chains[k].replay()
+            eng.host_step += k
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e6)
+        res[k] = min(ts)
+    x = np.array(ks, dtype=float)
+    y = np.array([res[k] for k in ks])
+    slope, icpt = np.polyfit(x, y, 1)
+    # the empty region: sync -> t0 -> sync
+    torch.cuda.synchronize()
+    e = []
+    for _ in range(20):
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        e.append((time.perf_counter() - t0) * 1e6)
+    print(json.dumps({"us_per_region": {str(k): round(v, 1) for k, v in res.items()},
+                      "fit_us_per_step": round(float(slope), 2), "fit_region_overhead_us": round(float(icpt), 1),
+                      "empty_sync_us": round(float(min(e)), 1)}))
+
+
+if __name__ == "__main__":
+    main()
