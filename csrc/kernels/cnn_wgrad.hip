@@ -409,6 +409,8 @@ DEV void conv2_apply(const DmlcWgradArgs& A, int c4, int grp, char* smem, unsign
       flag[0] = __hip_atomic_fetch_max(w2_claim(A, c4, grp), g0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g0 + 1u;
     __syncthreads();
     f8.slot = slot + 1;
+    if (flag[0]) DMLC_STAMP(DMLC_TK_HEAD, 6);    // (timing build: no helper took it; the HEAD row is
+                                                 //  free for blocks >= 64 in this launch)
     if (flag[0]) conv2_reduce(A, c4, m, e, lr, f8);
     __syncthreads();                           // flag / LDS reused by the bias below
   } else if (s.w2f8 && s.mode == 0 && tid == 0) {
@@ -436,6 +438,7 @@ DEV void conv2_help(const DmlcWgradArgs& A, int j, char* smem, unsigned hg0, int
   }
   __syncthreads();
   if (flag[0]) {
+    DMLC_STAMP(DMLC_TK_SGD, 5);                // (timing build: this helper took the half)
     int b, m, e;
     w2_chunk(A, grp, b, m, e);
     const W2Fp8 f8 = {A.sgd.w2f8 ? w2_fp8_scale(A.sgd, step) : 0.f, (int)((step & 1) ^ 1),
@@ -548,15 +551,15 @@ __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
         const CTask T = dw_ctask(d);
         PreRegs R;
         pre_issue(a.fc, T, parity, R, threadIdx.x);
-        __syncthreads();                       // the previous role's LDS reads are done
-        pre_store(a.fc, T, R, smem, threadIdx.x);
         dw_task<false>(a.fc, T, R, step, smem, threadIdx.x);
       }
+      DMLC_STAMP(DMLC_TK_SGD, 3);
       conv1_apply(a, blockIdx.x, smem, g0, step, true);
     } else if (a.apply) {
       conv1_apply(a, blockIdx.x, smem, g0, step);
     }
     if (helper) conv2_help(a, blockIdx.x, smem, hg0, step);
+    DMLC_STAMP(DMLC_TK_SGD, 4);
   } else {
     conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, smem, a.apply != 0);
     if (a.apply) conv2_apply(a, c4, grp, smem, g0, step);

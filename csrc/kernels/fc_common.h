@@ -353,6 +353,13 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
   };
   const T3 t0 = tile(0), t1 = tile(1), t2 = tile(2), t3 = tile(3);
   if (HANDOFF) DMLC_STAMP(DMLC_TK_GEMM, 3);
+  // no hand-off (inputs from earlier launches): the caller issued R and returned at once, so the
+  // prefetch and the tile loads are in flight together -- one memory round trip, not two
+  if (!HANDOFF) {
+    __syncthreads();                           // the previous role's LDS reads are done
+    pre_store(a, T, R, smem, tid);
+    DMLC_STAMP(DMLC_TK_GEMM, 5);
+  }
   put(0, t0); put(1, t1); put(2, t2); put(3, t3);
   __syncthreads();
   const int w = wave_id(), lane = tid & 63, g = lane >> 4, li = lane & 15;
@@ -370,6 +377,7 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
   mma_128x64(sa, sb, Kpad >> 5, acc, w, g, li);
   __syncthreads();
   if (HANDOFF) DMLC_STAMP(DMLC_TK_GEMM, 4);
+  else DMLC_STAMP(DMLC_TK_GEMM, 6);
   // fused SGD modes: the SGD kernel's update expression (w -= (lr * grad_scale) * g), so the weights
   // are bit-identical to the gradient + SGD-launch path
   const float f = lr_sched(a.lr0, a.decay, a.decay_steps, a.staircase, a.warmup, step) * a.grad_scale;
