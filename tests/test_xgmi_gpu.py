@@ -208,12 +208,14 @@ def _rank_exact_w(rank, world, port, out, wire):
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("world,wire", [(3, "fp32"), (3, "bf16"), (8, "fp32"), (8, "bf16")])
+@pytest.mark.parametrize("world,wire", [(3, "fp32"), (3, "bf16"), (4, "fp32"), (5, "bf16"), (6, "fp32"),
+                                        (7, "bf16"), (8, "fp32"), (8, "bf16")])
 def test_xgmi_allreduce_w_ranks_exact(tmp_path, world, wire):
-    """W = 3 and W = 8 ranks (all on the test box's one GPU, each mapping every peer through HIP IPC as
+    """W = 3..8 ranks (all on the test box's one GPU, each mapping every peer through HIP IPC as
     on an 8-GPU node): every replica holds, bit for bit, the rank-ordered fp32 sum (bf16 wire: of the
     bf16-rounded inputs, rounded to bf16) for two buckets whose sizes divide by nothing convenient,
-    eager and graph-replayed; no timeout.  The W = 3, 5-8 kernel instances had never executed."""
+    eager and graph-replayed; no timeout.  Every world size an 8-GPU node can run executes its kernel
+    instance (W = 2 has its own test)."""
     import torch.multiprocessing as mp
     from dmlc.cli import free_port
     mp.spawn(_rank_exact_w, args=(world, free_port(), str(tmp_path), wire), nprocs=world, join=True)
