@@ -476,7 +476,9 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
               const Tensor& dh2, const Tensor& loss_part, const Tensor& correct_part, const Tensor& dp2,
               const Tensor& gw1, const Tensor& gw2, const Tensor& gw3, const Tensor& gb1, const Tensor& gb2,
               const Tensor& gb3, bool fuse_sgd, at::ArrayRef<double> sched, int64_t nvalid, const Tensor& step,
-              const c10::optional<Tensor>& step_copy, const Tensor& sync, const Tensor& err, bool dw_tasks) {
+              const c10::optional<Tensor>& step_copy, const Tensor& sync, const Tensor& err, bool dw_tasks,
+              const c10::optional<Tensor>& am2, const c10::optional<Tensor>& w2d, const c10::optional<Tensor>& dp1,
+              const c10::optional<Tensor>& dy2) {
   const int64_t B = p2.size(0);
   TORCH_CHECK(B >= 16 && B <= 256 && B % 16 == 0, "fc_chain: batch must be a multiple of 16 in [16, 256]");
   check(p2, "p2", at::kBFloat16, {B, 2304});
@@ -505,7 +507,7 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
   check_numel(gb2, "gb2", at::kFloat, 192);
   check_numel(gb3, "gb3", at::kFloat, 10);
   check_numel(step, "step", at::kLong, 1);
-  check_min(sync, "sync", at::kInt, 19 * 32);
+  check_min(sync, "sync", at::kInt, 28 * 32);
   check_min(err, "err", at::kInt, 1);
   TORCH_CHECK(sched.size() == 6, "fc_chain: sched = {lr0, decay, decay_steps, staircase, warmup, grad_scale}");
   if (nvalid < 0) nvalid = B;
@@ -537,7 +539,21 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
   }
   a.sync = reinterpret_cast<unsigned int*>(sync.data_ptr<int>());
   a.err = reinterpret_cast<unsigned int*>(err.data_ptr<int>());
-  CHECK_HIP(dmlc_fc_chain(&a, stream_of(p2)));
+  // am2 / w2d / dp1 / dy2: the conv2 input gradient runs in the same launch (one image per workgroup)
+  const bool dg_on = am2.has_value();
+  TORCH_CHECK(dg_on == w2d.has_value() && dg_on == dp1.has_value() && dg_on == dy2.has_value(),
+              "fc_chain: am2, w2d, dp1, dy2 come together");
+  DmlcConv2DgradArgs g;
+  memset(&g, 0, sizeof(g));
+  if (dg_on) {
+    check(*am2, "am2", at::kByte, {B, 6, 6, 64});
+    check(*w2d, "w2d", at::kBFloat16, {64, 1600});
+    check(*dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+    check(*dy2, "dy2", at::kBFloat16, {B, 144, 64});
+    g.dp2 = dp2.data_ptr(); g.am2 = am2->data_ptr<uint8_t>(); g.wd = w2d->data_ptr();
+    g.dp1 = dp1->data_ptr(); g.dy2 = dy2->data_ptr(); g.B = (int)B;
+  }
+  CHECK_HIP(dmlc_fc_chain(&a, dg_on ? &g : nullptr, stream_of(p2)));
 }
 
 static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mode, double grad_scale, at::IntArrayRef off,
@@ -703,7 +719,8 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
     f.lr0 = (float)lr0; f.decay = (float)decay; f.decay_steps = (float)decay_steps; f.staircase = staircase;
     f.warmup = (float)warmup; f.grad_scale = (float)grad_scale;
     f.err = a.bar + 10 * 32;
-    a.fc_in_launch = 1;
+    const char* first = getenv("DMLC_FC_DW_FIRST");
+    a.fc_in_launch = first && first[0] == '1' ? 2 : 1;
   }
   c10::DeviceGuard guard(dp1.device());
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
@@ -746,7 +763,8 @@ TORCH_LIBRARY(dmlc, m) {
         "bool relu_logits, Tensor(c!) h1, Tensor(d!) h2, Tensor(e!) dl, Tensor(f!) dh1, Tensor(g!) dh2, "
         "Tensor(h!) loss_part, Tensor(i!) correct_part, Tensor(j!) dp2, Tensor(k!) gw1, Tensor(l!) gw2, "
         "Tensor(m!) gw3, Tensor(n!) gb1, Tensor(o!) gb2, Tensor(p!) gb3, bool fuse_sgd, float[] sched, "
-        "int nvalid, Tensor step, Tensor(q!)? step_copy, Tensor(r!) sync, Tensor(s!) err, bool dw_tasks=True) -> ()");
+        "int nvalid, Tensor step, Tensor(q!)? step_copy, Tensor(r!) sync, Tensor(s!) err, bool dw_tasks=True, "
+        "Tensor? am2=None, Tensor? w2d=None, Tensor(t!)? dp1=None, Tensor(u!)? dy2=None) -> ()");
   m.def("wgrad_sgd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor p1, Tensor dy2, int groups2, Tensor xraw, Tensor(z!) bar, "
         "Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor(r!) part1, Tensor(s!) partb1, "

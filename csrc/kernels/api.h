@@ -204,7 +204,7 @@ struct DmlcFcArgs {
   int dw_tasks;                      // the fc-chain launch runs the dW tasks (0: the wgrad launch does)
   float lr0, decay, decay_steps, warmup, grad_scale; int staircase;
   const int64_t* step; int64_t* step_copy;             // device step counter; copy for the SGD reader
-  unsigned int* sync;                // >= 19 * 32 zeroed uints (counters re-arm themselves)
+  unsigned int* sync;                // >= 28 * 32 zeroed uints (counters re-arm themselves)
   unsigned int* err;                 // sticky error word (bit 2: a seam wait timed out)
 };
 
@@ -297,7 +297,9 @@ hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s);
 hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s);
 hipError_t dmlc_gemm_grouped(DmlcGemmGroup* g, hipStream_t s);
-hipError_t dmlc_fc_chain(const DmlcFcArgs* a, hipStream_t s);
+// dg: null, or the conv2 dgrad of the same batch, run in the chain's workgroups (dg->dp2 == a->dp2;
+// a->sync >= 28 * 32 words)
+hipError_t dmlc_fc_chain(const DmlcFcArgs* a, const DmlcConv2DgradArgs* dg, hipStream_t s);
 hipError_t dmlc_head(const DmlcHeadArgs* a, hipStream_t s);
 hipError_t dmlc_sgd(DmlcSgdArgs* a, hipStream_t s);
 

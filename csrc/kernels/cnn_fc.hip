@@ -24,7 +24,10 @@
 // outputs (cntB) plus a total; the last block to finish re-arms them (zero) for the next launch.
 // Every spin is bounded and sets the sticky error word (the engine's wgrad barrier error word) --
 // all 256 blocks must be co-resident (one per CU: ~150 KB of LDS each; host-checked).
+#include <string.h>
+
 #include "fc_common.h"
+#include "conv2_core.h"
 
 namespace dmlc {
 
@@ -45,6 +48,8 @@ struct HL {
 };
 constexpr int FC_LDS = L_DP2_END > HL::BYTES ? L_DP2_END : HL::BYTES;
 static_assert(FC_LDS <= 160 * 1024, "fc chain LDS exceeds a CU");
+constexpr int FC_LDS_ALL = FC_LDS > (int)DG_LDS ? FC_LDS : (int)DG_LDS;   // with the conv2 dgrad
+static_assert(FT == NT && FC_LDS_ALL <= 160 * 1024, "the dgrad runs in the chain's workgroups");
 static_assert(L_FWD_B + FC_KS * 64 * 2 <= FC_LDS && L_RED + 8 * 64 * 4 <= FC_LDS, "task images");
 
 // =================================================================================================
@@ -332,7 +337,7 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
 }
 
 
-__global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a) {
+__global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a, DmlcConv2DgradArgs dg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, blk = blockIdx.x;
   const int H = a.B / FC_RB;
@@ -340,6 +345,10 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a) {
   const int parity = (int)(step & 1);
   if (blk == 0 && tid == 0 && a.step_copy) *a.step_copy = step;
   const int nc = ctask_count(a);
+  __shared__ unsigned s_epoch;
+  if (tid == 0) s_epoch = ld_relaxed(epochW(a));
+  __syncthreads();                             // (in hand before this block can arrive below)
+  const unsigned epoch = s_epoch;
   if (blk < H) {
     // head block: its rows, then (after every head) the C tasks past the GEMM blocks' share
     head_task(a, blk, smem, tid);
@@ -350,7 +359,7 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a) {
       const CTask T = ctask(a, t);
       pre_issue(a, T, parity, R, tid);
       pre_store(a, T, R, smem, tid);
-      c_task(a, T, R, step, smem, tid);
+      c_task(a, T, R, step, smem, tid, epoch);
     }
     DMLC_STAMP(DMLC_TK_HEAD, 6);
   } else {
@@ -374,12 +383,13 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a) {
       __syncthreads();                         // the forward's LDS staging is dead
       pre_store(a, T, R, smem, tid);
       DMLC_STAMP(DMLC_TK_GEMM, 2);
-      c_task(a, T, R, step, smem, tid);
+      c_task(a, T, R, step, smem, tid, epoch);
       DMLC_STAMP(DMLC_TK_GEMM, 5);
     }
   }
-  // the last block to finish re-arms the counters for the next launch (two-level ticket: one
-  // counter taking 256 arrivals in a row serialises them at the memory side)
+  // the last block to finish its chain work re-arms the counters for the next launch (two-level
+  // ticket: one counter taking 256 arrivals in a row serialises them at the memory side); the
+  // dgrad's dp2 counters are the epoch's set, so the ticket need not wait for the dgrad
   __syncthreads();
   if (tid == 0) {
     wait_vm_all();
@@ -387,10 +397,15 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a) {
       for (int m = 0; m < 4; ++m) {
         __hip_atomic_store(cntA(a, m), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(cntB(a, m), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cntD(a, epoch + 1, m), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __hip_atomic_store(cntBall(a), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(epochW(a), epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  // the conv2 input gradient of image blk (dg.B = 0: a separate launch does it): its dp2 row tile
+  // comes from this launch's dp2 tasks; everything else it reads was written by earlier launches
+  if (blk < dg.B) conv2_dgrad_image<true>(dg, blk, smem, cntD(a, epoch, blk >> 6), DP2_COL_TILES, a.err);
   if (blk < H) DMLC_STAMP(DMLC_TK_HEAD, 7);
   else DMLC_STAMP(DMLC_TK_GEMM, 6);
 }
@@ -399,9 +414,16 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a) {
 
 using namespace dmlc;
 
-extern "C" hipError_t dmlc_fc_chain(const DmlcFcArgs* a, hipStream_t s) {
+extern "C" hipError_t dmlc_fc_chain(const DmlcFcArgs* a, const DmlcConv2DgradArgs* dg, hipStream_t s) {
   if (a->B < 16 || a->B > 256 || a->B % 16 != 0 || a->mtiles != (a->B + 63) / 64 || !a->sync || !a->err)
     return hipErrorInvalidValue;
+  DmlcConv2DgradArgs d;
+  memset(&d, 0, sizeof(d));
+  if (dg) {
+    // one image per workgroup of the 256: the batch rows are the chain's, dp2 its own output
+    if (dg->B != a->B || dg->dp2 != a->dp2 || !dg->am2 || !dg->wd || !dg->dp1 || !dg->dy2) return hipErrorInvalidValue;
+    d = *dg;
+  }
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -409,7 +431,7 @@ extern "C" hipError_t dmlc_fc_chain(const DmlcFcArgs* a, hipStream_t s) {
       return hipErrorInvalidValue;
   }
   if (cus < FC_BLOCKS) return hipErrorInvalidValue;   // every block must be co-resident (one per CU)
-  DMLC_LDS_OPTIN(&k_fc_chain, FC_LDS);
-  hipLaunchKernelGGL(k_fc_chain, dim3(FC_BLOCKS), dim3(FT), FC_LDS, s, *a);
+  DMLC_LDS_OPTIN(&k_fc_chain, FC_LDS_ALL);
+  hipLaunchKernelGGL(k_fc_chain, dim3(FC_BLOCKS), dim3(FT), d.B ? FC_LDS_ALL : FC_LDS, s, *a, d);
   return hipGetLastError();
 }

@@ -539,19 +539,38 @@ __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
     step = *a.sgd.step_rd;
   }
   if (conv1) {
-    conv1_wgrad_block(a.w1, blockIdx.x, smem, a.apply != 0);
-    if (a.apply && a.fc_in_launch) {
-      // arrive at the conv1 barrier, then the fc weight gradients + their SGD (inputs from earlier
-      // launches: no waits) while the rest of the family arrives, then the conv1 reduction + SGD;
-      // the conv2 help comes last, when the conv2 slabs are ready anyway (running the fc tiles
-      // after the help instead made the helpers late: the conv2 tail grew by ~3 us)
-      conv1_arrive(a, g0);
+    if (a.apply && a.fc_in_launch == 2) {
+      // variant: the fc weight-gradient tiles first (their inputs come from earlier launches)
       const int parity = (int)(step & 1);
       for (int d = blockIdx.x; d < FC_DW_TASKS; d += a.w1.g1) {
         const CTask T = dw_ctask(d);
         PreRegs R;
         pre_issue(a.fc, T, parity, R, threadIdx.x);
         dw_task<false>(a.fc, T, R, step, smem, threadIdx.x);
+      }
+      DMLC_STAMP(DMLC_TK_SGD, 3);
+      __syncthreads();
+    }
+    conv1_wgrad_block(a.w1, blockIdx.x, smem, a.apply != 0);
+    if (a.apply && a.fc_in_launch == 2) {
+      conv1_apply(a, blockIdx.x, smem, g0, step);
+    } else if (a.apply && a.fc_in_launch) {
+      // arrive at the conv1 barrier, then the fc weight gradients + their SGD (inputs from earlier
+      // launches: no waits) while the rest of the family arrives, then the conv1 reduction + SGD;
+      // the conv2 help comes last, when the conv2 slabs are ready anyway (running the fc tiles
+      // after the help instead made the helpers late: the conv2 tail grew by ~3 us)
+      // (the first task's operand loads go out before the slab stores are drained: the arrival
+      // waits for both at once)
+      const int parity = (int)(step & 1);
+      if (blockIdx.x >= FC_DW_TASKS) conv1_arrive(a, g0);
+      for (int d = blockIdx.x; d < FC_DW_TASKS; d += a.w1.g1) {
+        const CTask T = dw_ctask(d);
+        PreRegs R;
+        pre_issue(a.fc, T, parity, R, threadIdx.x);
+        const bool first = d == (int)blockIdx.x;
+        dw_task<false>(a.fc, T, R, step, smem, threadIdx.x, [&]() {
+          if (first) conv1_arrive(a, g0);
+        });
       }
       DMLC_STAMP(DMLC_TK_SGD, 3);
       conv1_apply(a, blockIdx.x, smem, g0, step, true);

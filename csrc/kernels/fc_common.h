@@ -47,6 +47,11 @@ DEV unsigned* cntA(const DmlcFcArgs& a, int m) { return a.sync + 32 * m; }      
 DEV unsigned* cntB(const DmlcFcArgs& a, int m) { return a.sync + 32 * (4 + m); }    // m < 4
 DEV unsigned* cntBall(const DmlcFcArgs& a) { return a.sync + 32 * 8; }
 // a.sync + 32 * 10 .. + 32 * 19: the two-level end-of-launch ticket (common.h last_arrival)
+// a.sync + 32 * 9: launch epoch E; dp2 row tile m < 4 counts into set E & 1 (the launch's last
+// arrival re-arms the OTHER set and bumps E, so it can arrive before the dgrad's waits are done)
+DEV unsigned* epochW(const DmlcFcArgs& a) { return a.sync + 32 * 9; }
+DEV unsigned* cntD(const DmlcFcArgs& a, unsigned set, int m) { return a.sync + 32 * (20 + 4 * (set & 1) + m); }
+constexpr unsigned DP2_COL_TILES = 2304 / 128;
 
 DEV unsigned ld_relaxed(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 // one lane: spin until *p >= target (bounded; on give-up the sticky error word is set)
@@ -237,7 +242,7 @@ DEV void mma_128x64(const bf16* sa, const bf16* sb, int ksteps, Acc& acc, int w,
             mfrag(sb, 32 * wn + 16, kk, g, li));
 }
 
-DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid) {
+DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid, unsigned epoch) {
   bf16* sa = reinterpret_cast<bf16*>(smem + L_DP2_A);
   bf16* sb = reinterpret_cast<bf16*>(smem + L_DP2_B);
   const int mt = T.i, n0 = 128 * T.j;
@@ -275,24 +280,35 @@ DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid) {
   constexpr int LD = 132;
   acc.to_lds(ct, LD, 32 * wm, 32 * wn, g, li);
   __syncthreads();
+  // sc1 stores + the row tile's counter: the launch's conv2 dgrad (one image per workgroup) reads
+  // these rows as soon as all 18 column tiles of its row tile are published
+  const rsrc_t rd = buf_rsrc(a.dp2);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {                // 64 x 128 bf16 = 2048 x 8-B pieces
-    const int e = tid + u * FT, rr = e >> 5, cc = (e & 31) * 4;
+  for (int u = 0; u < 2; ++u) {                // 64 x 128 bf16 = 1024 x 16-B pieces
+    const int e = tid + u * FT, rr = e >> 4, cc = (e & 15) * 8;
     if (rr < rows) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(ct + rr * LD + cc);
-      st_maybe_nt<kNtGemm>(reinterpret_cast<bf16x4*>(DP2(a) + (size_t)(64 * mt + rr) * 2304 + n0 + cc),
-                           pack4(v[0], v[1], v[2], v[3]));
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(ct + rr * LD + cc);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(ct + rr * LD + cc + 4);
+      const uint2 lo = __builtin_bit_cast(uint2, pack4(v0[0], v0[1], v0[2], v0[3]));
+      const uint2 hi = __builtin_bit_cast(uint2, pack4(v1[0], v1[1], v1[2], v1[3]));
+      st16(rd, (uint32_t)((64 * mt + rr) * 2304 + n0 + cc) * 2, make_uint4(lo.x, lo.y, hi.x, hi.y));
     }
   }
+  publish(cntD(a, epoch, mt), nullptr);
 }
 
 // dW1 / dW2 / dW3: 128 x 64 tile of A^T B over the batch (A, B: bf16 [B][lda], [B][ldb])
 // One 16-B chunk per thread of a 64-row tile of an m-major hand-off operand: rows 64 m + (tid >> 3),
 // columns c0 + 8 (tid & 7) of a bf16 [B][ld] matrix (sc1; rows >= B / columns >= ncol read as zero)
+// (SC1 = false: the operand comes from an earlier launch -- plain loads, which may hit this XCD's L2;
+// the tasks sharing a column slice then fetch it from memory once per XCD, not once each)
+template <bool SC1 = true>
 DEV uint4 ld_mtile(const void* base, int ld, int c0, int ncol, int B, int m, int tid) {
   const int rw = 64 * m + (tid >> 3), col = c0 + 8 * (tid & 7);
   const bool ok = rw < B && col < ncol;
-  const uint4 v = ld16(buf_rsrc(base), ok ? (uint32_t)(rw * ld + col) * 2 : 0u);
+  const uint32_t off = ok ? (uint32_t)(rw * ld + col) * 2 : 0u;
+  const uint4 v = SC1 ? ld16(buf_rsrc(base), off)
+                      : __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(buf_rsrc(base), off, 0, 0));
   return ok ? v : make_uint4(0, 0, 0, 0);
 }
 DEV void st_mtile(bf16* img, int m, const uint4& v, int tid) {
@@ -302,8 +318,12 @@ DEV void st_mtile(bf16* img, int m, const uint4& v, int tid) {
 // HANDOFF (the fc-chain launch): the dh1 / h1 / h2 / dh2 / dl rows come from the head blocks of the
 // same launch -- wait for each 64-row tile's counter, sc1 loads.  Otherwise (the weight-gradient
 // launch) they were written by an earlier launch: no waits.
-template <bool HANDOFF>
-DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t step, char* smem, int tid) {
+struct NoOp { __device__ void operator()() const {} };
+// after_issue (no hand-off only): runs once every operand load is in flight (the wgrad launch's
+// conv1 blocks drain their slab stores and arrive at their barrier there, under the loads)
+template <bool HANDOFF, class F = NoOp>
+DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t step, char* smem, int tid,
+                 F&& after_issue = F{}) {
   bf16* sa = reinterpret_cast<bf16*>(smem + L_W1_A);
   bf16* sb = reinterpret_cast<bf16*>(smem + L_W1_B);
   const int Kpad = (a.B + 31) & ~31;
@@ -337,9 +357,9 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
     }
     const int Bm = on ? a.B : 0;            // a tile past the batch reads nothing (zeros)
     T3 r;
-    r.b = ld_mtile(pb, ldb, cb, ldb, Bm, m, tid);
-    r.a0 = ld_mtile(pa, lda, m0, need_a ? lda : 0, Bm, m, tid);
-    r.a1 = ld_mtile(pa, lda, m0 + 64, need_a ? lda : 0, Bm, m, tid);
+    r.b = ld_mtile<HANDOFF>(pb, ldb, cb, ldb, Bm, m, tid);
+    r.a0 = ld_mtile<HANDOFF>(pa, lda, m0, need_a ? lda : 0, Bm, m, tid);
+    r.a1 = ld_mtile<HANDOFF>(pa, lda, m0 + 64, need_a ? lda : 0, Bm, m, tid);
     return r;
   };
   auto put = [&](int m, const T3& r) __attribute__((always_inline)) {
@@ -356,6 +376,7 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
   // no hand-off (inputs from earlier launches): the caller issued R and returned at once, so the
   // prefetch and the tile loads are in flight together -- one memory round trip, not two
   if (!HANDOFF) {
+    after_issue();
     __syncthreads();                           // the previous role's LDS reads are done
     pre_store(a, T, R, smem, tid);
     DMLC_STAMP(DMLC_TK_GEMM, 5);
@@ -474,8 +495,9 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
   }
 }
 
-DEV void c_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t step, char* smem, int tid) {
-  if (T.kind == 0) dp2_task(a, T, smem, tid);
+DEV void c_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t step, char* smem, int tid,
+                unsigned epoch) {
+  if (T.kind == 0) dp2_task(a, T, smem, tid, epoch);
   else dw_task<true>(a, T, R, step, smem, tid);
 }
 

@@ -267,7 +267,7 @@ class FusedCifarEngine:
                          and os.environ.get("DMLC_FC_BRANCH", "0") != "1"
                          and os.environ.get("DMLC_FC_FUSED", "1") != "0")
         self.h1part8 = z(8, B, 384, dt=torch.float32) if self.fc_fused else None
-        self.fc_sync = torch.zeros(20 * 32, dtype=torch.int32, device=dev)
+        self.fc_sync = torch.zeros(28 * 32, dtype=torch.int32, device=dev)
         self._fc_src = None
         # head: head_rows(B) batch rows per workgroup (B / rows workgroups share the fc2 weight reads);
         # the fused fc chain's head takes 4 rows per workgroup
@@ -347,11 +347,23 @@ class FusedCifarEngine:
         # chunk of steps (the trainer checks it at every progress point without a device sync)
         self._err_host = (torch.zeros(1, dtype=torch.int32).pin_memory() if dev.type == "cuda"
                           else torch.zeros(1, dtype=torch.int32))
-        # single GPU, fused fc chain + apply mode: the fc weight-gradient tiles and every fc SGD run in
-        # the wgrad launch's conv1 blocks (idle ~8 us there while the conv2 blocks finish), so the fc
-        # chain launch ends with its dp2 tiles.  DMLC_FC_DW_WGRAD=0: the dW tiles stay in the chain.
+        # the plain bf16 conv2 dgrad (one image per workgroup) runs in the fc chain's workgroups, each
+        # once its dp2 row tile is published: one launch boundary less, but the hand-off (publish ->
+        # poll -> sc1 dp2 loads) costs ~2 us of it back.  Default: B > 192 (B=160 measured 0.2-1 us
+        # slower, profiles/r4_v6_fc_dgrad_ab.txt); DMLC_FC_DGRAD=1 / 0 forces it on / off.
+        fdg = os.environ.get("DMLC_FC_DGRAD", "auto")
+        self.fc_dgrad = (self.fc_fused and not self.fused_w1 and not self.fp8_dgrad and self.dgrad_split != 2
+                         and (fdg == "1" or (fdg != "0" and B > 192)))
+        self._dgrad_done = False
+        # single GPU, fused fc chain + apply mode: the fc weight-gradient tiles and every fc SGD can run
+        # in the wgrad launch's conv1 blocks (between their barrier arrival and the conv1 reduction),
+        # so the fc chain launch ends with its dp2 tiles.  Same-box A/B at B=256 (profiles/
+        # r4_v7_fc_dgrad_dw_ab.txt, us/step): chain dgrad off: dW in chain 81.8, in wgrad 80.4; chain
+        # dgrad on: dW in chain 79.8, in wgrad 80.2 -- so by default the dW tiles move to the wgrad
+        # launch only when the dgrad is not in the chain.  DMLC_FC_DW_WGRAD=1 / 0 forces it.
+        fdw = os.environ.get("DMLC_FC_DW_WGRAD", "auto")
         self.fc_dw_in_wgrad = (self.fc_fused and self.wgrad_apply
-                               and os.environ.get("DMLC_FC_DW_WGRAD", "1") != "0")
+                               and (fdw == "1" or (fdw != "0" and not self.fc_dgrad)))
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
                                                                         s_par=FC1_NUMEL)
@@ -484,7 +496,9 @@ class FusedCifarEngine:
                           p["full_weight_1"] if fused_sgd else gv["full_weight_1"], gv["full_weight_2"],
                           gv["full_weight_3"], gv["full_bias_1"], gv["full_bias_2"], gv["full_bias_3"], fused_sgd,
                           sched, self.Bv, self.step_t, self.step_sgd, self.fc_sync, self.wbar[10 * 32:10 * 32 + 1],
-                          not (fused_sgd and self.fc_dw_in_wgrad))
+                          not (fused_sgd and self.fc_dw_in_wgrad),
+                          *((self.am2, self.w2d, self.dp1, self.dy2) if self.fc_dgrad else ()))
+        self._dgrad_done = self.fc_dgrad
 
     def _conv_backward(self, src=None, apply: bool = False, reduce: bool = False):
         """apply: + the whole SGD in the wgrad launch (single GPU); reduce: + the conv slab reduction
@@ -500,7 +514,9 @@ class FusedCifarEngine:
                     self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw,
                     False)
             return
-        if self.fp8_dgrad:
+        if self._dgrad_done:
+            self._dgrad_done = False                 # the fc chain launch did it (fc_dgrad)
+        elif self.fp8_dgrad:
             o.conv2_dgrad_fp8(self.dp2, self.am2, self.w2f8[1], self.scale_w, self.dp1, self.dy2)
         elif self.dgrad_split == 2:
             o.conv2_dgrad_split(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)

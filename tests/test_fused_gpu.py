@@ -452,6 +452,61 @@ def test_fc_chain_launch_matches_three_launch_path(B, monkeypatch):
     assert abs(fused.read_stats(10)["loss"] - ref.read_stats(10)["loss"]) < 1e-2 * max(1.0, abs(ref.read_stats(10)["loss"]))
 
 
+@pytest.mark.parametrize("B", [160, 256])
+def test_dgrad_in_fc_chain_is_bit_identical(B, monkeypatch):
+    """The conv2 input gradient inside the fc chain launch (each workgroup's image once its dp2 row
+    tile's 18 column tasks have published) against the separate dgrad launch: dP1, dY2, every
+    gradient segment and the weights after eager + graph-replayed steps are bit-identical (the same
+    device function on the same operands; only the hand-off differs)."""
+    data, labels = _synthetic(8 * B, seed=63)
+    kw = dict(seed=64, lr=1e-3, relu_logits=False)
+    monkeypatch.setenv("DMLC_FC_DGRAD", "1")
+    fused = FusedCifarEngine(B, data, labels, **kw)
+    monkeypatch.setenv("DMLC_FC_DGRAD", "0")
+    ref = FusedCifarEngine(B, data, labels, **kw)
+    assert fused.fc_dgrad and not ref.fc_dgrad
+    idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(6))[:B].to(torch.int32)
+    for explicit in (None, idx):
+        g_ref = ref.compute_gradients(explicit).clone()
+        g_fus = fused.compute_gradients(explicit).clone()
+        torch.cuda.synchronize()
+        fused.check_barriers()
+        assert torch.equal(fused.dp2, ref.dp2)
+        assert torch.equal(fused.dy2, ref.dy2)
+        assert torch.equal(fused.dp1, ref.dp1)
+        assert torch.equal(g_fus, g_ref)
+    for eng in (fused, ref):
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(9)
+    torch.cuda.synchronize()
+    fused.check_barriers()
+    assert torch.equal(fused.master, ref.master)
+
+
+@pytest.mark.parametrize("B", [128, 256])
+def test_fc_dw_tiles_in_wgrad_launch_are_bit_identical(B, monkeypatch):
+    """The fc weight-gradient tiles + every fc SGD epilogue run in the wgrad launch's conv1 blocks
+    (DMLC_FC_DW_WGRAD=1) or in the fc chain (0): every epilogue applies the SGD kernel's expression,
+    so the weights after eager + graph-replayed steps are bit-identical either way."""
+    data, labels = _synthetic(8 * B, seed=65)
+    kw = dict(seed=66, lr=1e-3, relu_logits=False)
+    engs = []
+    for v in ("1", "0"):
+        monkeypatch.setenv("DMLC_FC_DW_WGRAD", v)
+        engs.append(FusedCifarEngine(B, data, labels, **kw))
+    assert engs[0].fc_dw_in_wgrad and not engs[1].fc_dw_in_wgrad
+    for eng in engs:
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(7)
+    torch.cuda.synchronize()
+    for eng in engs:
+        eng.check_barriers()
+    assert torch.isfinite(engs[0].master).all()
+    assert torch.equal(engs[0].master, engs[1].master)
+
+
 def test_fc_chain_graph_replay_is_deterministic(monkeypatch):
     """Two engines, same seed, same steps through the persistent fc chain: bit-identical weights
     (fixed-order split-K sums, no atomics on data)."""

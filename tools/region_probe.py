@@ -4,7 +4,12 @@ bench.py brackets them (synchronize -> t0 -> one graph replay of k steps -> sync
 A linear fit over k separates the per-step time (slope) from the per-region overhead (intercept:
 graph launch submission, the first kernel's dispatch after an idle queue, the final sync).
 
-  python tools/region_probe.py [--batch 256] [--reps 5]
+  python tools/region_probe.py [--batch 256] [--reps 5] [--poll] [--spin]
+
+--poll: busy-poll an event recorded after the replay (event.query()) before the closing synchronize
+        -- does the region's fixed cost sit in the host's wake-up from a blocking wait?
+--spin: hipSetDeviceFlags(hipDeviceScheduleSpin) on torch's HIP runtime before the device is
+        initialised (the runtime then spins instead of sleeping in every synchronize)
 """
 import argparse
 import json
@@ -25,7 +30,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--poll", action="store_true")
+    ap.add_argument("--spin", action="store_true")
     a = ap.parse_args()
+    if a.spin:
+        import ctypes
+        lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        rc = lib.hipSetDeviceFlags(ctypes.c_uint(1))      # hipDeviceScheduleSpin
+        print(f"hipSetDeviceFlags(spin) -> {rc}", file=sys.stderr)
     g = torch.Generator().manual_seed(0)
     data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g).cuda()
     labels = torch.randint(0, 10, (50000,), dtype=torch.int32, generator=g).cuda()
@@ -49,6 +61,11 @@ def main():
             t0 = time.perf_counter()
             eng.chains[k].replay()
             eng.host_step += k
+            if a.poll:
+                ev = torch.cuda.Event()
+                ev.record()
+                while not ev.query():
+                    pass
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e6)
         res[k] = min(ts)
@@ -62,7 +79,7 @@ def main():
         t0 = time.perf_counter()
         torch.cuda.synchronize()
         e.append((time.perf_counter() - t0) * 1e6)
-    print(json.dumps({"us_per_region": {str(k): round(v, 1) for k, v in res.items()},
+    print(json.dumps({"mode": "spin" if a.spin else "poll" if a.poll else "sync", "us_per_region": {str(k): round(v, 1) for k, v in res.items()},
                       "fit_us_per_step": round(float(slope), 2), "fit_region_overhead_us": round(float(icpt), 1),
                       "empty_sync_us": round(float(min(e)), 1)}))
 
