@@ -349,11 +349,13 @@ class FusedCifarEngine:
                           else torch.zeros(1, dtype=torch.int32))
         # the plain bf16 conv2 dgrad (one image per workgroup) runs in the fc chain's workgroups, each
         # once its dp2 row tile is published: one launch boundary less, but the hand-off (publish ->
-        # poll -> sc1 dp2 loads) costs ~2 us of it back.  Default: B > 192 (B=160 measured 0.2-1 us
-        # slower, profiles/r4_v6_fc_dgrad_ab.txt); DMLC_FC_DGRAD=1 / 0 forces it on / off.
+        # poll -> sc1 dp2 loads) costs ~2 us of it back.  With the fc dW tiles kept in the chain (below)
+        # it measured 1.8-2.5 us/step faster at B = 144 / 160 / 192 / 224 / 256 (profiles/
+        # r4_v8_fc_dgrad_b144_256_ab.txt); even at B = 128, where the split dgrad (2 workgroups per
+        # image) is the default.  DMLC_FC_DGRAD=1 / 0 forces it on / off.
         fdg = os.environ.get("DMLC_FC_DGRAD", "auto")
-        self.fc_dgrad = (self.fc_fused and not self.fused_w1 and not self.fp8_dgrad and self.dgrad_split != 2
-                         and (fdg == "1" or (fdg != "0" and B > 192)))
+        self.fc_dgrad = (self.fc_fused and not self.fused_w1 and not self.fp8_dgrad
+                         and (fdg == "1" or (fdg != "0" and self.dgrad_split != 2)))
         self._dgrad_done = False
         # single GPU, fused fc chain + apply mode: the fc weight-gradient tiles and every fc SGD can run
         # in the wgrad launch's conv1 blocks (between their barrier arrival and the conv1 reduction),
