@@ -8,6 +8,7 @@ graph launch submission, the first kernel's dispatch after an idle queue, the fi
 
 --poll: busy-poll an event recorded after the replay (event.query()) before the closing synchronize
         -- does the region's fixed cost sit in the host's wake-up from a blocking wait?
+--events: HIP events around the replay (GPU-side time of the k steps) + the replay call's host time
 --spin: hipSetDeviceFlags(hipDeviceScheduleSpin) on torch's HIP runtime before the device is
         initialised (the runtime then spins instead of sleeping in every synchronize)
 """
@@ -32,6 +33,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--poll", action="store_true")
     ap.add_argument("--spin", action="store_true")
+    ap.add_argument("--events", action="store_true", help="also: GPU time between events recorded around the "
+                    "replay, and the host time of the replay call itself")
     a = ap.parse_args()
     if a.spin:
         import ctypes
@@ -52,15 +55,23 @@ def main():
         eng.run(k)
     eng.run(256)
     torch.cuda.synchronize()
-    res = {}
+    res, host_us, ev_us = {}, {}, {}
     for k in ks:
         ts = []
         for _ in range(a.reps):
             eng.run(64)                          # busy before, as after bench.py's warm-up
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            if a.events:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            th = time.perf_counter()
             eng.chains[k].replay()
+            host_us.setdefault(k, []).append((time.perf_counter() - th) * 1e6)
             eng.host_step += k
+            if a.events:
+                e1.record()
             if a.poll:
                 ev = torch.cuda.Event()
                 ev.record()
@@ -68,6 +79,8 @@ def main():
                     pass
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e6)
+            if a.events:
+                ev_us.setdefault(k, []).append(e0.elapsed_time(e1) * 1000.0)
         res[k] = min(ts)
     x = np.array(ks, dtype=float)
     y = np.array([res[k] for k in ks])
@@ -81,7 +94,9 @@ def main():
         e.append((time.perf_counter() - t0) * 1e6)
     print(json.dumps({"mode": "spin" if a.spin else "poll" if a.poll else "sync", "us_per_region": {str(k): round(v, 1) for k, v in res.items()},
                       "fit_us_per_step": round(float(slope), 2), "fit_region_overhead_us": round(float(icpt), 1),
-                      "empty_sync_us": round(float(min(e)), 1)}))
+                      "empty_sync_us": round(float(min(e)), 1),
+                      "replay_call_us": {str(k): round(min(v), 1) for k, v in host_us.items()},
+                      "event_us": {str(k): round(min(v), 1) for k, v in ev_us.items()}}))
 
 
 if __name__ == "__main__":
