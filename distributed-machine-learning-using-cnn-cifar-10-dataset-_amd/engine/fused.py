@@ -487,6 +487,7 @@ class FusedCifarEngine:
         the preceding _forward(train=True).  fused_sgd: the fc1 weights are updated in the dW1
         epilogue (single GPU), else the fc1 weight gradient goes to the flat gradient."""
         assert self._fc_src is not None, "_fc_chain follows a training _forward"
+        assert not self._dgrad_done, "the previous fc chain's conv backward never ran"
         idx, counter, period = self._fc_src
         self._fc_src = None
         p, gv = self.pv, self.gv

@@ -165,7 +165,7 @@ def test_dp2_tune_schedule_agrees_across_ranks(tmp_path, allreduce):
     assert torch.isfinite(t0["flat"]).all()
 
 
-def _nccl1_rank(rank, world, port, out, steps, dtype="bf16"):
+def _nccl1_rank(rank, world, port, out, steps, dtype="bf16", B=32):
     sys.path.insert(0, REPO)
     import datetime
     import torch.distributed as dist
@@ -177,7 +177,7 @@ def _nccl1_rank(rank, world, port, out, steps, dtype="bf16"):
     x, y = _data()
     res = {}
     for sched in ("serial", "overlap"):
-        eng = FusedCifarEngine(32, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dp_force=True,
+        eng = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dp_force=True,
                                dp_schedule=sched, allreduce="rccl", dtype=dtype)
         assert eng.dp and eng.capture_comm and eng.single_graph, (eng.dp, eng.capture_comm)
         # the DP step reduces the conv slabs inside the wgrad launch (fp8 too: round 3 asserted here)
@@ -195,21 +195,23 @@ def _nccl1_rank(rank, world, port, out, steps, dtype="bf16"):
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
-def test_captured_rccl_allreduce_world1_equals_single_gpu(tmp_path, dtype):
+@pytest.mark.parametrize("dtype,B", [("bf16", 32), ("fp8", 32), ("bf16", 256)])
+def test_captured_rccl_allreduce_world1_equals_single_gpu(tmp_path, dtype, B):
     """The RCCL path with the all-reduce captured inside the step graph (capture_comm) and chained
     steps, on a 1-rank nccl group (dp_force: the DP step -- conv slabs reduced in the wgrad launch,
     all-reduce, apply-only SGD -- runs at world size 1).  A 1-rank sum is the identity, so it must
     equal the plain single-GPU step bit for bit, for both step schedules; fp8 (BASELINE config 5)
-    also compares the e4m3 weight shadows and the delayed scales."""
+    also compares the e4m3 weight shadows and the delayed scales.  B=256: the fc chain with the conv2
+    dgrad inside it and its dW tiles writing gradients (the DP form) against the single-GPU step's
+    fused-SGD epilogues."""
     import torch.multiprocessing as mp
     from dmlc.cli import free_port
     from dmlc.engine.fused import FusedCifarEngine
     steps = 11
-    mp.spawn(_nccl1_rank, args=(1, free_port(), str(tmp_path), steps, dtype), nprocs=1, join=True)
+    mp.spawn(_nccl1_rank, args=(1, free_port(), str(tmp_path), steps, dtype, B), nprocs=1, join=True)
     res = torch.load(tmp_path / "nccl1.pt", weights_only=True)
     x, y = _data()
-    ref = FusedCifarEngine(32, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dtype=dtype)
+    ref = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dtype=dtype)
     for _ in range(steps):
         ref.step()
     torch.cuda.synchronize()
