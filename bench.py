@@ -214,8 +214,7 @@ def main():
         if args.dp_schedule == "auto" and hasattr(eng, "tune_schedule") and info.world_size > 1:
             eng.tune_schedule(iters=max(10, args.warmup), steps_per_graph=args.steps_per_graph)
         # a short timed region replays as ONE graph of exactly --steps steps
-        if (args.steps <= 2 * args.steps_per_graph and hasattr(eng, "add_chain")
-                and os.environ.get("DMLC_BENCH_EXACT_CHAIN", "1") != "0"):
+        if args.steps <= 2 * args.steps_per_graph and hasattr(eng, "add_chain"):
             eng.add_chain(args.steps)
         # replay every captured chain once (first launches of a graph pay its upload): untimed
         # training steps on top of the W warm-up steps, reported as graph_warmup_steps

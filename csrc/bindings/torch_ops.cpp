@@ -211,99 +211,25 @@ void conv2_dgrad_fp8(const Tensor& dp2, const Tensor& am2, const Tensor& w2d8, c
   CHECK_HIP(dmlc_conv2_dgrad_fp8(&a, stream_of(dp2)));
 }
 
-void conv2_dgrad_w1(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const c10::optional<Tensor>& dp1,
-                    const Tensor& dy2, const Tensor& am1, const Tensor& xraw, int64_t cy, int64_t cx,
-                    const Tensor& part1, const Tensor& partb1) {
-  const int64_t B = dp2.size(0);
-  check(dp2, "dp2", at::kBFloat16, {B, 6, 6, 64});
-  check(am2, "am2", at::kByte, {B, 6, 6, 64});
-  check(w2d, "w2d", at::kBFloat16, {64, 1600});
-  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  check(am1, "am1", at::kByte, {B, 12, 12, 64});
-  TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
-  check(part1, "part1", at::kFloat, {B, 80, 64});
-  check(partb1, "partb1", at::kFloat, {B, 64});
-  c10::DeviceGuard guard(dp2.device());
-  DmlcConv2DgradArgs a;
-  a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
-  a.dp1 = nullptr;
-  if (dp1.has_value()) {
-    check(*dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
-    a.dp1 = dp1->data_ptr();
-  }
-  a.dy2 = dy2.data_ptr(); a.B = (int)B;
-  DmlcConv1WgradArgs w;
-  memset(&w, 0, sizeof(w));
-  w.xraw = xraw_ptr(xraw, B);
-  w.cy = (int)cy; w.cx = (int)cx;
-  w.am1 = am1.data_ptr<uint8_t>(); w.part1 = part1.data_ptr<float>(); w.partb1 = partb1.data_ptr<float>();
-  w.g1 = (int)B; w.B = (int)B;
-  CHECK_HIP(dmlc_conv2_dgrad_w1(&a, &w, stream_of(dp2)));
-}
-
-void conv1_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
-                 int64_t cy, int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1,
-                 const Tensor& partb1, const c10::optional<Tensor>& xraw) {
-  const int64_t B = dp1.size(0), g1 = part1.size(0);
-  check_data(data);
-  TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
-  TORCH_CHECK(g1 >= 1 && g1 <= B, "split-K groups must be in [1,B]");
-  check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
-  check(am1, "am1", at::kByte, {B, 12, 12, 64});
-  check(part1, "part1", at::kFloat, {g1, 80, 64});
-  check(partb1, "partb1", at::kFloat, {g1, 64});
-  c10::DeviceGuard guard(dp1.device());
-  DmlcConv1WgradArgs a;
-  a.data = data.data_ptr<uint8_t>(); a.src = index_src(idx, counter, period, B);
-  check_order_fits(a.src, data.size(0));
-  a.cy = (int)cy; a.cx = (int)cx;
-  a.dp1 = dp1.data_ptr(); a.am1 = am1.data_ptr<uint8_t>();
-  a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1; a.B = (int)B;
-  a.xraw = xraw_ptr(xraw, B);
-  CHECK_HIP(dmlc_conv1_wgrad(&a, stream_of(dp1)));
-}
-
-// conv2 weight-gradient slabs: [g2][1600][64] fp32 or bf16 (the two kernels agree via part2_bf16)
-static int check_part2(const Tensor& part2, int64_t g2) {
-  const bool b = part2.scalar_type() == at::kBFloat16;
-  check(part2, "part2", b ? at::kBFloat16 : at::kFloat, {g2, 1600, 64});
-  return b ? 1 : 0;
-}
-
-void conv2_wgrad(const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2) {
-  const int64_t B = p1.size(0), g2 = part2.size(0);
-  TORCH_CHECK(g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
-  check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
-  check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  const int p2b = check_part2(part2, g2);
-  check(partb2, "partb2", at::kFloat, {g2, 64});
-  c10::DeviceGuard guard(p1.device());
-  DmlcConv2WgradArgs a;
-  a.p1 = p1.data_ptr(); a.dy2 = dy2.data_ptr(); a.part2 = part2.data_ptr(); a.part2_bf16 = p2b;
-  a.partb2 = partb2.data_ptr<float>(); a.g2 = (int)g2; a.B = (int)B;
-  CHECK_HIP(dmlc_conv2_wgrad(&a, stream_of(p1)));
-}
-
+// conv2 weight-gradient slabs: [g2][1600][64] fp32
 static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter,
                                 int64_t period, int64_t cy, int64_t cx, const Tensor& dp1, const Tensor& am1,
                                 const Tensor& part1, const Tensor& partb1, const Tensor& p1, const Tensor& dy2,
                                 const Tensor& part2, const Tensor& partb2, int64_t groups2,
-                                const c10::optional<Tensor>& xraw, bool with_conv1) {
-  const int64_t B = p1.size(0), g1 = with_conv1 ? part1.size(0) : 0, g2 = groups2;
+                                const c10::optional<Tensor>& xraw) {
+  const int64_t B = p1.size(0), g1 = part1.size(0), g2 = groups2;
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
-  TORCH_CHECK((!with_conv1 || (g1 >= 1 && g1 <= B)) && g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
+  TORCH_CHECK(g1 >= 1 && g1 <= B && g2 >= 1 && g2 <= B, "split-K groups must be in [1,B]");
   TORCH_CHECK(part2.size(0) == g2, "wgrad: one conv2 slab per image group");
   TORCH_CHECK(g1 + 4 * g2 <= 1024, "wgrad: too many workgroups");
-  if (with_conv1) {
-    check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
-    check(am1, "am1", at::kByte, {B, 12, 12, 64});
-    check(part1, "part1", at::kFloat, {g1, 80, 64});
-    check(partb1, "partb1", at::kFloat, {g1, 64});
-  }
+  check(dp1, "dp1", at::kBFloat16, {B, 12, 12, 64});
+  check(am1, "am1", at::kByte, {B, 12, 12, 64});
+  check(part1, "part1", at::kFloat, {g1, 80, 64});
+  check(partb1, "partb1", at::kFloat, {g1, 64});
   check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
   check(dy2, "dy2", at::kBFloat16, {B, 144, 64});
-  const int p2b = check_part2(part2, g2);
+  check(part2, "part2", at::kFloat, {g2, 1600, 64});
   check(partb2, "partb2", at::kFloat, {g2, 64});
   DmlcWgradArgs a;
   memset(&a, 0, sizeof(a));                      // (fc_in_launch off unless wgrad_sgd sets it)
@@ -313,7 +239,7 @@ static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10
   a.w1.dp1 = dp1.data_ptr(); a.w1.am1 = am1.data_ptr<uint8_t>();
   a.w1.part1 = part1.data_ptr<float>(); a.w1.partb1 = partb1.data_ptr<float>(); a.w1.g1 = (int)g1; a.w1.B = (int)B;
   a.w1.xraw = xraw_ptr(xraw, B);
-  a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr(); a.w2.part2_bf16 = p2b;
+  a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr();
   a.w2.partb2 = partb2.data_ptr<float>(); a.w2.g2 = (int)g2; a.w2.B = (int)B;
   a.apply = 0; a.bar = nullptr; a.helpers = 0;
   memset(&a.sgd, 0, sizeof(a.sgd));
@@ -323,9 +249,9 @@ static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10
 void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
            int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
            const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2,
-           const c10::optional<Tensor>& xraw, bool with_conv1) {
+           const c10::optional<Tensor>& xraw) {
   DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
-                               groups2, xraw, with_conv1);
+                               groups2, xraw);
   c10::DeviceGuard guard(dp1.device());
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
 }
@@ -345,7 +271,7 @@ void gemm_grouped(at::TensorList A, at::TensorList Bm, at::TensorList C, const c
   DmlcGemmGroup G;
   memset(&G, 0, sizeof(G));
   G.nprob = n;
-  static const int xcd_map = getenv("DMLC_GEMM_XCD") ? atoi(getenv("DMLC_GEMM_XCD")) : 1;
+  static const int xcd_map = 1;    // XCD-aware tile order (cnn_gemm.hip)
   G.xcd_map = xcd_map;
   if (step.has_value()) {
     check_numel(*step, "step", at::kLong, 1);
@@ -579,7 +505,7 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
   const int64_t g1 = part1.size(0), g2 = part2.size(0);
   check(part1, "part1", at::kFloat, {g1, 80, 64});
   check(partb1, "partb1", at::kFloat, {g1, 64});
-  const int p2b = check_part2(part2, g2);
+  check(part2, "part2", at::kFloat, {g2, 1600, 64});
   check(partb2, "partb2", at::kFloat, {g2, 64});
   TORCH_CHECK(loss_part.numel() >= 1, "loss partials missing");
   const int64_t B = batch;
@@ -605,7 +531,7 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
   a.mode = (int)mode; a.grad_scale = (float)grad_scale;
   for (int i = 0; i < 10; ++i) a.off[i] = (int)off[i];
   a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1;
-  a.part2 = part2.data_ptr(); a.part2_bf16 = p2b; a.g2 = (int)g2;
+  a.part2 = part2.data_ptr(); a.g2 = (int)g2;
   a.partb2 = partb2.data_ptr<float>(); a.B = (int)B;
   a.w1f = w1f.data_ptr(); a.w2f = w2f.data_ptr(); a.w2d = w2d.data_ptr(); a.fc1n = fc1n.data_ptr();
   a.fc2t = fc2t.data_ptr(); a.fc2n = fc2n.data_ptr(); a.fc3t = fc3t.data_ptr(); a.fc3d = fc3d.data_ptr();
@@ -679,7 +605,7 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
                int64_t groups2, const Tensor& xraw, const Tensor& bar, DMLC_SGD_PARAMS,
                const c10::optional<at::TensorList> fc_acts) {
   DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
-                               groups2, xraw, true);
+                               groups2, xraw);
   TORCH_CHECK((mode == 0 && fc1_fused && step_rd.has_value() && roles == 0 && finalize &&
                grad_scale == 1.0) || (mode == 1 && roles == 0),
               "wgrad_sgd: the single-GPU mode-0 step (fc1 epilogue, the head's step copy) or mode 1 (reduce only)");
@@ -687,8 +613,7 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   a.sgd = make_sgd(DMLC_SGD_ARGS);
   a.apply = 1;
   a.bar = reinterpret_cast<unsigned int*>(bar.data_ptr<int>());
-  static const bool helpers = [] { const char* e = getenv("DMLC_WGRAD_HELPERS"); return !(e && e[0] == '0'); }();
-  a.helpers = helpers ? 1 : 0;
+  a.helpers = 1;
   a.fc_in_launch = 0;
   memset(&a.fc, 0, sizeof(a.fc));
   if (fc_acts.has_value()) {
@@ -719,8 +644,7 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
     f.lr0 = (float)lr0; f.decay = (float)decay; f.decay_steps = (float)decay_steps; f.staircase = staircase;
     f.warmup = (float)warmup; f.grad_scale = (float)grad_scale;
     f.err = a.bar + 10 * 32;
-    const char* first = getenv("DMLC_FC_DW_FIRST");
-    a.fc_in_launch = first && first[0] == '1' ? 2 : 1;
+    a.fc_in_launch = 1;
   }
   c10::DeviceGuard guard(dp1.device());
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
@@ -744,14 +668,9 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("conv2_fwd_split(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("conv2_dgrad_split(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv2_dgrad_fp8(Tensor dp2, Tensor am2, Tensor w2d8, Tensor scale_w, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
-  m.def("conv2_dgrad_w1(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!)? dp1, Tensor(b!) dy2, Tensor am1, Tensor xraw, "
-        "int cy, int cx, Tensor(c!) part1, Tensor(d!) partb1) -> ()");
-  m.def("conv1_wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
-        "Tensor(a!) part1, Tensor(b!) partb1, Tensor? xraw=None) -> ()");
-  m.def("conv2_wgrad(Tensor p1, Tensor dy2, Tensor(a!) part2, Tensor(b!) partb2) -> ()");
   m.def("wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor(a!) part1, Tensor(b!) partb1, Tensor p1, Tensor dy2, Tensor(c!) part2, Tensor(d!) partb2, "
-        "int groups2, Tensor? xraw=None, bool with_conv1=True) -> ()");
+        "int groups2, Tensor? xraw=None) -> ()");
   m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params, Tensor? step=None, "
         "Tensor(b!)? shadow=None, float[] sched=[]) -> ()");
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
@@ -794,9 +713,6 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("conv2_fwd_split", &conv2_fwd_split);
   m.impl("conv2_dgrad_split", &conv2_dgrad_split);
   m.impl("conv2_dgrad_fp8", &conv2_dgrad_fp8);
-  m.impl("conv2_dgrad_w1", &conv2_dgrad_w1);
-  m.impl("conv1_wgrad", &conv1_wgrad);
-  m.impl("conv2_wgrad", &conv2_wgrad);
   m.impl("wgrad", &wgrad);
   m.impl("gemm_grouped", &gemm_grouped);
   m.impl("head", &head);

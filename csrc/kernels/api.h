@@ -111,11 +111,10 @@ struct DmlcConv1WgradArgs {
 struct DmlcConv2WgradArgs {
   const void* p1;           // bf16 [B][12][12][64]   (conv2 input)
   const void* dy2;          // bf16 [B][144][64]      (conv2 pre-activation gradient)
-  void* part2;              // [g2][1600][64] fp32, or bf16 when part2_bf16
+  void* part2;              // [g2][1600][64] fp32
   float* partb2;            // [g2][64] conv2 bias-grad partials (written by the c4 == 0 blocks)
   int g2;
   int B;
-  int part2_bf16;           // slabs stored as bf16 (partial sums of g2-th of the batch, rounded once)
 };
 
 
@@ -205,7 +204,7 @@ struct DmlcFcArgs {
   float lr0, decay, decay_steps, warmup, grad_scale; int staircase;
   const int64_t* step; int64_t* step_copy;             // device step counter; copy for the SGD reader
   unsigned int* sync;                // >= 28 * 32 zeroed uints (counters re-arm themselves)
-  unsigned int* err;                 // sticky error word (bit 2: a seam wait timed out)
+  unsigned int* err;                 // sticky error word (value 2 = bit 1: a seam wait timed out)
 };
 
 // Fused SGD over the flat fp32 parameter buffer (+ split-K partial reduction, LR schedule from the
@@ -218,8 +217,7 @@ struct DmlcSgdArgs {
   // flat offsets of the 10 tensors, TF order
   int off[10];
   const float* part1; const float* partb1; int g1;   // conv1 partials [g1][80][64], [g1][64]
-  const void* part2; int g2;                         // conv2 partials [g2][1600][64] (fp32 or bf16)
-  int part2_bf16;
+  const void* part2; int g2;                         // conv2 partials [g2][1600][64] fp32
   const float* partb2; int B;                        // conv2 bias partials [g2][64]
   // bf16 shadows
   void* w1f; void* w2f; void* w2d; void* fc1n; void* fc2t; void* fc2n; void* fc3t; void* fc3d;
@@ -269,7 +267,7 @@ struct DmlcWgradArgs {
   DmlcConv2WgradArgs w2;
   int apply;
   unsigned int* bar;
-  int helpers;              // apply mode: idle conv1 blocks help reduce the conv2 slabs (DMLC_WGRAD_HELPERS=0 off)
+  int helpers;              // apply mode: idle conv1 blocks help reduce the conv2 slabs (always on)
   DmlcSgdArgs sgd;
   // apply mode with the fc chain (fc_in_launch): the conv1 blocks, whose conv1 work ends ~8 us before
   // the conv2 blocks', also run the fc weight-gradient tiles (dW1 / dW2 / dW3 + bias gradients,
@@ -292,9 +290,6 @@ hipError_t dmlc_conv2_dgrad_fp8(const DmlcConv2DgradFp8Args* a, hipStream_t s);
 hipError_t dmlc_fp8_roundtrip(const float* x, float* y, int n, float scale, hipStream_t s);
 hipError_t dmlc_conv2_dgrad(const DmlcConv2DgradArgs* a, hipStream_t s);
 // conv2 dgrad + the conv1 weight gradient of each image (one slab per image: w1->g1 == B, xraw set)
-hipError_t dmlc_conv2_dgrad_w1(const DmlcConv2DgradArgs* a, const DmlcConv1WgradArgs* w1, hipStream_t s);
-hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s);
-hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s);
 hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s);
 hipError_t dmlc_gemm_grouped(DmlcGemmGroup* g, hipStream_t s);
 // dg: null, or the conv2 dgrad of the same batch, run in the chain's workgroups (dg->dp2 == a->dp2;

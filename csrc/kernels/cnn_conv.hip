@@ -167,99 +167,6 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// conv2 dgrad + conv1 weight gradient of one image per workgroup in ONE launch.  The conv1 weight
-// gradient only needs what this block already holds -- the pool1 gradient dp1 (the conv2 dgrad
-// output, in LDS), the image's argmax bytes and raw pixels (LDS-DMA'd at entry, landed by the conv2
-// core's barriers) -- so it runs right here instead of in the weight-gradient launch, which is then
-// conv2 only (more CUs for it), and dp1 never goes through global memory.  One fp32 slab per image.
-// LDS: [0, 32K) conv2 core input, then the shifted planes (w1_common.h) | [32K, 50K) dp1 [144][64]
-// unswizzled | dp2 + argmax2 | weight slices (80 KB), then dY1 / the reduction buffer | argmax1 |
-// raw image.
-constexpr size_t DW_OUTS = C2_XIN * 2, DW_DP2 = DW_OUTS + C2_OUT * 2, DW_AM2 = DW_DP2 + 2304 * 2;
-constexpr size_t DW_WS = DW_AM2 + 2304, DW_AM1 = DW_WS + ((size_t)W1_DYT * 2 > WS_BYTES ? (size_t)W1_DYT * 2 : WS_BYTES);
-constexpr size_t DW_IMG = DW_AM1 + 9216, DW_LDS = DW_IMG + 3072;
-static_assert(DW_WS + WS_BYTES <= DW_AM1 && W1_FL_BYTES <= (size_t)W1_DYT * 2, "dgrad+w1 LDS map");
-static_assert((size_t)W1_XS * 2 <= DW_OUTS && DW_LDS <= 160 * 1024, "dgrad+w1 LDS map");
-
-// LDS-DMA of n KB (global 16-B aligned) into LDS: 1 KB per wave-instruction, waves round-robin
-DEV void dma_kb(void* lds, const void* src, int nkb, int w, int lane) {
-  for (int j = w; j < nkb; j += NT / 64)
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(src) + j * 1024 + lane * 16,
-                                     (LDS_AS void*)(reinterpret_cast<char*>(lds) + j * 1024), 16, 0, 0);
-}
-
-__global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_w1(DmlcConv2DgradArgs a, DmlcConv1WgradArgs w1) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* dyp = reinterpret_cast<bf16*>(smem);
-  bf16* outs = reinterpret_cast<bf16*>(smem + DW_OUTS);
-  bf16* dp2 = reinterpret_cast<bf16*>(smem + DW_DP2);
-  uint8_t* am2 = reinterpret_cast<uint8_t*>(smem + DW_AM2);
-  bf16* ws = reinterpret_cast<bf16*>(smem + DW_WS);
-  uint8_t* am1 = reinterpret_cast<uint8_t*>(smem + DW_AM1);
-  uint8_t* img = reinterpret_cast<uint8_t*>(smem + DW_IMG);
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = wave_id();
-  const int g = lane >> 4, li = lane & 15;
-  DMLC_STAMP(DMLC_TK_DGRAD, 0);
-  // the conv1 wgrad operands of this image: in flight during the whole conv2 dgrad
-  dma_kb(am1, w1.am1 + (size_t)b * 9216, 9, w, lane);
-  dma_kb(img, w1.xraw + (size_t)b * 3072, 3, w, lane);
-  stage16<288>(dp2, reinterpret_cast<const bf16*>(a.dp2) + (size_t)b * 2304, tid);
-  stage16<144>(am2, a.am2 + (size_t)b * 2304, tid);
-  ws_dma(reinterpret_cast<const bf16*>(a.wd), 0, ws, w, lane);  // kernel row 0 of the weights
-  bf16* dy2 = reinterpret_cast<bf16*>(a.dy2) + (size_t)b * 9216;
-  for (int s = tid; s < 2048; s += NT) {           // halo of the padded 16x16 grad image
-    const int pix = s >> 3, c = s & 7;
-    const int r = pix >> 4, col = pix & 15;
-    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(dyp + swzpad(pix, c)) = bf16x8{};
-  }
-  __syncthreads();
-  DMLC_STAMP(DMLC_TK_DGRAD, 1);
-  for (int task = tid; task < 36 * 8; task += NT) {
-    const int win = task >> 3, c = task & 7, py = win / 6, px = win - py * 6;
-    float o[4][8];
-    pool_bwd_2x2<6>(dp2, am2, py, px, c, o);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
-      const bf16x8 v = to_bf16x8(o[k]);
-      *reinterpret_cast<bf16x8*>(dyp + swzpad((y + 2) * 16 + x + 2, c)) = v;
-      *reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8) = v;
-    }
-  }
-  lds_barrier();   // publishes dyp only; the dy2 global stores need not drain here
-  DMLC_STAMP(DMLC_TK_DGRAD, 2);
-
-  conv2_tiles(reinterpret_cast<const bf16*>(a.wd), dyp, ws, w, g, li, tid, ws, [&](int ct, int t, const f32x4& acc) {
-    const int px = 16 * t + li, cb = 16 * ct + 4 * g;
-    *reinterpret_cast<bf16x4*>(outs + px * 64 + cb) = pack4(acc[0], acc[1], acc[2], acc[3]);
-  });
-  __syncthreads();                                 // dp1 complete; the core's LDS regions are free
-  DMLC_STAMP(DMLC_TK_DGRAD, 3);
-  if (a.dp1) {                                     // optional global copy (numerics tests)
-    bf16* dp1 = reinterpret_cast<bf16*>(a.dp1) + (size_t)b * 9216;
-    for (int s = tid; s < 1152; s += NT) *reinterpret_cast<bf16x8*>(dp1 + s * 8) = lds_b128(outs + s * 8);
-  }
-  // conv1 weight gradient of this image (w1_common.h)
-  bf16* xs = dyp;
-  bf16* dyt = ws;
-  const int ch = w & 1, ks = w >> 1;
-  w1_ones_plane15(xs, tid);
-  w1_zero_dy(dyt, tid);
-  lds_barrier();
-  w1_planes(xs, img, w1.cy, w1.cx, tid);
-  w1_pool_bwd(dyt, outs, am1, w, lane);            // ends with a barrier: dY1 and the planes complete
-  f32x4 acc[2][5];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int t = 0; t < 5; ++t) acc[h][t] = zero4();
-  w1_mfma(dyt, xs, acc, ks, ch, g, li);
-  __syncthreads();
-  w1_flush(reinterpret_cast<char*>(ws), acc, w1.part1 + (size_t)b * 80 * 64, w1.partb1 + b * 64, ks, ch, lane, tid);
-  DMLC_STAMP(DMLC_TK_DGRAD, 4);
-}
-
-// ---------------------------------------------------------------------------------------------
 // conv1 -> pool1 -> conv2 -> pool2 of one image in ONE launch (bf16 path): the images are
 // independent, so the pool1 output goes straight into conv2's zero-padded LDS input instead of
 // round-tripping through global memory and a second launch (p1 / am1 are still written for the
@@ -365,19 +272,6 @@ hipError_t dmlc_conv12_fwd(const DmlcConv1FwdArgs* a1, const DmlcConv2FwdArgs* a
   DMLC_LDS_OPTIN(&k_conv12_fwd, C12_LDS);
   if (a1->B != a2->B || a1->amax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_conv12_fwd, dim3(a1->B), dim3(NT), C12_LDS, s, *a1, *a2);
-  return hipGetLastError();
-}
-
-hipError_t dmlc_conv2_dgrad_w1(const DmlcConv2DgradArgs* a, const DmlcConv1WgradArgs* w1, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv2_dgrad_w1),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)DW_LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  if (a->B != w1->B || !w1->xraw || !w1->am1 || !w1->part1 || !w1->partb1 || w1->g1 != a->B) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_conv2_dgrad_w1, dim3(a->B), dim3(NT), DW_LDS, s, *a, *w1);
   return hipGetLastError();
 }
 

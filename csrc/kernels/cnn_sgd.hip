@@ -43,8 +43,7 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
     }
   }
   if (a.mode == 0 || a.mode == 1)
-    g = a.part2_bf16 ? split_sum_bf16<C2_SPLIT>(reinterpret_cast<const bf16*>(a.part2) + e, 1600 * 64, a.g2, lds, threadIdx.x)
-                     : split_sum<C2_SPLIT>(reinterpret_cast<const float*>(a.part2) + e, 1600 * 64, a.g2, lds, threadIdx.x);
+    g = split_sum<C2_SPLIT>(reinterpret_cast<const float*>(a.part2) + e, 1600 * 64, a.g2, lds, threadIdx.x);
   if (threadIdx.x >= T) return;
   if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[2] + e);
   if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[2] + e) = g; return; }

@@ -95,11 +95,6 @@ DEV void conv1_wgrad_block(const DmlcConv1WgradArgs& a, const int grp, char* sme
   DMLC_STAMP(DMLC_TK_W1, 4);
 }
 
-__global__ __launch_bounds__(W1T, 1) void k_conv1_wgrad(DmlcConv1WgradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv1_wgrad_block(a, blockIdx.x, smem);
-}
-
 // ---------------------------------------------------------------------------------------------
 constexpr int W2T = 512;
 // dY rows: 128 B with the 16-column tiles XOR-swizzled by row bits 1 and 3 -- the tr reads of rows
@@ -215,17 +210,14 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
     if (b == b0) DMLC_STAMP(DMLC_TK_W2, 4);
   }
   DMLC_STAMP(DMLC_TK_W2, 2);
-  // slab element e of this group: fp32, or bf16 (half the bytes the SGD reads back and the kernel
-  // boundary writes back from L2; each element is a partial sum over G-th of the batch, rounded once)
+  // slab element e of this group (fp32 partial sum over G-th of the batch)
   const size_t slab0 = (size_t)grp * 1600 * 64;
   auto put4 = [&](size_t e, const f32x4& v) {
     if (coh) st_sc1(buf_rsrc(a.part2), (uint32_t)(slab0 + e) * 4, v);
-    else if (a.part2_bf16) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.part2) + slab0 + e) = pack4(v[0], v[1], v[2], v[3]);
     else st_maybe_nt<kNtDefault>(reinterpret_cast<f32x4*>(reinterpret_cast<float*>(a.part2) + slab0 + e), v);
   };
   auto put1 = [&](size_t e, float v) {
     if (coh) st_sc1(buf_rsrc(a.part2), (uint32_t)(slab0 + e) * 4, v);
-    else if (a.part2_bf16) reinterpret_cast<bf16*>(a.part2)[slab0 + e] = (bf16)v;
     else reinterpret_cast<float*>(a.part2)[slab0 + e] = v;
   };
   __syncthreads();                             // every MFMA read of LDS is done: reuse it for staging
@@ -265,11 +257,6 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
     for (int i = 0; i < 4; ++i) put1((size_t)(24 * 64 + 16 * c4 + 4 * g + i) * 64 + 16 * w + li, acc[12][i]);
   }
   DMLC_STAMP(DMLC_TK_W2, 3);
-}
-
-__global__ __launch_bounds__(W2T, 1) void k_conv2_wgrad(DmlcConv2WgradArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  conv2_wgrad_block(a, blockIdx.x, 0, smem);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -539,22 +526,8 @@ __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
     step = *a.sgd.step_rd;
   }
   if (conv1) {
-    if (a.apply && a.fc_in_launch == 2) {
-      // variant: the fc weight-gradient tiles first (their inputs come from earlier launches)
-      const int parity = (int)(step & 1);
-      for (int d = blockIdx.x; d < FC_DW_TASKS; d += a.w1.g1) {
-        const CTask T = dw_ctask(d);
-        PreRegs R;
-        pre_issue(a.fc, T, parity, R, threadIdx.x);
-        dw_task<false>(a.fc, T, R, step, smem, threadIdx.x);
-      }
-      DMLC_STAMP(DMLC_TK_SGD, 3);
-      __syncthreads();
-    }
     conv1_wgrad_block(a.w1, blockIdx.x, smem, a.apply != 0);
-    if (a.apply && a.fc_in_launch == 2) {
-      conv1_apply(a, blockIdx.x, smem, g0, step);
-    } else if (a.apply && a.fc_in_launch) {
+    if (a.apply && a.fc_in_launch) {
       // arrive at the conv1 barrier, then the fc weight gradients + their SGD (inputs from earlier
       // launches: no waits) while the rest of the family arrives, then the conv1 reduction + SGD;
       // the conv2 help comes last, when the conv2 slabs are ready anyway (running the fc tiles
@@ -592,17 +565,6 @@ using namespace dmlc;
 
 extern "C" {
 
-hipError_t dmlc_conv1_wgrad(const DmlcConv1WgradArgs* a, hipStream_t s) {
-  DMLC_LDS_OPTIN(&k_conv1_wgrad, W1_LDS);
-  hipLaunchKernelGGL(k_conv1_wgrad, dim3(a->g1), dim3(W1T), W1_LDS, s, *a);
-  return hipGetLastError();
-}
-
-hipError_t dmlc_conv2_wgrad(const DmlcConv2WgradArgs* a, hipStream_t s) {
-  hipLaunchKernelGGL(k_conv2_wgrad, dim3(4 * a->g2), dim3(W2T), W2_LDS, s, *a);
-  return hipGetLastError();
-}
-
 hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s) {
   DMLC_LDS_OPTIN(&k_wgrad, WG_LDS);
   const int blocks = a->w1.g1 + 4 * a->w2.g2;
@@ -624,7 +586,7 @@ hipError_t dmlc_wgrad(const DmlcWgradArgs* a, hipStream_t s) {
     if (a->fc_in_launch && (g.mode != 0 || !g.fc1_fused || a->fc.fuse_sgd != 2 || a->fc.B < 16 || a->fc.B > 256 ||
                             !a->fc.p2 || !a->fc.dh1 || !a->fc.mw2 || !a->fc.fc2t))
       return hipErrorInvalidValue;
-    if (a->w1.g1 < 1 || a->w1.g1 > cus || 4 * a->w2.g2 > cus || a->w2.part2_bf16 || !a->bar || !a->w1.xraw ||
+    if (a->w1.g1 < 1 || a->w1.g1 > cus || 4 * a->w2.g2 > cus || !a->bar || !a->w1.xraw ||
         !ok_mode || g.part1 != a->w1.part1 ||
         g.part2 != a->w2.part2 || g.g1 != a->w1.g1 || g.g2 != a->w2.g2 || g.bidx_n > a->w1.g1 * W1T)
       return hipErrorInvalidValue;

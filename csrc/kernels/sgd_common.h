@@ -77,35 +77,6 @@ DEV float4 split_sum(const float* __restrict__ p, size_t stride, int n, float4* 
   return t;
 }
 
-// The same over bf16 slabs (4 bf16 = 8 bytes per slab and thread), summed in fp32 in the same order.
-DEV float4 bf4(uint2 u) {
-  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
-                     __uint_as_float(u.y & 0xffff0000u));
-}
-template <int S, int U = 8>
-DEV float4 split_sum_bf16(const bf16* __restrict__ p, size_t stride, int n, float4* lds, int tid) {
-  constexpr int T = 256 / S;
-  const int sp = tid / T, idx = tid % T;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (tid < 256) {
-    for (int q = sp; q < n; q += U * S) {
-      uint2 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        v[u] = load_sel(reinterpret_cast<const uint2*>(p + (size_t)(q + u * S) * stride), reinterpret_cast<const uint2*>(p),
-                        q + u * S < n);
-#pragma unroll
-      for (int u = 0; u < U; ++u) s = add4(s, bf4(v[u]));
-    }
-    lds[tid] = s;
-  }
-  __syncthreads();
-  float4 t = lds[idx];
-#pragma unroll
-  for (int k = 1; k < S; ++k) t = add4(t, lds[k * T + idx]);
-  return t;
-}
-
 // w: the master value, loaded by the caller BEFORE the slab reduction so that its memory latency
 // overlaps the slab loads instead of adding a second dependent round trip
 DEV float4 sgd4(float* m, float4 w, float4 g, float lr, float scale, bool apply) {

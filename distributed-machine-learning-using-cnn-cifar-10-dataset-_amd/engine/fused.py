@@ -1,36 +1,45 @@
 """Fused MI355X training engine for the reference CNN (hand-written HIP kernels + HIP graphs + RCCL).
 
 One training step (= one ``mon_sess.run([train_op, loss])`` of /root/reference/cifar10cnn.py:230,
-SURVEY.md §3.3) is six kernel launches on the single-GPU bf16 path (B > 128), all reading their
-inputs from device memory:
+SURVEY.md §3.3) is THREE kernel launches on the single-GPU bf16 path at 128 < B <= 256, all reading
+their inputs from device memory:
 
   1 conv12_fwd   uint8 gather + center crop + conv1 + bias + ReLU + pool1 (+argmax), handed through
                  LDS to conv2 + bias + ReLU + pool2 (+argmax) -- one workgroup per image
-  2 gemm         fc1 forward, split-K fp32 partials
-  3 head         fc1 reduce/bias/ReLU, fc2, fc3, ReLU-logits, softmax-xent, accuracy, dlogits→dh2→dh1
-  4 gemm (x7)    fc1 dgrad + dW1 + dW2 + dW3 + db1 + db2 + db3 in ONE grouped launch
-  5 conv2_dgrad  pool2/ReLU backward (2x2-ownership gather) + conv2 input-gradient
-  6 wgrad        ONE launch, two block roles: pool1/ReLU backward + conv1 weight/bias gradients,
-                 and conv2 weight/bias gradients per (input-channel quarter, image group); split-K slabs
-                 ... and, on one GPU, the whole SGD (wgrad_apply, cnn_wgrad.hip): each slab family meets
-                 at a sub-grid barrier and every block reduces its share of the slabs in the SGD
-                 kernel's order and applies the update; the conv1 blocks also update fc2/fc3/biases,
-                 publish the stats and bump global_step (the fc1 weights were updated in launch 4's
-                 epilogue)
-  7 sgd          (data parallel, fp8, or DMLC_WGRAD_SGD=0) slab reduction + SGD + LR schedule + bf16
-                 shadow refresh + global_step++ + stats
+  2 fc_chain     one persistent launch (cnn_fc.hip): fc1 forward (split-K tiles) -> MLP head (fc1
+                 reduce / bias / ReLU, fc2, fc3, ReLU logits, softmax xent, accuracy, dlogits -> dh2 ->
+                 dh1) -> dp2 = dh1 W1^T tiles + the fc weight-gradient tiles with the fc1 SGD in their
+                 epilogue -> the conv2 input gradient of each workgroup's image (pool2/ReLU backward
+                 gather + conv2 dgrad, conv2_core.h) once its dp2 row tile is published
+  3 wgrad        pool1/ReLU backward + conv1 weight/bias gradients and conv2 weight/bias gradients
+                 (split-K slabs), then -- on one GPU -- the whole rest of the SGD in the same launch
+                 (sub-grid barrier per slab family, every block reduces its share in the SGD kernel's
+                 order and applies the update + bf16 shadows; the stats, global_step and the next
+                 step's batch rows too)
 
-At B <= 128 (conv_split = 2, cnn_split.hip) launch 1 becomes conv1_fwd_split + conv2_fwd_split and
-launch 5 conv2_dgrad_split (two or four workgroups per image, so a small batch fills the 256 CUs):
-seven launches.  The fp8 path runs conv1 and conv2 forward as two launches.
+At B <= 128 launch 1 becomes conv1_fwd_split + conv2_fwd_split (cnn_split.hip, two or four
+workgroups per image so a small batch fills the 256 CUs) and the conv2 input gradient runs as its
+own channel-split launch (conv2_dgrad_split) with the fc weight-gradient tiles in the wgrad launch:
+five launches.  B > 256 (and ranks sharing one GPU) use the three-launch fc path (grouped fc1 GEMM,
+head, grouped backward GEMM).  The fp8 path (BASELINE config 5) runs conv1 and the fp8 conv2 forward
+as two launches, the fp8 conv2 dgrad as its own launch and the SGD as its own launch.
+
+Data parallel (N > 1): the wgrad launch reduces the conv slabs into the flat gradient instead of
+applying them, then the gradient is exchanged and applied -- serial schedule: one all-reduce of the
+whole flat gradient (xGMI peer-to-peer kernel or RCCL) and one SGD launch; overlap schedule: the fc
+bucket on a comm stream beside the conv backward.
 
 Every data-consuming kernel computes its batch rows from the device-resident global_step and the
 generated epoch order (data/order.py: a keyed Feistel permutation per epoch, no index buffer), so
 the whole step is a static HIP graph and ``k`` consecutive steps -- across epoch boundaries -- are
 one graph replay.  Any batch size works: the kernels run on the batch padded to the 16-row tile and
-the head gives padding rows zero loss weight (their gradients are exactly zero).  With data parallelism the fc
-gradients (90 % of the bytes, complete after launch 5) are all-reduced over RCCL on a side stream
-while launches 6-7 run, then the conv bucket, then the SGD applies.
+the head gives padding rows zero loss weight (their gradients are exactly zero).
+
+Variants: every default below is the measured-fastest path of its configuration; the alternatives
+that stay are the bitwise references the tests compare against, selected with the ``variant``
+dict of the constructor (VARIANT_DEFAULTS).  Two environment switches turn a persistent,
+co-residency-dependent launch off without code changes: DMLC_FC_FUSED=0 (the fc chain) and
+DMLC_WGRAD_SGD=0 (the in-launch SGD / slab reduction of the wgrad launch).
 """
 from __future__ import annotations
 
@@ -57,15 +66,26 @@ def _ops():
 
 
 SEG_OFF = [s.offset for s in M.PARAM_SPECS]
-# batch rows per head workgroup (2 or 4; DMLC_HEAD_ROWS overrides it for A/B runs).  Default: 2 up
-# to B=256 (more workgroups on the otherwise idle chip: 82.6-83.1 vs 83.1-83.5 us per step at B=256,
-# profiles/r2_v26_head_rows_groups_sweep.txt; same-session bench.py A/B at 400 steps 3.14-3.16 M vs
-# 3.12-3.15 M, profiles/r2_v27_head_rows_ab_b256.txt), 4 above (each workgroup streams all of fc2).
-HEAD_ROWS_ENV = os.environ.get("DMLC_HEAD_ROWS")
 
 
 def head_rows(B: int) -> int:
-    return int(HEAD_ROWS_ENV) if HEAD_ROWS_ENV else (2 if B <= 256 else 4)
+    """Batch rows per workgroup of the three-launch path's head kernel: 2 up to B=256 (more
+    workgroups on the otherwise idle chip, profiles/r2_v26_head_rows_groups_sweep.txt), 4 above
+    (each workgroup streams all of fc2)."""
+    return 2 if B <= 256 else 4
+
+
+# The engine's path choices (constructor ``variant=``).  None = chosen per configuration.
+VARIANT_DEFAULTS = {
+    "split_fwd": False,        # conv1 and conv2 forward as two launches (bitwise reference of conv12_fwd)
+    "fc_fused": None,          # the persistent fc chain (B <= 256, one rank per GPU); env DMLC_FC_FUSED=0 off
+    "fc_dgrad": None,          # conv2 dgrad inside the fc chain (default: when the dgrad is one WG per image)
+    "fc_dw_in_wgrad": None,    # fc dW tiles in the wgrad launch (default: when the dgrad is not in the chain)
+    "fc1_epilogue": True,      # single GPU: the fc1 update in the dW1 epilogue
+    "wgrad_sgd": True,         # in-launch SGD / slab reduction of the wgrad launch; env DMLC_WGRAD_SGD=0 off
+    "wgrad_sgd_fp8": False,    # the same for --dtype fp8 (bit-identical, measured 1.4 % slower at B=1024)
+    "fp8_dgrad": True,         # fp8: the conv2 input gradient on e4m3 too
+}
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
 # int32 words of the wgrad apply-mode barriers (DMLC_WBAR_WORDS); the last line is the error word
@@ -95,7 +115,12 @@ class FusedCifarEngine:
                  capture_comm: Optional[bool] = None, dtype: str = "bf16", allreduce: str = "auto",
                  dp_schedule: str = "serial", dp_force: bool = False, warmup_steps: int = 0,
                  conv_split: Optional[int] = None, conv1_split: Optional[int] = None,
-                 w2_slab: Optional[str] = None):
+                 dgrad_split: Optional[int] = None, variant: Optional[dict] = None):
+        unknown = set(variant or {}) - set(VARIANT_DEFAULTS)
+        if unknown:
+            raise ValueError(f"unknown engine variant keys {sorted(unknown)}")
+        V = dict(VARIANT_DEFAULTS, **(variant or {}))
+        self.variant = V
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -115,8 +140,7 @@ class FusedCifarEngine:
         self.cy, self.cx = crop_offset
         self.comm_dtype = comm_dtype
         if capture_comm is None:     # RCCL collectives go into the step graph unless told otherwise
-            capture_comm = (self.dp and self._pg_backend() == "nccl"
-                            and os.environ.get("DMLC_CAPTURE_COMM", "1") != "0")
+            capture_comm = self.dp and self._pg_backend() == "nccl"
         self.capture_comm = bool(capture_comm)
         self.seed = seed
         if dtype not in ("bf16", "fp8"):
@@ -171,9 +195,9 @@ class FusedCifarEngine:
         self.fc3t, self.fc3d = z(16, 192), z(192, 32)
         # fp8 conv2 forward + input gradient (BASELINE config 5): e4m3 weight shadows [0] forward
         # (co-major) and [1] the dgrad's flipped ci-major copy, delayed per-tensor weight scale;
-        # DMLC_FP8_DGRAD=0 keeps the conv2 input gradient in bf16
+        # variant fp8_dgrad=False keeps the conv2 input gradient in bf16
         self.fp8 = dtype == "fp8"
-        self.fp8_dgrad = self.fp8 and os.environ.get("DMLC_FP8_DGRAD", "1") != "0"
+        self.fp8_dgrad = self.fp8 and bool(V["fp8_dgrad"])
         if self.fp8:
             self.w2f8 = z(2, 64, 1600, dt=torch.uint8)
             self.amax_x = z(B, dt=torch.float32)      # per-image activation maxima (conv1 -> conv2)
@@ -181,62 +205,32 @@ class FusedCifarEngine:
             self.scale_w = z(2, dt=torch.float32)
 
         # --- activations / workspaces -------------------------------------------------------
-        self.fc1_split = fc1_split or int(os.environ.get("DMLC_FC1_SPLIT", "0") or 0) or self._pick_fc1_split(B)
-        # both weight gradients run in ONE launch (ops.wgrad: no stream fork/join in the graph);
-        # DMLC_SPLIT_WGRAD=1 runs them as two kernels on forked streams instead (A/B comparisons)
-        self.merged_wgrad = os.environ.get("DMLC_SPLIT_WGRAD", "0") != "1"
-        # conv1 and conv2 forward in one launch (bf16 path; DMLC_SPLIT_FWD=1: two launches)
-        self.fused_fwd = os.environ.get("DMLC_SPLIT_FWD", "0") != "1"
+        self.fc1_split = fc1_split or self._pick_fc1_split(B)
+        # conv1 and conv2 forward in one launch (bf16 path; variant split_fwd: two launches)
+        self.fused_fwd = not V["split_fwd"]
         # channel-split convolutions (cnn_split.hip): conv_split = 2 runs conv1 forward (conv1_split =
         # 2 or 4 workgroups per image), conv2 forward and the conv2 input gradient as 2 workgroups per
         # image, so a small batch fills the 256 CUs; 1 = one workgroup per image (cnn_conv.hip).
-        # DMLC_CONV_SPLIT / DMLC_CONV1_SPLIT override (A/B runs).
-        env_cs = int(os.environ.get("DMLC_CONV_SPLIT", "0")) or None
-        env_c1 = int(os.environ.get("DMLC_CONV1_SPLIT", "0")) or None
         # same-session A/B (r3): B=128 73.5 us (split, conv1 2-way) vs 74.6 (conv1 4-way) vs 79.0 (one
         # workgroup per image); B=256 85.1 vs 82.9 -- the split pays only while the chip is not full
-        self.conv_split = 1 if self.fp8 else (conv_split or env_cs or (2 if B <= 128 else 1))
-        self.conv1_split = conv1_split or env_c1 or 2
-        # the conv2 input gradient's split, independently of the forward's (DMLC_DGRAD_SPLIT, A/B runs)
-        self.dgrad_split = 1 if self.fp8 else int(os.environ.get("DMLC_DGRAD_SPLIT", "0") or 0) or self.conv_split
-        if self.conv_split not in (1, 2) or self.conv1_split not in (2, 4):
-            raise ValueError(f"conv_split must be 1 or 2 and conv1_split 2 or 4 ({self.conv_split}, {self.conv1_split})")
-        # DMLC_FUSED_W1=1: the conv1 weight gradient inside the conv2-dgrad launch (one slab per image,
-        # dp1 stays in LDS) and a conv2-only weight-gradient launch on the whole chip.  Measured at
-        # B=256 (r2): dgrad+w1 18.4 us + conv2 wgrad (40 pairs) 18.7 us = 37.1 us vs dgrad 11.2 us +
-        # merged wgrad ~26 us -- equal, and the SGD pays for 256 per-image slabs: off by default.
-        self.fused_w1 = self.merged_wgrad and os.environ.get("DMLC_FUSED_W1", "0") == "1"
+        self.conv_split = 1 if self.fp8 else (conv_split or (2 if B <= 128 else 1))
+        self.conv1_split = conv1_split or 2
+        # the conv2 input gradient's split, independently of the forward's
+        self.dgrad_split = 1 if self.fp8 else (dgrad_split or self.conv_split)
+        if self.conv_split not in (1, 2) or self.conv1_split not in (2, 4) or self.dgrad_split not in (1, 2):
+            raise ValueError(f"conv_split / dgrad_split must be 1 or 2 and conv1_split 2 or 4 "
+                             f"({self.conv_split}, {self.dgrad_split}, {self.conv1_split})")
         self.keep_dp1 = False          # tests: also write the pool1 gradient to global memory
-        # single-GPU step with the fc weight gradients + fc SGD on a second graph branch (they feed
-        # nothing on the conv backward path): main = dp2 GEMM -> conv backward -> (join) -> conv SGD;
-        # side = dW1/dW2/dW3/db GEMMs -> fc SGD.  DMLC_FC_BRANCH=0/1 overrides the default.
-        self.fc_branch = os.environ.get("DMLC_FC_BRANCH", "0") == "1"
-        # conv2 weight gradient: one block per (input-channel quarter, image group), one fp32 slab per
-        # group (self.g2 = groups = slabs the SGD kernel reduces); conv1: one block per image group.
-        # DMLC_W2_GROUPS / DMLC_W1_GROUPS override the defaults (kbench sweeps).
-        env_g2 = int(os.environ.get("DMLC_W2_GROUPS", "0")) or None
-        env_g1 = int(os.environ.get("DMLC_W1_GROUPS", "0")) or None
-        g2 = g2 or env_g2
-        g1 = g1 or env_g1
-        if self.fused_w1:
-            # conv1 runs inside the conv2-dgrad launch (one slab per image): the conv2 weight
-            # gradient has the whole chip
-            self.g2 = g2 or max(1, min(B, 64, round(B / 4)))
-            self.g1 = B
-        elif self.merged_wgrad:
-            # both in one launch of g1 + 4 * g2 <= 256 blocks (one wave of workgroups); multiples of 8
-            # keep every group's images on one XCD (cnn_wgrad.hip).  B=256: 128 + 4*32 -> 19.1 us vs
-            # 96 + 4*40 -> 19.8, 64 + 4*48 -> 23.4 (r2, register-staged conv1 scatter)
-            # (B=128: 32 groups of 4 images -> 69.2 us per step vs 16 groups of 8 -> 73.7, r3 sweep;
-            # B=256: 32 -> 81.7 vs 24 -> 85.1, 40 -> 83.1, 48 -> 86.8)
-            g2_ = max(1, min(B, 32, B // 4))
-            self.g2 = g2 or (g2_ // 8 * 8 if g2_ >= 8 else g2_)
-            # conv1: the CUs the conv2 blocks leave (one block per CU; past B=256 every block takes
-            # several images instead of the grid growing beyond the chip)
-            self.g1 = g1 or max(1, min(B, 256 - 4 * self.g2))
-        else:
-            self.g2 = g2 or max(1, min(B, B // 6))      # conv2 wgrad: 4 ci-quarter blocks x ~6 images per group
-            self.g1 = g1 or max(1, min(B, B // 2))      # conv1 wgrad: 2 images per block
+        # Both weight gradients run in ONE launch (ops.wgrad) of g1 + 4 * g2 <= 256 blocks (one wave
+        # of workgroups): conv2 one block per (input-channel quarter, image group), one fp32 slab per
+        # group (g2 = slabs the reduction sums); conv1 one block per image group on the CUs the conv2
+        # blocks leave.  Multiples of 8 keep every group's images on one XCD (cnn_wgrad.hip).
+        # B=128: 32 groups of 4 images -> 69.2 us per step vs 16 groups of 8 -> 73.7 (r3 sweep);
+        # B=256: 32 -> 81.7 vs 24 -> 85.1, 40 -> 83.1, 48 -> 86.8.  Past B=256 every conv1 block takes
+        # several images instead of the grid growing beyond the chip.
+        g2_ = max(1, min(B, 32, B // 4))
+        self.g2 = g2 or (g2_ // 8 * 8 if g2_ >= 8 else g2_)
+        self.g1 = g1 or max(1, min(B, 256 - 4 * self.g2))
         self.groups2 = self.g2
         self.p1, self.am1 = z(B, 12, 12, 64), z(B, 12, 12, 64, dt=torch.uint8)
         self.p2, self.am2 = z(B, 6, 6, 64), z(B, 6, 6, 64, dt=torch.uint8)
@@ -245,27 +239,20 @@ class FusedCifarEngine:
         self.dh1, self.dh2 = z(B, 384), z(B, 192)
         self.dp2 = z(B, 6, 6, 64)
         self.dp1, self.dy2 = z(B, 12, 12, 64), z(B, 144, 64)
-        # conv2 weight-gradient slabs (each a partial sum over 1/g2 of the batch, summed in fp32 by the
-        # SGD): fp32 by default.  "bf16" halves the 13 MB the wgrad writes and the SGD reads at g2=32
-        # (r3, same session: B=256 80.9 vs 82.2 us, B=128 68.1 vs 69.5) but adds a 4e-4 relative error
-        # to the conv2 weight gradient (fp32 slabs: 1e-7) and the loss-curve parity test's transient
-        # window then drifts 7 % from the fp32 eager engine (fp32 slabs: 2 %): opt-in only
-        # (w2_slab="bf16" or DMLC_W2_SLAB=bf16)
-        self.w2_slab = w2_slab or os.environ.get("DMLC_W2_SLAB", "fp32")
-        if self.w2_slab not in ("bf16", "fp32"):
-            raise ValueError(f"w2_slab must be bf16 or fp32, got {self.w2_slab!r}")
-        sdt = torch.bfloat16 if self.w2_slab == "bf16" else torch.float32
-        self.part2, self.partb2 = z(self.g2, 1600, 64, dt=sdt), z(self.g2, 64, dt=torch.float32)
+        # conv weight-gradient slabs: fp32 partial sums over 1/g of the batch each, summed in fixed
+        # order.  (bf16 conv2 slabs measured 1.3 us/step faster in r3 but added a 4e-4 relative error
+        # to the conv2 weight gradient and a 7 % drift in the loss-curve parity test: not kept.)
+        self.part2, self.partb2 = z(self.g2, 1600, 64, dt=torch.float32), z(self.g2, 64, dt=torch.float32)
         self.part1, self.partb1 = z(self.g1, 80, 64, dt=torch.float32), z(self.g1, 64, dt=torch.float32)
         # the whole fc chain of a training step (fc1 forward, head, fc backward) as ONE persistent
         # launch (cnn_fc.hip) instead of three: B <= 256, 256 co-resident workgroups (one per CU, so
-        # not when several ranks share a GPU), not beside the fc-branch graph.  DMLC_FC_FUSED=0 off.
+        # not when several ranks share a GPU).  DMLC_FC_FUSED=0 turns it off.
         local_ = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
         ndev_ = torch.cuda.device_count() if dev.type == "cuda" else 0
-        cus_ = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
-        self.fc_fused = (B <= 256 and cus_ >= 256 and local_ <= max(1, ndev_)
-                         and os.environ.get("DMLC_FC_BRANCH", "0") != "1"
-                         and os.environ.get("DMLC_FC_FUSED", "1") != "0")
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
+        fc_ok = B <= 256 and cus >= 256 and local_ <= max(1, ndev_)
+        self.fc_fused = (fc_ok if V["fc_fused"] is None else bool(V["fc_fused"]) and fc_ok) \
+            and os.environ.get("DMLC_FC_FUSED", "1") != "0"
         self.h1part8 = z(8, B, 384, dt=torch.float32) if self.fc_fused else None
         self.fc_sync = torch.zeros(28 * 32, dtype=torch.int32, device=dev)
         self._fc_src = None
@@ -275,10 +262,9 @@ class FusedCifarEngine:
         self.loss_part = z(B // hr, dt=torch.float32)
         self.correct_part = z(B // hr, dt=torch.int32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
-        # the head kernel copies the step counter here; the SGD launch reads the copy, so one of its
-        # workgroups can bump step_t without an arrival ticket (cnn_sgd.hip)
+        # the head kernel copies the step counter here; the SGD (launch or in-launch) reads the copy,
+        # so one of its workgroups can bump step_t without an arrival ticket (cnn_sgd.hip)
         self.step_sgd = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.sgd_ticket = os.environ.get("DMLC_SGD_TICKET", "0") == "1"   # A/B: the last-arriver ticket
         self.ticket = torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)   # two-level arrival counters
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
         self.logits_buf = z(B, 10, dt=torch.float32)
@@ -288,7 +274,7 @@ class FusedCifarEngine:
         gv = {k: self.grad[s.offset:s.offset + s.numel] for k, s in SEG.items()}
         self.gv = gv
 
-        # grouped GEMM problem lists
+        # grouped GEMM problem lists (the three-launch fc path)
         self._fc1_fwd = dict(A=[self.p2.view(B, 2304)], B=[self.fc1n], C=[self.h1part], bias=[None],
                              params=_gemm_params(B, 384, 2304, 2304, 1, 384, 0, 384, 2, self.fc1_split,
                                                  b_par=FC1_NUMEL))
@@ -305,42 +291,31 @@ class FusedCifarEngine:
                     + _gemm_params(384, 8, B, 384, 0, 8, 0, 1, 3, nvalid=384)      # db1
                     + _gemm_params(192, 8, B, 192, 0, 8, 0, 1, 3, nvalid=192)      # db2
                     + _gemm_params(16, 8, B, 16, 0, 8, 0, 1, 3, nvalid=10)))       # db3
-        # the same problems as two launches: dp2 (conv backward path) | the fc weight / bias gradients
         fb = self._fc_bwd
-        self._fc_dx = {k: fb[k][:1] for k in ("A", "B", "C", "bias")}
-        self._fc_dx["params"] = fb["params"][:14]
-        self._fc_dw = {k: fb[k][1:] for k in ("A", "B", "C", "bias")}
-        self._fc_dw["params"] = fb["params"][14:]
         # single GPU: the same launch with dW1 as a fused SGD epilogue (c_mode 4) -- the fc1 weights
         # (83 % of the parameters) are updated where their gradient is produced instead of the fp32
         # gradient going through HBM to the SGD kernel (which then updates the fc1 bias only).
-        # Bitwise the same update (same lr expression, same fp32 arithmetic); DMLC_FC1_EPILOGUE=0 off
-        self.fc1_epilogue = (not self.dp and not self.fc_branch
-                             and os.environ.get("DMLC_FC1_EPILOGUE", "1") != "0")
+        # Bitwise the same update (same lr expression, same fp32 arithmetic); variant fc1_epilogue off
+        self.fc1_epilogue = not self.dp and bool(V["fc1_epilogue"])
         # single GPU + fc1 epilogue: the merged weight-gradient launch also runs the rest of the SGD
         # (cnn_wgrad.hip apply mode: sub-grid barriers per slab family, the SGD kernel's reduction
         # order -> bit-identical weights) and the step has no SGD launch.  DMLC_WGRAD_SGD=0 off.
-        cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
-        in_launch = (self.merged_wgrad and not self.fused_w1 and self.w2_slab == "fp32"
-                     and 1 <= self.g1 <= cus and 4 * self.g2 <= cus
+        in_launch = (1 <= self.g1 <= cus and 4 * self.g2 <= cus and bool(V["wgrad_sgd"])
                      and os.environ.get("DMLC_WGRAD_SGD", "1") != "0")
         # fp8: bit-identical too (the e4m3 shadows + amax slots in-launch), but measured slower at
-        # B=1024 (207.5 vs 204.7 us, profiles/r3_fp8_wgrad_sgd_ab.txt): opt-in DMLC_WGRAD_SGD_FP8=1
-        self.wgrad_apply = (in_launch and self.fc1_epilogue and not self.sgd_ticket
-                            and (not self.fp8 or os.environ.get("DMLC_WGRAD_SGD_FP8", "0") == "1"))
+        # B=1024 (207.5 vs 204.7 us, profiles/r3_fp8_wgrad_sgd_ab.txt): variant wgrad_sgd_fp8 opts in
+        self.wgrad_apply = in_launch and self.fc1_epilogue and (not self.fp8 or bool(V["wgrad_sgd_fp8"]))
         # data parallel: the same launch reduces the conv slabs into the flat gradient (the reduce-only
         # SGD launch before the all-reduce goes away).  Needs the launch's blocks co-resident, so not
         # when several ranks share one GPU (rehearsals / tests: another rank's kernels hold CUs).
         local = int(os.environ.get("LOCAL_WORLD_SIZE", world_size))
         ndev = torch.cuda.device_count() if dev.type == "cuda" else 0
         reduce_ok = in_launch and self.dp and local <= max(1, ndev)
-        # reduce-only also serves compute_gradients() on one GPU.  fp8 included: the round-3 report of a
-        # wrong conv1 gradient under the in-launch reduction (cosine 0.24 at B=64) came from an
-        # intermediate build; on this one tools/dbg_race.py 64 fp8 finds 0/5 mismatches against the
-        # two-launch path and test_fp8_gpu.py covers reduce mode at B=64/100/1024 bit for bit
+        # reduce-only also serves compute_gradients() on one GPU (fp8 included: bit for bit the
+        # two-launch path, tests/test_fp8_gpu.py)
         self._grad_in_launch = in_launch and (self.wgrad_apply or reduce_ok)
         # the data-parallel step takes the in-launch reduction exactly when compute_gradients() does
-        # (one predicate: the DP step and _conv_backward's assertion can never disagree)
+        # (one predicate: the DP step and _conv_backward can never disagree)
         self.wgrad_reduce = self.dp and self._grad_in_launch
         self.wbar = torch.zeros(WBAR_WORDS, dtype=torch.int32, device=dev)   # barrier words + error word
         # pinned host copy of the barrier error word, refreshed by queue_error_copy() behind each
@@ -351,21 +326,21 @@ class FusedCifarEngine:
         # once its dp2 row tile is published: one launch boundary less, but the hand-off (publish ->
         # poll -> sc1 dp2 loads) costs ~2 us of it back.  With the fc dW tiles kept in the chain (below)
         # it measured 1.8-2.5 us/step faster at B = 144 / 160 / 192 / 224 / 256 (profiles/
-        # r4_v8_fc_dgrad_b144_256_ab.txt); even at B = 128, where the split dgrad (2 workgroups per
-        # image) is the default.  DMLC_FC_DGRAD=1 / 0 forces it on / off.
-        fdg = os.environ.get("DMLC_FC_DGRAD", "auto")
-        self.fc_dgrad = (self.fc_fused and not self.fused_w1 and not self.fp8_dgrad
-                         and (fdg == "1" or (fdg != "0" and self.dgrad_split != 2)))
+        # r4_v8_fc_dgrad_b144_256_ab.txt); at B <= 128 the split dgrad (2 workgroups per image) stays
+        # its own launch.  Variant fc_dgrad forces it on / off.
+        fdg = V["fc_dgrad"]
+        self.fc_dgrad = (self.fc_fused and not self.fp8_dgrad
+                         and (bool(fdg) if fdg is not None else self.dgrad_split != 2))
         self._dgrad_done = False
         # single GPU, fused fc chain + apply mode: the fc weight-gradient tiles and every fc SGD can run
         # in the wgrad launch's conv1 blocks (between their barrier arrival and the conv1 reduction),
         # so the fc chain launch ends with its dp2 tiles.  Same-box A/B at B=256 (profiles/
         # r4_v7_fc_dgrad_dw_ab.txt, us/step): chain dgrad off: dW in chain 81.8, in wgrad 80.4; chain
         # dgrad on: dW in chain 79.8, in wgrad 80.2 -- so by default the dW tiles move to the wgrad
-        # launch only when the dgrad is not in the chain.  DMLC_FC_DW_WGRAD=1 / 0 forces it.
-        fdw = os.environ.get("DMLC_FC_DW_WGRAD", "auto")
+        # launch only when the dgrad is not in the chain.  Variant fc_dw_in_wgrad forces it.
+        fdw = V["fc_dw_in_wgrad"]
         self.fc_dw_in_wgrad = (self.fc_fused and self.wgrad_apply
-                               and (fdw == "1" or (fdw != "0" and not self.fc_dgrad)))
+                               and (bool(fdw) if fdw is not None else not self.fc_dgrad))
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
                                                                         s_par=FC1_NUMEL)
@@ -384,7 +359,6 @@ class FusedCifarEngine:
         if self.dp:
             self.comm_info.update(schedule=dp_schedule, backend=self._backend(),
                                   captured_comm=bool(self.capture_comm or self.xgmi is not None))
-        self.side_stream = torch.cuda.Stream(device=dev)
         self.host_step = 0
         self._sync_bidx()
         self.refresh_shadows()
@@ -392,15 +366,12 @@ class FusedCifarEngine:
     # ------------------------------------------------------------------------------------------
     @staticmethod
     def _pick_fc1_split(B: int) -> int:
-        # the largest split in (9, 6, 4, 3, 2) whose (B/64) * 6 tiles * split workgroups stay <= 450;
-        # 9 makes each K slice 256 = two 128-deep chunks.  Whole-step sweeps (tools/sweep_fc.py,
-        # profiles/r2_v26_fc1_split_sweep.jsonl): B=256 9 -> 82.2 vs 8 -> 83.0 us, B=512 9 best,
-        # B=1024 4 -> 208.7 vs 2 -> 211.5 / 9 -> 211.7 us
+        # the largest power-of-two split in (8, 4, 2) whose (B/64) * 6 tiles * split workgroups stay
+        # <= 450: with the XCD-aware GEMM order (cnn_gemm.hip) every XCD gets its own K slice of p2
+        # and W1 (split 8: one slice per XCD).  Whole-step sweeps: tools/sweep_fc.py,
+        # profiles/r2_v26_fc1_split_sweep.jsonl.
         tiles = max(1, math.ceil(B / 64)) * 6
-        # XCD-aware GEMM order (cnn_gemm.hip, default): a power-of-two split gives every XCD its own
-        # K slice of p2 and W1 (split 8: one slice per XCD)
-        cands = (8, 4, 2) if os.environ.get("DMLC_GEMM_XCD", "1") != "0" else (9, 6, 4, 3, 2)
-        for s in cands:
+        for s in (8, 4, 2):
             if tiles * s <= 450:
                 return s
         return 1
@@ -486,8 +457,10 @@ class FusedCifarEngine:
         """fc1 forward + head + fc backward in one persistent launch (cnn_fc.hip), for the batch of
         the preceding _forward(train=True).  fused_sgd: the fc1 weights are updated in the dW1
         epilogue (single GPU), else the fc1 weight gradient goes to the flat gradient."""
-        assert self._fc_src is not None, "_fc_chain follows a training _forward"
-        assert not self._dgrad_done, "the previous fc chain's conv backward never ran"
+        if self._fc_src is None:
+            raise RuntimeError("_fc_chain must follow a training _forward")
+        if self._dgrad_done:
+            raise RuntimeError("the previous fc chain's conv backward never ran")
         idx, counter, period = self._fc_src
         self._fc_src = None
         p, gv = self.pv, self.gv
@@ -510,13 +483,6 @@ class FusedCifarEngine:
         idx, counter, period = src or (self.bidx, None, 1)
         assert not apply or (self.wgrad_apply and src is None), "apply mode: the training step only"
         assert not reduce or self._grad_in_launch
-        if self.fused_w1:
-            o.conv2_dgrad_w1(self.dp2, self.am2, self.w2d, self.dp1 if self.keep_dp1 else None, self.dy2, self.am1,
-                             self.xraw, self.cy, self.cx, self.part1, self.partb1)
-            o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
-                    self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw,
-                    False)
-            return
         if self._dgrad_done:
             self._dgrad_done = False                 # the fc chain launch did it (fc_dgrad)
         elif self.fp8_dgrad:
@@ -534,19 +500,8 @@ class FusedCifarEngine:
                         *(self._sgd_args(mode=0, fc1_fused=True) if apply else self._sgd_args(mode=1)),
                         fc_acts=fc_acts)
             return
-        if self.merged_wgrad:
-            o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
-                    self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw)
-            return
-        # the two weight-gradient kernels are independent: fork them onto two streams (two parallel
-        # branches of the captured graph) so they share the chip
-        main = torch.cuda.current_stream(self.device)
-        self.side_stream.wait_stream(main)
-        with torch.cuda.stream(self.side_stream):
-            o.conv2_wgrad(self.p1, self.dy2, self.part2, self.partb2)
-        o.conv1_wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
-                      self.part1, self.partb1, self.xraw)
-        main.wait_stream(self.side_stream)
+        o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
+                self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw)
 
     def _sgd_args(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True,
                   fc1_fused: bool = False) -> tuple:
@@ -556,7 +511,7 @@ class FusedCifarEngine:
                 self.loss_part, self.correct_part, self.stats,
                 *((self.w2f8, self.amax_w, self.scale_w) if self.fp8 else (None, None, None)),
                 roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup, fc1_fused,
-                None if mode == 3 or self.sgd_ticket else self.step_sgd)
+                None if mode == 3 else self.step_sgd)
 
     def _sgd(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True, fc1_fused: bool = False):
         self.ops.sgd(*self._sgd_args(mode, scale, roles, finalize, fc1_fused))
@@ -582,9 +537,14 @@ class FusedCifarEngine:
             return
         e = int(self._err_host[0]) if cached else int(self.wbar[10 * 32].item())
         if e != 0:
+            # error word: value 1 = a wgrad sub-grid barrier, value 2 = an fc chain hand-off timed out
             mode = "apply" if self.wgrad_apply else "reduce"
-            where = "fc chain" if e & 2 and not e & 1 else f"wgrad {mode} mode"
-            raise RuntimeError(f"{where}: a sub-grid barrier timed out (blocks not co-resident, error word {e})")
+            parts = []
+            if e & 1:
+                parts.append(f"k_wgrad ({mode} mode): a sub-grid barrier timed out; rerun with DMLC_WGRAD_SGD=0")
+            if e & 2:
+                parts.append("k_fc_chain: a hand-off wait timed out; rerun with DMLC_FC_FUSED=0")
+            raise RuntimeError("; ".join(parts) + f" (blocks not co-resident, error word {e})")
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
@@ -650,9 +610,17 @@ class FusedCifarEngine:
     def _seg_apply_conv(self):
         self._sgd(mode=2, scale=1.0, roles=1, finalize=True)
 
-    def compute_gradients(self, idx: Optional[torch.Tensor] = None):
+    def compute_gradients(self, idx: Optional[torch.Tensor] = None, check: bool = True):
         """Forward + backward only (no update); the full gradient lands in ``self.grad``.
-        ``idx``: explicit dataset rows (int32 [Bv]) instead of this step's generated batch."""
+        ``idx``: explicit dataset rows (int32 [Bv]) instead of this step's generated batch.
+        ``check``: synchronise and raise if a persistent launch's hand-off timed out (the gradient
+        would be partial); pass False to keep the call asynchronous and call check_barriers() later."""
+        g = self._compute_gradients(idx)
+        if check:
+            self.check_barriers()
+        return g
+
+    def _compute_gradients(self, idx: Optional[torch.Tensor] = None):
         if idx is None:
             self._seg_compute_a()
             if self._grad_in_launch:
@@ -670,11 +638,21 @@ class FusedCifarEngine:
         self._sgd(mode=1)
         return self.grad
 
+    def _reset_step_state(self):
+        """Forget a half-issued step (an exception between the fc chain and the conv backward, an
+        interrupted capture): the next step starts clean instead of failing the pairing checks."""
+        self._fc_src = None
+        self._dgrad_done = False
+
     def _eager_step(self):
+        try:
+            self._eager_step_body()
+        except BaseException:
+            self._reset_step_state()
+            raise
+
+    def _eager_step_body(self):
         if not self.dp:
-            if self.fc_branch:
-                self._branched_step()
-                return
             if self.fc1_epilogue:
                 self._forward(self.bidx, None, 1, train=True)
                 self._fc_backward(fused_sgd=True)
@@ -691,21 +669,6 @@ class FusedCifarEngine:
             self._serial_dp_step([self._seg_compute_ab, self._seg_apply])
             return
         self._dp_step([self._seg_compute_a, self._seg_compute_b_launch, self._seg_apply_fc, self._seg_apply_conv])
-
-    def _branched_step(self):
-        """Single-GPU step on two graph branches (fc_branch): the fc weight gradients and the fc SGD
-        run beside the conv backward; the conv SGD (which bumps global_step) after the join."""
-        o = self.ops
-        self._forward(self.bidx, None, 1, train=True)
-        self._gemm(self._fc_dx)
-        main = torch.cuda.current_stream(self.device)
-        self.side_stream.wait_stream(main)
-        with torch.cuda.stream(self.side_stream):
-            self._gemm(self._fc_dw)
-            self._sgd(mode=0, roles=2, finalize=False)
-        self._conv_backward()
-        main.wait_stream(self.side_stream)
-        self._sgd(mode=0, roles=1, finalize=True)
 
     def _seg_compute_ab(self):
         self._seg_compute_a()
@@ -759,6 +722,7 @@ class FusedCifarEngine:
         as a sum of chains -- no single-step tails, no host gap between the chained steps.
         RCCL without ``capture_comm``: compute graphs around eager collectives (no chains)."""
         torch.cuda.synchronize(self.device)
+        self._reset_step_state()
         self.graphs, self.chains = [], {}
         pool = torch.cuda.graph_pool_handle()
         if self.single_graph:

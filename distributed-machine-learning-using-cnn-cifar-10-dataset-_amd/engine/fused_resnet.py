@@ -12,7 +12,7 @@ all HIP kernels of csrc/kernels/resnet.hip, captured as one HIP graph:
   bwd  l=18..1   dgrad_l: g_z_l (BN backward, prologue) -> g_a_{l-1} (+ shortcut grad) -> ReLU mask
                  -> g_y_{l-1} and the BN_{l-1} reductions (epilogue)
        l=18..0   wgrad_l, split-K fp32 slabs: in the same launch as dgrad_l (block roles), or on a
-                 side stream (a second graph branch, DMLC_RN_WGRAD_BRANCH=1)
+                 side stream (a second graph branch, wgrad_branch=True)
   sgd            slab reduction + SGD (conv, BN gamma/beta, fc) + BN running statistics (momentum 0.1)
                  + bf16 weight shadows + global_step++ + stats ring
 
@@ -22,7 +22,6 @@ in two halves around ONE all-reduce of the 1.1 MB flat gradient (mode 1 -> RCCL 
 from __future__ import annotations
 
 import math
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -59,7 +58,7 @@ def layer_table():
     return layers
 
 
-NSLOT = 8            # DMLC_RN_NSLOT
+NSLOT = 8            # BN statistics slots per layer (resnet.hip)
 LAYERS = layer_table()
 NL = len(LAYERS)
 assert NL == 19
@@ -90,7 +89,8 @@ class FusedResNetEngine:
                  rank: int = 0, process_group=None, seed: int = 0, groups: Optional[List[int]] = None,
                  stats_len: int = 4096, comm_dtype: str = "fp32", wgrad_branch: Optional[bool] = None,
                  allreduce: str = "auto", capture_comm: Optional[bool] = None, dp_force: bool = False,
-                 deterministic: Optional[bool] = None, warmup_steps: int = 0):
+                 deterministic: Optional[bool] = None, warmup_steps: int = 0,
+                 merged_bwd: Optional[bool] = None, bwd_img_level: int = 1, sgd_split: bool = False):
         ops = _ops()
         self.ops = ops
         self.device = torch.device(device or "cuda")
@@ -110,7 +110,7 @@ class FusedResNetEngine:
         if capture_comm is None:                 # RCCL collectives inside the step graph (nccl only)
             import torch.distributed as dist
             nccl = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
-            capture_comm = self.dp and nccl and os.environ.get("DMLC_CAPTURE_COMM", "1") != "0"
+            capture_comm = self.dp and nccl
         self.capture_comm = bool(capture_comm)
 
         assert data.dtype == torch.uint8 and tuple(data.shape[1:]) == (32, 32, 3)
@@ -167,19 +167,17 @@ class FusedResNetEngine:
         self.stat, self.red = self.acc[0], self.acc[1]
         # deterministic BN statistics (default): per-block fp32 partials + per-slot group tickets, the
         # group's last block sums its partials in block order into the slot (resnet.hip det_flush) --
-        # bitwise reproducible, no per-step zeroing; DMLC_RN_DETERMINISTIC=0: fp64 atomics
-        if deterministic is None:
-            deterministic = os.environ.get("DMLC_RN_DETERMINISTIC", "1") != "0"
-        self.deterministic = bool(deterministic)
+        # bitwise reproducible, no per-step zeroing; deterministic=False: fp64 atomics
+        self.deterministic = True if deterministic is None else bool(deterministic)
         self.det = (torch.zeros(2, NL, B * 128 + 8 * 32, dtype=torch.float32, device=dev)
                     if self.deterministic else None)
         det = (lambda k, l: self.det[k][l]) if self.deterministic else (lambda k, l: None)
         self._det_stat = [det(0, l) for l in range(NL)]
         self._det_red = [det(1, l) for l in range(NL)]
-        # per-image backward (k_rn_bwd_img, merged backward only): DMLC_RN_BWD_IMG = 0 off, 1 the 16->16
+        # per-image backward (k_rn_bwd_img, merged backward only): bwd_img_level 0 off, 1 the 16->16
         # layers (their wgrad keeps one slab per image anyway), 2 also the 32->32 stride-1 layers (one
         # slab per image instead of B/2 groups: more slab bytes for the SGD, fewer re-reads)
-        self.bwd_img_level = int(os.environ.get("DMLC_RN_BWD_IMG", "1") or 0)
+        self.bwd_img_level = int(bwd_img_level)
         self.groups = groups or [B if (self.bwd_img_level >= 2 and B <= 256 and (ci, co, h, s) == (32, 32, 16, 1))
                                  else self._pick_groups(B, ci, co) for _, ci, co, h, s in LAYERS]
         self.part = [z(g, _kp(ci), co, dt=torch.float32) for g, (_, ci, co, _, _) in zip(self.groups, LAYERS)]
@@ -188,12 +186,10 @@ class FusedResNetEngine:
         self.correct_img = z(B, dt=torch.int32)
         self.logits_buf = z(B, 10, dt=torch.float32)
         self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
-        # DMLC_SGD_TICKET=0: the head copies the step counter here and the SGD reads the copy, so its
-        # BN layer-0 block bumps step_t without an arrival ticket.  Unlike the CNN step (-0.9 us) this
-        # measured no better here (r3: 0.679 / 0.682 ms vs 0.675 / 0.678 with the ticket), so the
-        # ticket stays the default
+        # The SGD finds the last arriver with a ticket (the CNN engine's ticketless form -- the head
+        # copies the step counter for the SGD -- measured no better here in r3: 0.679 / 0.682 ms vs
+        # 0.675 / 0.678 with the ticket); step_sgd is the kernel argument that form would use
         self.step_sgd = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.sgd_ticket = os.environ.get("DMLC_SGD_TICKET", "1") == "1"
         self.ticket = torch.zeros(TICKET_WORDS, dtype=torch.int32, device=dev)   # two-level arrival counters
         self.stats = torch.zeros(stats_len, 4, dtype=torch.float32, device=dev)
 
@@ -208,19 +204,16 @@ class FusedResNetEngine:
         #   two launches, 1 stream 363 k   590 k
         #   wgrads on a branch     336 k   620 k   19 fork/join edges in the graph
         # The merged kernel runs at the occupancy of the larger (wgrad) body, which costs more than the
-        # saved launches once each layer has >= ~4 dgrad workgroups per CU; DMLC_RN_WGRAD_BRANCH /
-        # DMLC_RN_MERGED_BWD override the choice.
-        if wgrad_branch is None:
-            wgrad_branch = os.environ.get("DMLC_RN_WGRAD_BRANCH", "1" if B > 256 else "0") == "1"
-        self.wgrad_branch = wgrad_branch
-        self.merged_bwd = os.environ.get("DMLC_RN_MERGED_BWD", "1" if B <= 256 else "0") == "1"
-        # DMLC_RN_SGD_SPLIT=1 (single GPU, merged backward): the SGD of stage 3 (layers 13-18) and of
+        # saved launches once each layer has >= ~4 dgrad workgroups per CU; wgrad_branch / merged_bwd
+        # override the choice.
+        self.wgrad_branch = (B > 256) if wgrad_branch is None else bool(wgrad_branch)
+        self.merged_bwd = (B <= 256) if merged_bwd is None else bool(merged_bwd)
+        # sgd_split=True (single GPU, merged backward): the SGD of stage 3 (layers 13-18) and of
         # stage 2 (7-12) runs on a graph branch as soon as their weight gradients are complete, beside
         # the stage-2 / stage-1 backward; the main-stream SGD does the rest and publishes the step.
         # Measured at B=256: 341 k vs 371 k img/s with one SGD launch -- the co-resident SGD blocks
         # slow the one-image-per-workgroup backward more than the hidden slab reads save: off.
-        self.sgd_split = (os.environ.get("DMLC_RN_SGD_SPLIT", "0") == "1" and not self.dp and self.merged_bwd
-                          and not self.wgrad_branch)
+        self.sgd_split = bool(sgd_split) and not self.dp and self.merged_bwd and not self.wgrad_branch
         self._sgd_points = {13: (13, NL), 7: (7, 13)}    # after bwd launch of layer l: SGD of [lo, hi)
         self.host_step = 0
         self._stem_src = None          # explicit (idx, counter, period) of the stem wgrad, else generated
@@ -230,12 +223,11 @@ class FusedResNetEngine:
     @staticmethod
     def _pick_groups(B: int, cin: int, cout: int) -> int:
         """Split-K image groups of one wgrad (grid = groups x m-chunks): enough blocks to fill the chip
-        (``DMLC_RN_WG_BLOCKS``, default 256) while the fp32 slabs the SGD kernel reads back stay under
-        ``DMLC_RN_SLAB_MB`` (default 16 MB: 64 groups for the 64-channel layers, 677 -> 667 us/step at
-        B=256, profiles/r1_v17_rn_slab_cap_ab.txt) per layer.  A power of two in [8, B]."""
-        import os
-        blocks = int(os.environ.get("DMLC_RN_WG_BLOCKS", "256"))
-        cap = float(os.environ.get("DMLC_RN_SLAB_MB", "16")) * 2 ** 20
+        (256) while the fp32 slabs the SGD kernel reads back stay under 16 MB per layer (64 groups for
+        the 64-channel layers, 677 -> 667 us/step at B=256, profiles/r1_v17_rn_slab_cap_ab.txt).  A
+        power of two in [8, B]."""
+        blocks = 256
+        cap = 16.0 * 2 ** 20
         mt = _kp(cin) // 16
         mc = 1 if mt <= 12 else (2 if mt <= 24 else 3)      # Wg<>::MC in resnet.hip
         lim = min(blocks / mc, cap / (_kp(cin) * cout * 4))
@@ -282,7 +274,7 @@ class FusedResNetEngine:
     def _per_image(self, l) -> bool:
         """Layer l's dgrad and wgrad from one workgroup per image (k_rn_bwd_img): the 16->16 stride-1
         layers whose weight gradient already keeps one split-K slab per image (G == B, B <= 256).
-        DMLC_RN_BWD_IMG=0: the merged launch with separate wgrad blocks."""
+        bwd_img_level=0: the merged launch with separate wgrad blocks."""
         _, ci, co, h, s = LAYERS[l]
         lvl = {(16, 16, 32, 1): 1, (32, 32, 16, 1): 2}.get((ci, co, h, s))
         return bool(lvl and self.bwd_img_level >= lvl and self.part[l].shape[0] == self.B)
@@ -347,7 +339,7 @@ class FusedResNetEngine:
                         self.red, self.fc_part, self.loss_img, self.correct_img, self.step_t, self.ticket, self.stats,
                         mode, self.lr0, self.decay, self.decay_steps, self.staircase, R.BN_MOMENTUM, self.warmup,
                         layers[0], layers[1], tail, self.Bv,
-                        None if mode == 3 or self.sgd_ticket else self.step_sgd)
+                        None)
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist

@@ -96,11 +96,9 @@ class _FusedAdapter:
     def check_comm(self):
         # a timed-out wgrad sub-grid barrier is not a peer failure (a restart would repeat it): a plain
         # RuntimeError, raised before anything (e.g. a checkpoint) can use the step's weights
+        # (the engine's message names the kernel whose wait timed out and the switch that turns it off)
         if hasattr(self.eng, "check_barriers"):
-            try:
-                self.eng.check_barriers(cached=True)
-            except RuntimeError as e:
-                raise RuntimeError(f"{e}; rerun with DMLC_WGRAD_SGD=0") from e
+            self.eng.check_barriers(cached=True)
         try:
             if getattr(self.eng, "xgmi", None) is not None:
                 self.eng.xgmi.check()
@@ -114,12 +112,9 @@ class _FusedAdapter:
     def stats(self) -> Dict[str, float]:
         st = self.eng.read_stats(self.eng.host_step)     # (a device sync: the error word is current too)
         if hasattr(self.eng, "check_barriers"):
-            # a sub-grid barrier of the single-GPU wgrad+SGD launch that timed out (its blocks were not
-            # co-resident) leaves wrong weights: stop loudly, DMLC_WGRAD_SGD=0 selects the SGD launch
-            try:
-                self.eng.check_barriers()
-            except RuntimeError as e:
-                raise RuntimeError(f"{e}; rerun with DMLC_WGRAD_SGD=0") from e
+            # a persistent launch's wait that timed out (its blocks were not co-resident) leaves wrong
+            # weights: stop loudly (the message names the kernel and its off switch)
+            self.eng.check_barriers()
         return st
 
     def tf_tensors(self) -> Dict[str, torch.Tensor]:

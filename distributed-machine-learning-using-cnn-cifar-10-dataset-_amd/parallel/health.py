@@ -93,10 +93,13 @@ class Heartbeat:
             except Exception as e:                      # store host gone / unreachable
                 if self._stop.is_set() or not self.active:
                     return
-                if 0 in done or self.rank == 0:
+                if 0 in done:
                     # the store lives in rank 0's process (reference-CLI worlds) or beside it: rank 0
                     # marked itself finished, so its store going away is its clean exit, not a failure
-                    # (this rank is about to finish too: its own collectives completed with rank 0's)
+                    # (this rank is about to finish too: its own collectives completed with rank 0's).
+                    # Rank 0 itself gets no such exemption: a store hosted in its own process cannot
+                    # vanish before stop() (which sets _stop first), so an unreachable store seen by
+                    # rank 0 is one hosted elsewhere (a torchrun agent, the ps role) -- a real failure.
                     return
                 self._fail(f"rendezvous store unreachable ({type(e).__name__}: {e})")
                 return

@@ -18,7 +18,6 @@ decision goes through MIN/MAX all-reduces, so it is identical on all ranks.
 """
 from __future__ import annotations
 
-import os
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -127,7 +126,7 @@ def select(numel: int, rank: int, world: int, device: torch.device, buckets: Lis
     and over RCCL additionally only if measured faster than RCCL on ``buckets`` ((offset, numel)),
     RCCL moving the same wire dtype."""
     info: Dict = {"allreduce": "rccl"}
-    if mode == "rccl" or world == 1 or device.type != "cuda" or os.environ.get("DMLC_NO_XGMI"):
+    if mode == "rccl" or world == 1 or device.type != "cuda":
         return None, info
     nccl = dist.get_backend(group) == "nccl"
     bdev = device if nccl else torch.device("cpu")

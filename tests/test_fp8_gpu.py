@@ -142,17 +142,15 @@ def test_lr_warmup_and_linear_scaling_on_device():
 
 
 @pytest.mark.parametrize("B", [64, 100, 1024])
-def test_fp8_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
+def test_fp8_sgd_in_wgrad_launch_is_bit_identical(B):
     """fp8 (BASELINE config 5) on one GPU: the SGD inside the wgrad launch also writes the e4m3
     shadows (forward w2f8, the dgrad's flipped copy) with the delayed per-tensor scale and the new
     weights' amax slots.  After eager + graph-replayed steps the parameters, both fp8 shadows, the
     scales and the stats equal the SGD-launch path bit for bit."""
     data, labels = _synthetic(8 * B, seed=51)
     kw = dict(seed=52, lr=1e-4, relu_logits=False, dtype="fp8")
-    monkeypatch.setenv("DMLC_WGRAD_SGD_FP8", "1")             # opt-in for fp8 (measured slower)
-    fused = FusedCifarEngine(B, data, labels, **kw)
-    monkeypatch.setenv("DMLC_WGRAD_SGD", "0")
-    ref = FusedCifarEngine(B, data, labels, **kw)
+    fused = FusedCifarEngine(B, data, labels, **kw, variant={"wgrad_sgd_fp8": True})   # opt-in (measured slower)
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"wgrad_sgd": False})
     assert fused.wgrad_apply and not ref.wgrad_apply and fused.fp8
     for eng in (ref, fused):
         eng.step()
@@ -171,17 +169,15 @@ def test_fp8_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [64, 100, 1024])
-def test_fp8_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B, monkeypatch):
+def test_fp8_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B):
     """fp8 compute_gradients() through the in-launch conv-slab reduction (reduce mode, the data-parallel
     path; helpers included at B=64) against the reduce-only SGD launch, bit for bit over the whole flat
     gradient, for the generated batch and an explicit index list -- the case round 3 excluded after a
     wrong conv1 gradient (cosine 0.24 at B=64) on an intermediate build."""
     data, labels = _synthetic(8 * B, seed=47)
     kw = dict(seed=48, lr=1e-4, relu_logits=False, dtype="fp8")
-    monkeypatch.setenv("DMLC_WGRAD_SGD_FP8", "1")             # single GPU: in-launch mode needs the opt-in
-    fused = FusedCifarEngine(B, data, labels, **kw)
-    monkeypatch.setenv("DMLC_WGRAD_SGD", "0")
-    ref = FusedCifarEngine(B, data, labels, **kw)
+    fused = FusedCifarEngine(B, data, labels, **kw, variant={"wgrad_sgd_fp8": True})   # single GPU: the opt-in
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"wgrad_sgd": False})
     assert fused._grad_in_launch and not ref._grad_in_launch and fused.fp8
     idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(3))[:B].to(torch.int32)
     for explicit in (None, idx, None):

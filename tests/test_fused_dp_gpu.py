@@ -56,15 +56,8 @@ def _dp_reference(world, B, steps, batches, comm_dtype, allreduce, fc_fused=Fals
     x, y = _data()
     # the fc kernels the ranks ran (ranks sharing one GPU run the three-launch fc path, not the
     # persistent fc chain, whose 256 workgroups must own the chip)
-    old = os.environ.get("DMLC_FC_FUSED")
-    os.environ["DMLC_FC_FUSED"] = "1" if fc_fused else "0"
-    try:
-        ref = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, staircase=False)
-    finally:
-        if old is None:
-            del os.environ["DMLC_FC_FUSED"]
-        else:
-            os.environ["DMLC_FC_FUSED"] = old
+    ref = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, staircase=False,
+                           variant={"fc_fused": bool(fc_fused)})
     assert ref.fc_fused == fc_fused
     init = ref.flat_params().clone()
     bf = (lambda t: t.to(torch.bfloat16).float()) if comm_dtype == "bf16" else (lambda t: t)

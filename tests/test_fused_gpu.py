@@ -61,24 +61,6 @@ def test_gradients_match_reference(B):
         assert cos > 0.995, (s.name, cos, _rel(a, b))
 
 
-@pytest.mark.parametrize("B,g2", [(64, 10), (256, 50), (48, 5)])
-def test_merged_wgrad_launch_matches_two_kernels(B, g2, monkeypatch):
-    """ops.wgrad (both weight gradients in one launch) vs the two separate kernels over the same image
-    groups: the blocks run the same bodies, so every slab -- and the whole gradient -- is
-    bit-identical, including group counts that leave the merged grid more than one wave of blocks."""
-    data, labels = _synthetic(4 * B, seed=7)
-    eng = FusedCifarEngine(B, data, labels, seed=6, g2=g2)
-    assert eng.merged_wgrad and not eng.fused_w1 and eng.groups2 == g2 and eng.g2 == g2
-    g_merged = eng.compute_gradients().cpu().clone()
-    monkeypatch.setenv("DMLC_SPLIT_WGRAD", "1")
-    ref = FusedCifarEngine(B, data, labels, seed=6, g1=eng.g1, g2=g2)
-    assert not ref.merged_wgrad and ref.g2 == g2
-    g_split = ref.compute_gradients().cpu().clone()
-    assert torch.equal(eng.part1, ref.part1) and torch.equal(eng.partb1, ref.partb1)
-    assert torch.equal(eng.part2, ref.part2) and torch.equal(eng.partb2, ref.partb2)
-    assert torch.equal(g_merged, g_split)
-
-
 def test_multi_step_graph_run_equals_eager_steps():
     """run(n) replays chains of 8/4/2/1 captured steps straight across epoch boundaries (the batch
     order is generated in-kernel from the step counter); the result is bit-identical to n eager
@@ -165,7 +147,7 @@ def test_lr_staircase_schedule_on_device():
     assert lrs == pytest.approx([0.1, 0.1, 0.05, 0.05, 0.025])
 
 
-def test_fused_conv12_forward_equals_two_launches(monkeypatch):
+def test_fused_conv12_forward_equals_two_launches():
     """ops.conv12_fwd (conv1 -> pool1 -> conv2 -> pool2 of an image in one workgroup, pool1 handed to
     conv2 through LDS) produces bit-identical p1 / argmax / p2 / logits to the two separate launches."""
     B = 64
@@ -174,8 +156,7 @@ def test_fused_conv12_forward_equals_two_launches(monkeypatch):
     assert fused.fused_fwd
     idx = torch.randperm(data.shape[0])[:B].to(torch.int32)
     lf = fused.forward_logits(idx).clone()
-    monkeypatch.setenv("DMLC_SPLIT_FWD", "1")
-    split = FusedCifarEngine(B, data, labels, seed=20, conv_split=1)
+    split = FusedCifarEngine(B, data, labels, seed=20, conv_split=1, variant={"split_fwd": True})
     assert not split.fused_fwd
     ls = split.forward_logits(idx).clone()
     for n in ("p1", "am1", "p2", "am2"):
@@ -277,57 +258,8 @@ def test_any_batch_size_masked_tail(B):
     assert abs(st["accuracy"] - want_acc) < 1e-6, (st, want_acc)
 
 
-@pytest.mark.parametrize("B", [64, 256])
-def test_fused_dgrad_conv1_wgrad_matches_separate_launches(B, monkeypatch):
-    """ops.conv2_dgrad_w1 (conv2 dgrad + the conv1 weight gradient of each image in one launch, one
-    slab per image) + the conv2-only weight-gradient launch vs the separate dgrad / merged wgrad
-    launches: dy2 and the conv2 gradient bit-identical, the conv1 slabs of each split group summed
-    equal to that group's slab, the whole gradient equal up to fp32 summation order."""
-    data, labels = _synthetic(4 * B, seed=8)
-    monkeypatch.setenv("DMLC_FUSED_W1", "1")
-    fused = FusedCifarEngine(B, data, labels, seed=9, conv_split=1)   # the per-image dgrad core in both
-    assert fused.fused_w1 and fused.g1 == B
-    g_f = fused.compute_gradients().cpu().clone()
-    monkeypatch.setenv("DMLC_FUSED_W1", "0")
-    ref = FusedCifarEngine(B, data, labels, seed=9, g2=fused.groups2, conv_split=1)
-    assert not ref.fused_w1
-    g_r = ref.compute_gradients().cpu().clone()
-    assert torch.equal(fused.dy2, ref.dy2)
-    assert torch.equal(fused.part2, ref.part2) and torch.equal(fused.partb2, ref.partb2)
-    for grp in range(ref.g1):                        # the split kernel's groups: images grp, grp + g1, ...
-        want = ref.part1[grp]
-        got = fused.part1[grp::ref.g1].sum(0)
-        assert torch.allclose(got, want, rtol=1e-4, atol=1e-5 * float(want.abs().max()) + 1e-12), grp
-    for s in M.PARAM_SPECS:
-        a, b = g_f[s.offset:s.offset + s.numel], g_r[s.offset:s.offset + s.numel]
-        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5 * float(b.abs().max()) + 1e-12), s.name
-
-
-@pytest.mark.parametrize("B", [128, 256])
-def test_fc_branch_step_is_bit_identical(B, monkeypatch):
-    """DMLC_FC_BRANCH=1: the fc weight gradients + fc SGD on a second graph branch beside the conv
-    backward, the conv SGD after the join.  Same kernels on the same data: after graph-replayed steps
-    the parameters, step counter and stats equal the one-branch step bit for bit."""
-    data, labels = _synthetic(8 * B, seed=41)
-    kw = dict(seed=40, lr=1e-4, relu_logits=False)     # (lr 1e-2 on raw pixels diverges to NaN in ~4 steps)
-    monkeypatch.setenv("DMLC_FC_FUSED", "0")           # the branch runs the three-launch fc kernels
-    ref = FusedCifarEngine(B, data, labels, **kw)
-    monkeypatch.setenv("DMLC_FC_BRANCH", "1")
-    br = FusedCifarEngine(B, data, labels, **kw)
-    assert br.fc_branch and not ref.fc_branch
-    for eng in (ref, br):
-        eng.step()
-        eng.capture(steps_per_graph=4)
-        eng.run(7)
-    torch.cuda.synchronize()
-    assert ref.global_step() == br.global_step() == 8
-    assert torch.isfinite(ref.master).all()
-    assert torch.equal(ref.master, br.master)
-    assert ref.read_stats(8) == br.read_stats(8)
-
-
 @pytest.mark.parametrize("B", [100, 256])
-def test_fc1_update_in_gemm_epilogue_is_bit_identical(B, monkeypatch):
+def test_fc1_update_in_gemm_epilogue_is_bit_identical(B):
     """Single GPU: the fc1 weight update runs in the dW1 GEMM's epilogue (c_mode 4) and the SGD kernel
     updates only the fc1 bias; the fc1 shadow is double-buffered by step parity.  After eager and
     graph-replayed steps (odd and even counts, a mid-run set_step, an eval forward) everything equals
@@ -335,8 +267,7 @@ def test_fc1_update_in_gemm_epilogue_is_bit_identical(B, monkeypatch):
     data, labels = _synthetic(8 * B, seed=43)
     kw = dict(seed=44, lr=1e-4, relu_logits=False)
     fused = FusedCifarEngine(B, data, labels, **kw)
-    monkeypatch.setenv("DMLC_FC1_EPILOGUE", "0")
-    ref = FusedCifarEngine(B, data, labels, **kw)
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"fc1_epilogue": False})
     assert fused.fc1_epilogue and not ref.fc1_epilogue
     idx = torch.arange(B, dtype=torch.int32)
     for eng in (ref, fused):
@@ -358,7 +289,7 @@ def test_fc1_update_in_gemm_epilogue_is_bit_identical(B, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [16, 100, 128, 256, 1024])
-def test_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
+def test_sgd_in_wgrad_launch_is_bit_identical(B):
     """Single GPU: the merged weight-gradient launch also runs the SGD (cnn_wgrad.hip apply mode:
     sub-grid barriers per slab family, each block reduces its share of the slabs in the SGD kernel's
     order, the conv1 blocks run the fc roles / stats / global_step / next batch rows) and the step has
@@ -368,8 +299,7 @@ def test_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
     data, labels = _synthetic(8 * B, seed=45)
     kw = dict(seed=46, lr=1e-4, relu_logits=False)
     fused = FusedCifarEngine(B, data, labels, **kw)
-    monkeypatch.setenv("DMLC_WGRAD_SGD", "0")
-    ref = FusedCifarEngine(B, data, labels, **kw)
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"wgrad_sgd": False})
     assert fused.wgrad_apply and not ref.wgrad_apply
     idx = torch.arange(min(B, 64), dtype=torch.int32)
     for eng in (ref, fused):
@@ -394,7 +324,7 @@ def test_sgd_in_wgrad_launch_is_bit_identical(B, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [16, 100, 256])
-def test_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B, monkeypatch):
+def test_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B):
     """Data-parallel / compute_gradients path: the merged weight-gradient launch reduces its own conv
     slabs into the flat gradient (SGD mode 1 inside cnn_wgrad.hip, helpers included) instead of a
     reduce-only SGD launch.  The whole flat gradient equals the two-launch path bit for bit, for the
@@ -402,8 +332,7 @@ def test_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B, monkeypatch):
     data, labels = _synthetic(8 * B, seed=47)
     kw = dict(seed=48, lr=1e-4, relu_logits=False)
     fused = FusedCifarEngine(B, data, labels, **kw)
-    monkeypatch.setenv("DMLC_WGRAD_SGD", "0")
-    ref = FusedCifarEngine(B, data, labels, **kw)
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"wgrad_sgd": False})
     assert fused._grad_in_launch and not ref._grad_in_launch
     idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(3))[:B].to(torch.int32)
     for explicit in (None, idx):
@@ -416,17 +345,15 @@ def test_conv_grad_reduction_in_wgrad_launch_is_bit_identical(B, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [16, 100, 128, 256])
-def test_fc_chain_launch_matches_three_launch_path(B, monkeypatch):
+def test_fc_chain_launch_matches_three_launch_path(B):
     """The persistent fc-chain launch (cnn_fc.hip: fc1 forward + head + fc backward, 256 co-resident
     workgroups, in-launch hand-offs) against the three-launch path (grouped GEMM, head, grouped
     GEMM) on the same weights and batch: loss, accuracy, the conv backward's input dp2 and every
     gradient segment agree to bf16 rounding (the fc1 split-K order differs: 8 slices, not 9)."""
     data, labels = _synthetic(8 * B, seed=61)
     kw = dict(seed=62, lr=1e-4, relu_logits=False)
-    monkeypatch.setenv("DMLC_FC_FUSED", "1")
-    fused = FusedCifarEngine(B, data, labels, **kw)
-    monkeypatch.setenv("DMLC_FC_FUSED", "0")
-    ref = FusedCifarEngine(B, data, labels, **kw)
+    fused = FusedCifarEngine(B, data, labels, **kw, variant={"fc_fused": True})
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"fc_fused": False})
     assert fused.fc_fused and not ref.fc_fused
     idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(5))[:B].to(torch.int32)
     for explicit in (None, idx):
@@ -453,17 +380,15 @@ def test_fc_chain_launch_matches_three_launch_path(B, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [160, 256])
-def test_dgrad_in_fc_chain_is_bit_identical(B, monkeypatch):
+def test_dgrad_in_fc_chain_is_bit_identical(B):
     """The conv2 input gradient inside the fc chain launch (each workgroup's image once its dp2 row
     tile's 18 column tasks have published) against the separate dgrad launch: dP1, dY2, every
     gradient segment and the weights after eager + graph-replayed steps are bit-identical (the same
     device function on the same operands; only the hand-off differs)."""
     data, labels = _synthetic(8 * B, seed=63)
     kw = dict(seed=64, lr=1e-3, relu_logits=False)
-    monkeypatch.setenv("DMLC_FC_DGRAD", "1")
-    fused = FusedCifarEngine(B, data, labels, **kw)
-    monkeypatch.setenv("DMLC_FC_DGRAD", "0")
-    ref = FusedCifarEngine(B, data, labels, **kw)
+    fused = FusedCifarEngine(B, data, labels, **kw, variant={"fc_dgrad": True})
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"fc_dgrad": False})
     assert fused.fc_dgrad and not ref.fc_dgrad
     idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(6))[:B].to(torch.int32)
     for explicit in (None, idx):
@@ -485,16 +410,15 @@ def test_dgrad_in_fc_chain_is_bit_identical(B, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [128, 256])
-def test_fc_dw_tiles_in_wgrad_launch_are_bit_identical(B, monkeypatch):
+def test_fc_dw_tiles_in_wgrad_launch_are_bit_identical(B):
     """The fc weight-gradient tiles + every fc SGD epilogue run in the wgrad launch's conv1 blocks
-    (DMLC_FC_DW_WGRAD=1) or in the fc chain (0): every epilogue applies the SGD kernel's expression,
+    (variant fc_dw_in_wgrad) or in the fc chain: every epilogue applies the SGD kernel's expression,
     so the weights after eager + graph-replayed steps are bit-identical either way."""
     data, labels = _synthetic(8 * B, seed=65)
     kw = dict(seed=66, lr=1e-3, relu_logits=False)
     engs = []
-    for v in ("1", "0"):
-        monkeypatch.setenv("DMLC_FC_DW_WGRAD", v)
-        engs.append(FusedCifarEngine(B, data, labels, **kw))
+    for v in (True, False):
+        engs.append(FusedCifarEngine(B, data, labels, **kw, variant={"fc_dw_in_wgrad": v}))
     assert engs[0].fc_dw_in_wgrad and not engs[1].fc_dw_in_wgrad
     for eng in engs:
         eng.step()
@@ -507,10 +431,9 @@ def test_fc_dw_tiles_in_wgrad_launch_are_bit_identical(B, monkeypatch):
     assert torch.equal(engs[0].master, engs[1].master)
 
 
-def test_fc_chain_graph_replay_is_deterministic(monkeypatch):
+def test_fc_chain_graph_replay_is_deterministic():
     """Two engines, same seed, same steps through the persistent fc chain: bit-identical weights
     (fixed-order split-K sums, no atomics on data)."""
-    monkeypatch.setenv("DMLC_FC_FUSED", "1")
     data, labels = _synthetic(2048, seed=71)
     engs = [FusedCifarEngine(256, data, labels, seed=72, lr=1e-3) for _ in range(2)]
     for eng in engs:

@@ -225,7 +225,7 @@ def test_cli_fused_resnet20_checkpoint_resume(tmp_path):
     assert int(CK.read_bundle(CK.latest_checkpoint(str(tmp_path)))["global_step"]) == 9
 
 
-def test_merged_backward_launch_matches_separate_launches(monkeypatch):
+def test_merged_backward_launch_matches_separate_launches():
     """rn_bwd (dgrad_l + wgrad_l as one launch, block roles) computes the same gradients as the two
     separate launches (up to the order of the fp64 BN-statistics atomics)."""
     B = 32
@@ -233,8 +233,7 @@ def test_merged_backward_launch_matches_separate_launches(monkeypatch):
     merged = FusedResNetEngine(B, data, labels, seed=12)
     assert merged.merged_bwd and not merged.wgrad_branch
     g_m = merged.compute_gradients().cpu().clone()
-    monkeypatch.setenv("DMLC_RN_MERGED_BWD", "0")
-    split = FusedResNetEngine(B, data, labels, seed=12)
+    split = FusedResNetEngine(B, data, labels, seed=12, merged_bwd=False)
     assert not split.merged_bwd
     g_s = split.compute_gradients().cpu().clone()
     assert _rel(g_m, g_s) < 1e-4, _rel(g_m, g_s)
@@ -242,16 +241,14 @@ def test_merged_backward_launch_matches_separate_launches(monkeypatch):
         assert _rel(lm, ls) < 1e-3
 
 
-def test_branch_sgd_split_equals_single_sgd_launch(monkeypatch):
+def test_branch_sgd_split_equals_single_sgd_launch():
     """The layer-range SGD launches on a graph branch (stage 3 after its last backward launch, stage
     2 after its) + the tail SGD give bitwise the same parameters, BN state and step as one SGD
     launch, eagerly and under graph replay."""
     B = 32
     data, labels = _data(8 * B, seed=21)
-    monkeypatch.setenv("DMLC_RN_SGD_SPLIT", "1")
-    split = FusedResNetEngine(B, data, labels, seed=5, lr=0.01)
+    split = FusedResNetEngine(B, data, labels, seed=5, lr=0.01, sgd_split=True)
     assert split.sgd_split
-    monkeypatch.setenv("DMLC_RN_SGD_SPLIT", "0")
     one = FusedResNetEngine(B, data, labels, seed=5, lr=0.01)
     assert not one.sgd_split
     for e in (split, one):
@@ -296,19 +293,17 @@ def test_any_batch_size_masked_tail(B):
 
 
 @pytest.mark.parametrize("B,level", [(32, 1), (256, 1), (64, 2), (256, 2)])
-def test_per_image_backward_is_bit_identical(B, level, monkeypatch):
+def test_per_image_backward_is_bit_identical(B, level):
     """The stride-1 layers' dgrad + wgrad from one workgroup per image (k_rn_bwd_img: the staged g_z and
     layer input serve both, one weight-gradient slab per image; level 1: the 16->16 layers, level 2:
     also the 32->32 ones) train exactly like the merged launch with separate wgrad blocks over the
-    same slabs (DMLC_RN_BWD_IMG=0): the same per-image sums in the same k-step order, so parameters,
+    same slabs (bwd_img_level=0): the same per-image sums in the same k-step order, so parameters,
     BN state and stats agree bit for bit after eager and graph-replayed steps."""
     data, labels = _data(4 * B, seed=31)
-    monkeypatch.setenv("DMLC_RN_BWD_IMG", str(level))
-    img = FusedResNetEngine(B, data, labels, seed=30)
+    img = FusedResNetEngine(B, data, labels, seed=30, bwd_img_level=level)
     assert all(img._per_image(l) for l in range(1, 7))
     assert all(img._per_image(l) for l in (8, 9, 10, 11, 12)) == (level == 2)
-    monkeypatch.setenv("DMLC_RN_BWD_IMG", "0")
-    ref = FusedResNetEngine(B, data, labels, seed=30, groups=list(img.groups))
+    ref = FusedResNetEngine(B, data, labels, seed=30, groups=list(img.groups), bwd_img_level=0)
     assert not any(ref._per_image(l) for l in range(1, 7))
     for eng in (ref, img):
         eng.step()

@@ -68,3 +68,20 @@ def test_store_loss_after_rank0_finished_is_a_clean_exit():
     time.sleep(1.0)
     hb1.stop(done=True)
     assert fails == [], fails
+
+
+def test_rank0_reports_a_store_hosted_elsewhere_going_away():
+    """a store hosted outside rank 0's process (a torchrun agent, the ps role) that
+    disappears mid-run is a real failure for rank 0 too -- its heartbeat must report it, not return
+    quietly and stop watching its peers."""
+    port = _free_port()
+    store = _store(port)
+    fails = []
+    hb0 = H.Heartbeat(0, 2, "127.0.0.1", port, interval_s=0.1, timeout_s=5.0, on_failure=fails.append).start()
+    time.sleep(0.3)
+    del store                                # the external store host dies; rank 0 is still running
+    deadline = time.monotonic() + 5.0
+    while not fails and time.monotonic() < deadline:
+        time.sleep(0.1)
+    hb0.stop(done=False)
+    assert fails and "store unreachable" in fails[0], fails

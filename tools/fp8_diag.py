@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """fp8 path diagnostics: loss / scales over a bench-like run, and the conv1 forward's cost with and
-without the activation-amax epilogue, for the fp8 conv2 dgrad on and off (DMLC_FP8_DGRAD)."""
+without the activation-amax epilogue, for the fp8 conv2 dgrad on and off (engine variant fp8_dgrad)."""
 import json
 import os
 import sys
@@ -30,9 +30,8 @@ def main():
     g = torch.Generator().manual_seed(0)
     data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
     labels = torch.randint(0, 10, (50000,), dtype=torch.int32, generator=g)
-    for dg in ("1", "0"):
-        os.environ["DMLC_FP8_DGRAD"] = dg
-        eng = FusedCifarEngine(B, data, labels, device="cuda", dtype="fp8")
+    for dg in (True, False):
+        eng = FusedCifarEngine(B, data, labels, device="cuda", dtype="fp8", variant={"fp8_dgrad": dg})
         eng.step()
         eng.capture()
         eng.run(60)

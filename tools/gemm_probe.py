@@ -96,7 +96,6 @@ def main():
                                         1.0 / eng.Bv, eng.relu_logits, True, eng.h1, eng.h2, eng.dl, eng.dh1,
                                         eng.dh2, eng.loss_part, eng.correct_part, None, eng.Bv, eng.step_t,
                                         eng.step_sgd), a.iters)
-    res["xcd_map"] = os.environ.get("DMLC_GEMM_XCD", "1")
     print(json.dumps(res))
 
 

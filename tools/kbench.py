@@ -74,28 +74,15 @@ def main():
     if eng.fp8:
         res["conv2_dgrad_fp8"] = timeit(lambda: o.conv2_dgrad_fp8(eng.dp2, eng.am2, eng.w2f8[1], eng.scale_w, eng.dp1,
                                                                   eng.dy2), a.iters)
-    if eng.fused_w1:
-        res["conv2_dgrad_w1"] = timeit(lambda: o.conv2_dgrad_w1(eng.dp2, eng.am2, eng.w2d, None, eng.dy2, eng.am1,
-                                                                eng.xraw, eng.cy, eng.cx, eng.part1, eng.partb1),
-                                       a.iters)
-    if not eng.fused_w1:
-        res["conv1_wgrad"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx, eng.dp1,
-                                                          eng.am1, eng.part1, eng.partb1, eng.xraw), a.iters)
-    if not eng.merged_wgrad:
-        res["conv2_wgrad"] = timeit(lambda: o.conv2_wgrad(eng.p1, eng.dy2, eng.part2, eng.partb2), a.iters)
     res["wgrad_merged"] = timeit(lambda: o.wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx,
                                                  eng.dp1, eng.am1, eng.part1, eng.partb1, eng.p1, eng.dy2,
-                                                 eng.part2, eng.partb2, eng.groups2, eng.xraw,
-                                                 not eng.fused_w1), a.iters)
+                                                 eng.part2, eng.partb2, eng.groups2, eng.xraw), a.iters)
     for pair in filter(None, a.wgrad_sweep.split(",")):
         g1, g2 = (int(v) for v in pair.split(":"))
         z = lambda *sh: torch.zeros(*sh, device=eng.device, dtype=torch.float32)
         p1, pb1, p2, pb2 = z(g1, 80, 64), z(g1, 64), z(g2, 1600, 64), z(g2, 64)
         res[f"wgrad_{g1}_{g2}"] = timeit(lambda: o.wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx, eng.dp1, eng.am1,
-                                                         p1, pb1, eng.p1, eng.dy2, p2, pb2, g2, eng.xraw, True), a.iters)
-        res[f"conv1_wgrad_{g1}"] = timeit(lambda: o.conv1_wgrad(eng.data, eng.bidx, None, 1, eng.cy, eng.cx, eng.dp1,
-                                                                eng.am1, p1, pb1, eng.xraw), a.iters)
-        res[f"conv2_wgrad_{g2}"] = timeit(lambda: o.conv2_wgrad(eng.p1, eng.dy2, p2, pb2), a.iters)
+                                                         p1, pb1, eng.p1, eng.dy2, p2, pb2, g2, eng.xraw), a.iters)
     res["conv_bwd"] = timeit(eng._conv_backward, a.iters)
     res["sgd_reduce_only"] = timeit(lambda: eng._sgd(mode=1), a.iters)
     res["sgd_full"] = timeit(lambda: eng._sgd(mode=0), a.iters)
@@ -103,9 +90,8 @@ def main():
     eng.capture()
     res["step_graph"] = timeit(lambda: eng.graphs[0].replay(), a.iters)
     res["sum_kernels"] = sum(v for k, v in res.items()
-                             if not k.startswith("step") and not re.match(r"(wgrad|conv1_wgrad|conv2_wgrad)_\d", k)
-                             and k not in ("sgd_reduce_only", "conv_bwd", "conv1_wgrad", "conv2_wgrad",
-                                                                   "conv2_dgrad" if eng.fused_w1 else "conv2_dgrad_w1")
+                             if not k.startswith("step") and not re.match(r"wgrad_\d", k)
+                             and k not in ("sgd_reduce_only", "conv_bwd")
                              and k not in (("conv1_fwd", "conv2_fwd") if eng.fused_fwd else ("conv12_fwd",)))
     cfg = dict(batch=a.batch, g1=eng.g1, g2=eng.g2, fc1_split=eng.fc1_split, dtype=a.dtype)
     print(json.dumps({"config": cfg, "us": {k: round(v, 2) for k, v in res.items()}}), flush=True)

@@ -1,6 +1,6 @@
-"""Sweep the fc1 forward split-K factor (and, per process, DMLC_HEAD_ROWS) of the fused CNN step at
-one batch size: whole captured steps timed, one JSON line per setting.
-usage: DMLC_HEAD_ROWS=4 python tools/sweep_fc.py [B] [split ...]"""
+"""Sweep the fc1 forward split-K factor of the fused CNN step (three-launch fc path) at one batch
+size: whole captured steps timed, one JSON line per setting.
+usage: python tools/sweep_fc.py [B] [split ...]"""
 import json
 import os
 import sys
