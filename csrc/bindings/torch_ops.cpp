@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../kernels/api.h"
+#include "../kernels/api_comm.h"
 #include "check.h"
 
 namespace {
@@ -44,6 +45,7 @@ void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>();
   a.amax = nullptr;
   a.xraw = xraw_ptr(xraw, B);
+  a.xraw_in = 0;
   if (amax.has_value()) {
     check_numel(*amax, "amax", at::kFloat, B);
     a.amax = amax->data_ptr<float>();
@@ -84,8 +86,9 @@ void fp8_roundtrip(const Tensor& x, const Tensor& y, double scale) {
 void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
                 int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& p1, const Tensor& am1,
                 const Tensor& w2f, const Tensor& b2, const Tensor& p2, const Tensor& am2,
-                const c10::optional<Tensor>& xraw) {
+                const c10::optional<Tensor>& xraw, bool xraw_in) {
   const int64_t B = p1.size(0);
+  TORCH_CHECK(!xraw_in || xraw.has_value(), "conv12_fwd: xraw_in needs the prefetched images");
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
   check(w1f, "w1f", at::kBFloat16, {64, 160});
@@ -104,6 +107,7 @@ void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tenso
   a1.w = w1f.data_ptr(); a1.bias = b1.data_ptr<float>(); a1.out = p1.data_ptr(); a1.am = am1.data_ptr<uint8_t>();
   a1.amax = nullptr;
   a1.xraw = xraw_ptr(xraw, B);
+  a1.xraw_in = xraw_in ? 1 : 0;
   DmlcConv2FwdArgs a2;
   a2.in = p1.data_ptr(); a2.w = w2f.data_ptr(); a2.bias = b2.data_ptr<float>();
   a2.out = p2.data_ptr(); a2.am = am2.data_ptr<uint8_t>(); a2.B = (int)B;
@@ -162,6 +166,7 @@ void conv1_fwd_split(const Tensor& data, const Tensor& idx, const c10::optional<
   a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>();
   a.amax = nullptr;
   a.xraw = xraw_ptr(xraw, B);
+  a.xraw_in = 0;
   CHECK_HIP(dmlc_conv1_fwd_split(&a, (int)nsplit, stream_of(out)));
 }
 
@@ -490,7 +495,8 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
          const Tensor& stats, const c10::optional<Tensor>& w2f8, const c10::optional<Tensor>& amax_w,
          const c10::optional<Tensor>& scale_w, int64_t roles, bool finalize, int64_t batch,
          const c10::optional<Tensor>& bidx, const c10::optional<Tensor>& order, double warmup, bool fc1_fused,
-         const c10::optional<Tensor>& step_rd) {
+         const c10::optional<Tensor>& step_rd, const c10::optional<Tensor>& xnext,
+         const c10::optional<Tensor>& xdata) {
   TORCH_CHECK(roles >= 0 && roles <= 2, "sgd roles must be 0..2");
   TORCH_CHECK(warmup >= 0.0, "sgd: warmup must be >= 0");
   TORCH_CHECK(mode >= 0 && mode <= 3, "sgd mode must be 0..3");
@@ -573,6 +579,14 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
     TORCH_CHECK(a.next.idx_base == nullptr, "sgd: order must be the host descriptor");
     a.bidx = bidx->data_ptr<int>(); a.bidx_n = (int)bidx->numel();
   }
+  a.xnext = nullptr; a.xdata = nullptr;
+  if (xnext.has_value()) {
+    TORCH_CHECK(xdata.has_value() && a.bidx, "sgd: xnext needs the dataset and bidx");
+    check(*xnext, "xnext", at::kByte, {a.bidx_n, 3072});
+    check_data(*xdata);
+    TORCH_CHECK(a.next.n <= xdata->size(0), "sgd: the order's rows exceed the dataset");
+    a.xnext = xnext->data_ptr<uint8_t>(); a.xdata = xdata->data_ptr<uint8_t>();
+  }
   return a;
 }
 
@@ -585,11 +599,22 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
       const Tensor &stats, const c10::optional<Tensor> &w2f8, const c10::optional<Tensor> &amax_w,          \
       const c10::optional<Tensor> &scale_w, int64_t roles, bool finalize, int64_t batch,                    \
       const c10::optional<Tensor> &bidx, const c10::optional<Tensor> &order, double warmup, bool fc1_fused,  \
-      const c10::optional<Tensor> &step_rd
+      const c10::optional<Tensor> &step_rd, const c10::optional<Tensor> &xnext, const c10::optional<Tensor> &xdata
 #define DMLC_SGD_ARGS                                                                                     \
   master, grad, mode, grad_scale, off, part1, partb1, part2, partb2, w1f, w2f, w2d, fc1n, fc2t, fc2n, fc3t, fc3d, \
       step, lr0, decay, decay_steps, staircase, ticket, loss_part, correct_part, stats, w2f8, amax_w, scale_w,  \
-      roles, finalize, batch, bidx, order, warmup, fc1_fused, step_rd
+      roles, finalize, batch, bidx, order, warmup, fc1_fused, step_rd, xnext, xdata
+
+// data parallel: the xGMI exchange of the whole flat gradient with the SGD update in its epilogue
+// (xgmi_allreduce.hip); `grad` must be the xGMI context's buffer
+void xgmi_allreduce_sgd(int64_t ctx, int64_t blocks, bool bf16_wire, DMLC_SGD_PARAMS) {
+  TORCH_CHECK(blocks >= 0 && blocks <= DMLC_XGMI_MAX_BLOCKS, "xgmi_allreduce_sgd: blocks must be in [0,128]");
+  TORCH_CHECK(mode == 2 && roles == 0 && finalize && !fc1_fused && !w2f8.has_value() && step_rd.has_value(),
+              "xgmi_allreduce_sgd: apply mode (2) over every role, bf16 shadows, the head's step copy");
+  DmlcSgdArgs a = make_sgd(DMLC_SGD_ARGS);
+  c10::DeviceGuard guard(master.device());
+  CHECK_HIP(dmlc_xgmi_allreduce_sgd((int)ctx, (int)blocks, bf16_wire ? 1 : 0, &a, stream_of(master)));
+}
 
 void sgd(DMLC_SGD_PARAMS) {
   DmlcSgdArgs a = make_sgd(DMLC_SGD_ARGS);
@@ -661,7 +686,7 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("conv2_fwd(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("conv12_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
         "Tensor(a!) p1, Tensor(b!) am1, Tensor w2f, Tensor b2, Tensor(c!) p2, Tensor(d!) am2, "
-        "Tensor(e!)? xraw=None) -> ()");
+        "Tensor(e!)? xraw=None, bool xraw_in=False) -> ()");
   m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv1_fwd_split(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
         "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? xraw, int nsplit) -> ()");
@@ -692,14 +717,23 @@ TORCH_LIBRARY(dmlc, m) {
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
         "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
-        "bool fc1_fused=False, Tensor? step_rd=None, Tensor[]? fc_acts=None) -> ()");
+        "bool fc1_fused=False, Tensor? step_rd=None, Tensor(v!)? xnext=None, Tensor? xdata=None, "
+        "Tensor[]? fc_acts=None) -> ()");
   m.def("sgd(Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor part1, Tensor partb1, "
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
         "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
         "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
-        "bool fc1_fused=False, Tensor? step_rd=None) -> ()");
+        "bool fc1_fused=False, Tensor? step_rd=None, Tensor(v!)? xnext=None, Tensor? xdata=None) -> ()");
+  m.def("xgmi_allreduce_sgd(int ctx, int blocks, bool bf16_wire, Tensor(a!) master, Tensor(b!) grad, int mode, "
+        "float grad_scale, int[] off, Tensor part1, Tensor partb1, "
+        "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
+        "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "
+        "float decay_steps, bool staircase, Tensor(l!) ticket, Tensor loss_part, Tensor correct_part, "
+        "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
+        "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
+        "bool fc1_fused=False, Tensor? step_rd=None, Tensor(v!)? xnext=None, Tensor? xdata=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
@@ -718,5 +752,6 @@ TORCH_LIBRARY_IMPL(dmlc, CUDA, m) {
   m.impl("head", &head);
   m.impl("fc_chain", &fc_chain);
   m.impl("sgd", &sgd);
+  m.impl("xgmi_allreduce_sgd", &xgmi_allreduce_sgd);
   m.impl("wgrad_sgd", &wgrad_sgd);
 }

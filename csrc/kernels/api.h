@@ -43,6 +43,8 @@ struct DmlcConv1FwdArgs {
   float* amax;              // nullable: fp8 path, float[B] per-image max of the pooled output (plain
                             //   stores, no atomics; the fp8 conv2 forward reduces them)
   uint8_t* xraw;            // nullable: copy of each row's raw uint8 image [B][3072] for the wgrad
+  int xraw_in;              // k_conv12_fwd: read row b's image from xraw[b] (written for this step by
+                            //   the previous step's finalizer), no index load, no copy-out
 };
 
 // conv2 5x5 (64->64) + bias + ReLU + maxpool 3x3/2 TF-SAME.  One workgroup per image.
@@ -252,6 +254,10 @@ struct DmlcSgdArgs {
   // 0/2 write fc1n[(s+1) & 1], mode 3 fc1n[s & 1].  fc1_fused (mode 0): the fc1 WEIGHT update already
   // ran in the dW1 GEMM's epilogue (c_mode 4) -- the fc1 role covers the fc1 bias only
   int fc1_fused;
+  // nullable: the finalizing launch also gathers the next step's raw images, xnext[b] = xdata[row of
+  // batch row b at step+1] (3072 B each), so the next forward reads its image without the index
+  // hop (DmlcConv1FwdArgs::xraw_in)
+  uint8_t* xnext; const uint8_t* xdata;
 };
 
 // Both weight gradients in one launch (blocks [0,g1): conv1; then 4 * g2 conv2 blocks, one slab per group).

@@ -31,6 +31,12 @@ int dmlc_xgmi_open(int ctx, const uint8_t* all_handles);
 // computed by one owner rank in fixed rank order and pushed to every peer, so replicas stay
 // bit-identical.  bf16_wire: the values cross the links as bf16 (sums in fp32, result bf16-rounded).
 hipError_t dmlc_xgmi_allreduce(int ctx, int64_t offset, int64_t numel, int blocks, int bf16_wire, hipStream_t s);
+// The same exchange over the whole flat gradient (the context's buffer) with the SGD update in its
+// epilogue: every thread applies the step (mode 2 of the SGD launch: master, every bf16 shadow, the
+// next batch rows; workgroup 0 publishes the stats and bumps global_step) to the elements it owns in
+// the exchange.  Replaces all-reduce + SGD launch in the data-parallel step (bf16 shadows only).
+struct DmlcSgdArgs;
+hipError_t dmlc_xgmi_allreduce_sgd(int ctx, int blocks, int bf16_wire, const DmlcSgdArgs* sgd, hipStream_t s);
 // Sticky error word of the context (device memory): bit 0 = a barrier timed out.
 int dmlc_xgmi_error(int ctx);
 void dmlc_xgmi_destroy(int ctx);

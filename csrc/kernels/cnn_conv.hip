@@ -202,9 +202,13 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int i = 0; i < 4; ++i) b4[h][i] = a1.bias[32 * cp + 16 * h + 4 * g + i];
-  const int img = batch_index(a1.src, a1.B, b);
   uint8_t* raw = reinterpret_cast<uint8_t*>(cout);          // the conv1 output region is free until its epilogue
-  stage_conv1_raw(raw, a1.data + (size_t)img * 3072, a1.xraw ? a1.xraw + (size_t)b * 3072 : nullptr, tid);
+  if (a1.xraw_in) {                            // prefetched by the previous step: one load, no index hop
+    stage_conv1_raw(raw, a1.xraw + (size_t)b * 3072, nullptr, tid);
+  } else {
+    const int img = batch_index(a1.src, a1.B, b);
+    stage_conv1_raw(raw, a1.data + (size_t)img * 3072, a1.xraw ? a1.xraw + (size_t)b * 3072 : nullptr, tid);
+  }
   lds_barrier();   // (the xraw copy's global stores need not drain)
   stage_conv1_input(xin, raw, a1.cy, a1.cx, tid);
   // conv2's padded input: zero halo (rows/cols 0,1,14,15); the interior comes from pool1

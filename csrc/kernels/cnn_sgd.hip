@@ -112,6 +112,9 @@ __global__ __launch_bounds__(256) void k_sgd(DmlcSgdArgs a) {
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r < a.bidx_n) a.bidx[r] = order_row(a.next, step + 1, r);
   }
+  // ... and their raw images (the wgrad launch, the last reader of xnext, has completed)
+  if (a.xnext)
+    for (int r = blockIdx.x; r < a.bidx_n; r += gridDim.x) copy_next_row(a, step, r, threadIdx.x);
   if (a.step_rd != a.step) {
     // the step was read from the head's copy: no block of this launch reads *a.step, so workgroup 0
     // alone sums the head's partials (an earlier launch), publishes the stats and bumps the counter

@@ -551,6 +551,10 @@ __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
       conv1_apply(a, blockIdx.x, smem, g0, step);
     }
     if (helper) conv2_help(a, blockIdx.x, smem, hg0, step);
+    // the next step's raw images over xraw: every conv1 block passed the conv1 barrier after its
+    // image loop, so no block of this launch reads xraw any more
+    if (a.apply && a.sgd.mode == 0 && a.sgd.xnext)
+      for (int r = blockIdx.x; r < a.sgd.bidx_n; r += a.w1.g1) copy_next_row(a.sgd, step, r, threadIdx.x);
     DMLC_STAMP(DMLC_TK_SGD, 4);
   } else {
     conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, smem, a.apply != 0);

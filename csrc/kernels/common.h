@@ -152,6 +152,28 @@ DEV float4 ld_sc1(rsrc_t r, uint32_t off) {
 }
 DEV void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // s_waitcnt vmcnt(0)
 
+// Producer -> next-launch activation stores (the conv kernels' pooled outputs / argmax bytes, the
+// dgrad's dY2 / dP1).  Default: streaming (nt) stores, kept in this XCD's L2 until the kernel
+// boundary writes them back.  -DDMLC_WT_STORES (experiment build): write-through (sc1) buffer
+// stores, which leave no dirty lines for the boundary's write-back.  `base` must be wave-uniform.
+#ifdef DMLC_WT_STORES
+constexpr bool kWtStores = true;
+#else
+constexpr bool kWtStores = false;
+#endif
+DEV void st_out16(void* base, uint32_t byte_off, const uint4& v) {
+  if constexpr (kWtStores)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), buf_rsrc(base), byte_off, 0, kSC1);
+  else
+    st_maybe_nt<kNtDefault>(reinterpret_cast<uint4*>(reinterpret_cast<char*>(base) + byte_off), v);
+}
+DEV void st_out8(void* base, uint32_t byte_off, const uint2& v) {
+  if constexpr (kWtStores)
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), buf_rsrc(base), byte_off, 0, kSC1);
+  else
+    st_maybe_nt<kNtDefault>(reinterpret_cast<uint2*>(reinterpret_cast<char*>(base) + byte_off), v);
+}
+
 // Sub-grid barrier among the n co-resident blocks sharing (cnt, gen) (each on its own 128-B line,
 // zero-initialised; they re-arm themselves).  Thread 0 reads the generation BEFORE its block can
 // arrive (bar_gen), arrives once the block's coherent stores are acknowledged (bar_arrive) and spins

@@ -20,8 +20,8 @@ namespace dmlc {
 // them spilled the staging registers to scratch.)  Every weight byte crosses L2 -> CU once per block.
 // Rows are 640 B with the 16-B chunks XOR-swizzled by (row & 7), which keeps the A-fragment reads
 // (16 co rows x 4 chunks per ds_read_b128) conflict-free.
-// Wave w owns c_out tiles 2cp, 2cp+1 (cp = w & 1) and pixel tiles pg, pg+4, pg+8 (< 9), pg = w >> 1:
-// per k-chunk it reads 2 A and 2-3 B fragments (ds_read_b128, conflict-free) for 4-6 MFMAs.
+// Tile ownership: see conv2_core below (per k-chunk a wave reads 2 A and 2-3 B fragments,
+// ds_read_b128, conflict-free, for 4-5 MFMAs).
 constexpr int WS_ELEMS = 64 * 320;            // one slice, bf16
 constexpr size_t WS_BYTES = 2 * WS_ELEMS * 2;
 
@@ -58,9 +58,16 @@ DEV void ws_put(bf16* buf, int w, int lane, Slice5 v) {
   p[0] = v.a; p[64] = v.b; p[128] = v.c; p[192] = v.d; p[256] = v.e;
 }
 
-template <int NPX>
-DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][NPX], int pg, int cp,
-                    int g, int li, int tid, const bf16* s0, int tk = -1) {
+// Tile ownership (r5): wave w = (cp, pg), cp = w & 1, pg = w >> 1, owns c_out tiles 2cp, 2cp+1 of the
+// pixel tiles pg and pg+4 (4 tile-units of 50 k-chunks each), and waves 0-3 also pixel tile 8 for
+// ONE c_out tile, 2cp + pg (EXTRA: 5 units).  Waves w and w+4 share a SIMD, so every SIMD carries 9
+// of the 36 units -- the earlier 2-3 pixel tiles x 2 c_out tiles per wave put 10 on two SIMDs and 8
+// on the other two.  Every output tile is still summed by one wave in the same k order, so the
+// results are bit-identical to that tiling.
+template <bool EXTRA>
+DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][2], f32x4& accx, int pg, int cp,
+                    int xsel, int g, int li, int tid, const bf16* s0, int tk = -1) {
+  constexpr int NPX = EXTRA ? 3 : 2;
   const int w = wave_id(), lane = tid & 63, sw = li & 7;
   // Per-lane LDS element offsets, computed once: every fragment read of the loop is then one
   // ds_read_b128 at (offset register + compile-time immediate), no per-chunk address VALU (the swizzle
@@ -72,7 +79,7 @@ DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][N
   int xo[NPX][8][2];
 #pragma unroll
   for (int t = 0; t < NPX; ++t) {
-    const int px = 16 * (pg + 4 * t) + li;
+    const int px = 16 * (t < 2 ? pg + 4 * t : 8) + li;
     const int y = px / 12, x = px - y * 12;
     const int pb = y * 16 + x, key0 = (x + 4 * y) & 7;
 #pragma unroll
@@ -84,7 +91,8 @@ DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][N
 #pragma unroll
   for (int s = 0; s < 2; ++s) ao[s] = (32 * cp + li) * 320 + (((4 * s + g) ^ sw) << 3);
 #pragma unroll
-  for (int t = 0; t < NPX; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
+  for (int t = 0; t < 2; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
+  accx = zero4();
   if (!s0) ws_dma(Wg, 0, ws, w, lane);
   const bf16* sb0 = s0 ? s0 : ws;
   __syncthreads();                                       // (waits vmcnt(0): the DMA has landed)
@@ -114,10 +122,11 @@ DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][N
       if (j + 1 < 10) load_chunk(kh, j + 1, A0[cur ^ 1], A1[cur ^ 1], BX[cur ^ 1]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < NPX; ++t) {
+      for (int t = 0; t < 2; ++t) {
         acc[0][t] = mfma16(A0[cur], BX[cur][t], acc[0][t]);
         acc[1][t] = mfma16(A1[cur], BX[cur][t], acc[1][t]);
       }
+      if constexpr (EXTRA) accx = mfma16(xsel ? A1[cur] : A0[cur], BX[cur][NPX - 1], accx);
       __builtin_amdgcn_sched_barrier(0);
     }
     if (kh < 4) __syncthreads();                         // next slice landed; this one fully read
@@ -126,111 +135,22 @@ DEV void conv2_core(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[2][N
   if (tk >= 0) DMLC_STAMP(tk, 7);
 }
 
-// Wide-tile variant (DMLC_CONV2_WIDE=1): wave w owns ALL 4 c_out tiles x pixel group pg x K half kk (input
-// channels 32kk..32kk+31 of every tap), pg = (w + kk) & 3 so the 3-tile group is not paired with itself
-// on a SIMD (waves w, w+4): per k-chunk 4 A + 2-3 B fragment reads for 8-12 MFMAs, i.e. 1250 instead
-// of 1700 ds_read_b128 per image (the core was LDS-bandwidth co-bound).  The two K halves meet once
-// through the slice buffer the last kernel row did not use (fixed order: deterministic).
-template <int NPX>
-DEV void conv2_core_wide(const bf16* Wg, const bf16* xin, bf16* ws, f32x4 (&acc)[4][NPX], int pg, int kk,
-                         int g, int li, int tid, const bf16* s0) {
-  const int w = wave_id(), lane = tid & 63;
-  int xo[NPX][8];
-#pragma unroll
-  for (int t = 0; t < NPX; ++t) {
-    const int px = 16 * (pg + 4 * t) + li;
-    const int y = px / 12, x = px - y * 12;
-    const int pb = y * 16 + x, key0 = (x + 4 * y) & 7;
-#pragma unroll
-    for (int d = 0; d < 8; ++d) xo[t][d] = pb * 64 + (((4 * kk + g) ^ ((key0 + d) & 7)) << 3);
-  }
-  const int ao = li * 320 + (((4 * kk + g) ^ (li & 7)) << 3);
-#pragma unroll
-  for (int t = 0; t < NPX; ++t)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c][t] = zero4();
-  if (!s0) ws_dma(Wg, 0, ws, w, lane);
-  const bf16* sb0 = s0 ? s0 : ws;
-  __syncthreads();                                       // (waits vmcnt(0): the DMA has landed)
-  auto load_chunk = [&](int kh, int kw, bf16x8 (&a)[4], bf16x8 (&bx)[NPX]) {
-    const bf16* wr = slice_buf(sb0, ws, kh) + kw * 64 + ao;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) a[c] = lds_b128(wr + c * 16 * 320);
-#pragma unroll
-    for (int t = 0; t < NPX; ++t) bx[t] = lds_b128(xin + xo[t][(kw + 4 * kh) & 7] + (kh * 16 + kw) * 64);
-  };
-#pragma unroll
-  for (int kh = 0; kh < 5; ++kh) {
-    if (kh < 4) ws_dma(Wg, kh + 1, ws + ((kh + 1) & 1) * WS_ELEMS, w, lane);
-    bf16x8 A[2][4], BX[2][NPX];
-    load_chunk(kh, 0, A[0], BX[0]);
-#pragma unroll
-    for (int kw = 0; kw < 5; ++kw) {
-      const int cur = kw & 1;
-      wait_lds();
-      __builtin_amdgcn_sched_barrier(0);
-      if (kw + 1 < 5) load_chunk(kh, kw + 1, A[cur ^ 1], BX[cur ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < NPX; ++t)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c][t] = mfma16(A[cur][c], BX[cur][t], acc[c][t]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (kh < 4) __syncthreads();                         // next slice landed; this one fully read
-  }
-}
-static_assert(9 * 4 * 64 * 16 <= WS_ELEMS * 2, "K-half partials fit one slice buffer");
-
-// fn(co_tile, px_tile, acc) for every finished 16x16 output tile (called by the waves that own it).
-// Default: the 2 co x 2-3 px tiling without a K split; DMLC_CONV2_WIDE=1 (a variant build) selects the
-// wide tiles -- measured 0.8-1.3 % SLOWER per step at B = 128 / 256 / 512 (r3, same-session A/B), so the
-// core is not bound by its LDS read bandwidth.
+// fn(co_tile, px_tile, acc) for every finished 16x16 output tile (called by the wave that owns it).
+// (A 4-c_out-tile-per-wave variant with a K split measured 0.8-1.3 % slower per step in r3: the core
+// is not bound by its LDS read bandwidth; removed in r5.)
 template <class F>
 DEV void conv2_tiles(const bf16* Wg, const bf16* xin, bf16* ws, int w, int g, int li, int tid, const bf16* s0,
                      F&& fn, int tk = -1) {
-#if !defined(DMLC_CONV2_WIDE) || !DMLC_CONV2_WIDE
   const int cp = w & 1, pg = w >> 1;
-  if (pg == 0) {
-    f32x4 acc[2][3];
-    conv2_core<3>(Wg, xin, ws, acc, pg, cp, g, li, tid, s0, tk);
-#pragma unroll
-    for (int t = 0; t < 3; ++t) { fn(2 * cp, pg + 4 * t, acc[0][t]); fn(2 * cp + 1, pg + 4 * t, acc[1][t]); }
+  f32x4 acc[2][2], accx;
+  if (w < 4) {
+    conv2_core<true>(Wg, xin, ws, acc, accx, pg, cp, pg, g, li, tid, s0, tk);
+    fn(2 * cp + pg, 8, accx);
   } else {
-    f32x4 acc[2][2];
-    conv2_core<2>(Wg, xin, ws, acc, pg, cp, g, li, tid, s0, tk);
-#pragma unroll
-    for (int t = 0; t < 2; ++t) { fn(2 * cp, pg + 4 * t, acc[0][t]); fn(2 * cp + 1, pg + 4 * t, acc[1][t]); }
+    conv2_core<false>(Wg, xin, ws, acc, accx, pg, cp, 0, g, li, tid, s0, tk);
   }
-#else
-  const int kk = w >> 2, pg = (w + kk) & 3, lane = tid & 63;
-  f32x4* red = reinterpret_cast<f32x4*>(ws + WS_ELEMS);   // slice buffer 1: free after kernel row 3
-  auto finish = [&](auto& acc, auto npx) {
-    constexpr int NPX = decltype(npx)::value;
-    if (kk == 1) {
 #pragma unroll
-      for (int t = 0; t < NPX; ++t)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) red[((pg + 4 * t) * 4 + c) * 64 + lane] = acc[c][t];
-    }
-    lds_barrier();
-    if (kk == 0) {
-#pragma unroll
-      for (int t = 0; t < NPX; ++t)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) fn(c, pg + 4 * t, acc[c][t] + red[((pg + 4 * t) * 4 + c) * 64 + lane]);
-    }
-  };
-  if (pg == 0) {
-    f32x4 acc[4][3];
-    conv2_core_wide<3>(Wg, xin, ws, acc, pg, kk, g, li, tid, s0);
-    finish(acc, std::integral_constant<int, 3>{});
-  } else {
-    f32x4 acc[4][2];
-    conv2_core_wide<2>(Wg, xin, ws, acc, pg, kk, g, li, tid, s0);
-    finish(acc, std::integral_constant<int, 2>{});
-  }
-#endif
+  for (int t = 0; t < 2; ++t) { fn(2 * cp, pg + 4 * t, acc[0][t]); fn(2 * cp + 1, pg + 4 * t, acc[1][t]); }
 }
 
 // conv2 input gradient of image b: pool2/ReLU backward (gather over the 2x2 ownership windows) into
@@ -302,7 +222,7 @@ DEV void conv2_dgrad_image(const DmlcConv2DgradArgs& a, int b, char* smem, unsig
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
-      st_maybe_nt<kNtDg>(reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + pc * 8), dv[k]);
+      st_out16(dy2, (uint32_t)((y * 12 + x) * 64 + pc * 8) * 2, __builtin_bit_cast(uint4, dv[k]));
     }
   }
   lds_barrier();   // publishes dyp only; the dy2 global stores need not drain here
@@ -318,7 +238,7 @@ DEV void conv2_dgrad_image(const DmlcConv2DgradArgs& a, int b, char* smem, unsig
   bf16* dp1 = reinterpret_cast<bf16*>(a.dp1) + (size_t)b * 9216;
   for (int s = tid; s < 1152; s += NT) {
     const int p = s >> 3, c = s & 7;
-    st_maybe_nt<kNtDg>(reinterpret_cast<bf16x8*>(dp1 + p * 64 + c * 8), lds_b128(outs + swz128(p, c)));
+    st_out16(dp1, (uint32_t)(p * 64 + c * 8) * 2, __builtin_bit_cast(uint4, lds_b128(outs + swz128(p, c))));
   }
   DMLC_STAMP(DMLC_TK_DGRAD, 4);
 }

@@ -229,8 +229,8 @@ DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid, uint32_t* 
       if (j < 4) alo |= arg << (8 * j);
       else ahi |= arg << (8 * (j - 4));
     }
-    st_maybe_nt<kNtFwd>(reinterpret_cast<uint4*>(out + q * 64 + c * 8), o);
-    st_maybe_nt<kNtFwd>(reinterpret_cast<uint2*>(am + q * 64 + c * 8), make_uint2(alo, ahi));
+    st_out16(out, (uint32_t)(q * 64 + c * 8) * 2, o);
+    st_out8(am, (uint32_t)(q * 64 + c * 8), make_uint2(alo, ahi));
     if (pad_lds) *reinterpret_cast<uint4*>(pad_lds + swzpad((py + 2) * (HO + 4) + px + 2, c)) = o;
   }
   if (vmax) *vmax = bmax;

@@ -230,6 +230,15 @@ DEV void fc_role(const DmlcSgdArgs& a, int r, float lr, int64_t step, float4* ld
   else fc_tail_block(a, r - FC2_BLOCKS, lr, tid);
 }
 
+// The next step's raw image of batch row `row` into xnext[row] (192 16-B chunks; threads tid < 192 of
+// the caller copy one each).  Called once every reader of the current xnext contents is done.
+DEV void copy_next_row(const DmlcSgdArgs& a, int64_t step, int row, int tid) {
+  if (tid >= 192) return;
+  const int src = order_row(a.next, step + 1, row);
+  reinterpret_cast<uint4*>(a.xnext + (size_t)row * 3072)[tid] =
+      reinterpret_cast<const uint4*>(a.xdata + (size_t)src * 3072)[tid];
+}
+
 // Publish the step's stats into the ring and bump the device global_step (one wave, lanes < 64).
 // loss / accuracy partials come from the head (an earlier launch).
 DEV void publish_step(const DmlcSgdArgs& a, int64_t step, float lr, int lane) {

@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "api_comm.h"
+#include "sgd_common.h"
 
 namespace dmlc {
 
@@ -99,14 +100,10 @@ __device__ __forceinline__ float4 unpack_bf16x4(uint2 u) {
                      __uint_as_float(u.y & 0xffff0000u));
 }
 
+// The exchange of one launch: returns once every element this thread owns (element i belongs to
+// thread (i - off4) % stride in EVERY phase) holds the sum over ranks in this rank's buffer.
 template <int W, bool BF16>
-__global__ __launch_bounds__(XT) void k_xgmi_allreduce(XgmiArgs a) {
-  XgmiSignal* self = a.sigs[a.rank];
-  __shared__ uint32_t s_e;
-  if (threadIdx.x == 0) s_e = ld_sys(&self->epoch[blockIdx.x]) + 1u;
-  __syncthreads();
-  const uint32_t e = s_e;
-  const int64_t stride = (int64_t)gridDim.x * XT, t0 = (int64_t)blockIdx.x * XT + threadIdx.x;
+__device__ __forceinline__ void xgmi_exchange(const XgmiArgs& a, uint32_t e, int64_t t0, int64_t stride) {
   if (BF16)                            // my whole bucket -> my wire buffer (read by the owners)
     for (int64_t i = a.off4 + t0; i < a.off4 + a.n4; i += stride) a.wires[a.rank][i] = pack_bf16x4(a.bufs[a.rank][i]);
 
@@ -140,7 +137,82 @@ __global__ __launch_bounds__(XT) void k_xgmi_allreduce(XgmiArgs a) {
   peer_barrier<W>(a, 1, e);            // every rank's pushes into my buffer landed
   if (BF16)                            // every slice, mine included, from the bf16 sums
     for (int64_t i = a.off4 + t0; i < a.off4 + a.n4; i += stride) a.bufs[a.rank][i] = unpack_bf16x4(a.wires[a.rank][i]);
-  if (threadIdx.x == 0) st_sys(&self->epoch[blockIdx.x], e);
+}
+
+template <int W, bool BF16>
+__global__ __launch_bounds__(XT) void k_xgmi_allreduce(XgmiArgs a) {
+  XgmiSignal* self = a.sigs[a.rank];
+  __shared__ uint32_t s_e;
+  if (threadIdx.x == 0) s_e = ld_sys(&self->epoch[blockIdx.x]) + 1u;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * XT, t0 = (int64_t)blockIdx.x * XT + threadIdx.x;
+  xgmi_exchange<W, BF16>(a, s_e, t0, stride);
+  if (threadIdx.x == 0) st_sys(&self->epoch[blockIdx.x], s_e);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Exchange + SGD in ONE launch (data parallel, r5): the step's optimizer update runs in the
+// all-reduce kernel's epilogue instead of a separate SGD launch.  After the second peer barrier each
+// thread owns a fixed set of float4s of the flat gradient (the exchange's element -> thread map), so
+// it applies SGD to exactly those: master -= lr * grad_scale * sum, plus every bf16 shadow of those
+// four weights in the layout its kernel reads -- the SGD launch's mode-2 expressions
+// (sgd_common.h), so the weights are bit-identical to all-reduce + SGD launch
+// (tests/test_fused_dp_gpu.py::test_xgmi_sgd_epilogue_is_bit_identical).  Workgroup 0 then publishes
+// the step's stats and bumps global_step (the LR came from the head's step copy); every thread
+// writes its next-step batch row.  bf16 shadows only: the fp8 path keeps its SGD launch.
+__device__ __forceinline__ void sgd_apply4(const DmlcSgdArgs& s, int64_t q, float lr, int64_t step) {
+  const int e0 = (int)(4 * q), end = s.off[9] + 10;
+  if (e0 >= end) return;
+  const float f = lr * s.grad_scale;
+  if (e0 + 4 > end) {                  // the fc3 bias tail: master is exactly `end` floats long
+    for (int e = e0; e < end; ++e) s.master[e] -= f * s.grad[e];
+    return;
+  }
+  float4 w = *reinterpret_cast<const float4*>(s.master + e0);
+  const float4 g = *reinterpret_cast<const float4*>(s.grad + e0);
+  w.x -= f * g.x; w.y -= f * g.y; w.z -= f * g.z; w.w -= f * g.w;
+  *reinterpret_cast<float4*>(s.master + e0) = w;
+  if (e0 < s.off[1]) {                                  // conv1 kernel HWIO [5,5,3,64]
+    const int r = e0 - s.off[0];
+    conv1_shadow4(s, r >> 6, r & 63, w);
+  } else if (e0 >= s.off[2] && e0 < s.off[3]) {         // conv2 kernel [5,5,64,64]
+    const int r = e0 - s.off[2];
+    conv2_shadow4(s, r >> 6, r & 63, w);
+  } else if (e0 >= s.off[4] && e0 < s.off[5]) {         // fc1 weight: same-layout shadow, next step's slot
+    bf16* shadow = reinterpret_cast<bf16*>(s.fc1n) + (((step + 1) & 1) ? 884736 : 0);
+    *reinterpret_cast<bf16x4*>(shadow + (e0 - s.off[4])) = pack4(w.x, w.y, w.z, w.w);
+  } else if (e0 >= s.off[6] && e0 < s.off[7]) {         // fc2 weight [384 k][192 n]
+    const int r = e0 - s.off[6], k = r / 192, n = r - k * 192;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(s.fc2n) + r) = pack4(w.x, w.y, w.z, w.w);
+    bf16* t = reinterpret_cast<bf16*>(s.fc2t) + (size_t)n * 384 + k;
+    t[0] = (bf16)w.x; t[384] = (bf16)w.y; t[2 * 384] = (bf16)w.z; t[3 * 384] = (bf16)w.w;
+  } else if (e0 >= s.off[8] && e0 < s.off[9]) {         // fc3 weight [192 k][10 n]
+    const float v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = e0 - s.off[8] + j, k = r / 10, n = r - k * 10;
+      reinterpret_cast<bf16*>(s.fc3t)[n * 192 + k] = (bf16)v[j];
+      reinterpret_cast<bf16*>(s.fc3d)[k * 32 + n] = (bf16)v[j];
+    }
+  }                                                      // biases: no shadow
+}
+
+template <int W, bool BF16>
+__global__ __launch_bounds__(XT) void k_xgmi_allreduce_sgd(XgmiArgs a, DmlcSgdArgs s) {
+  XgmiSignal* self = a.sigs[a.rank];
+  __shared__ uint32_t s_e;
+  if (threadIdx.x == 0) s_e = ld_sys(&self->epoch[blockIdx.x]) + 1u;
+  const int64_t step = *s.step_rd;                       // the head's copy: nobody bumps it here
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * XT, t0 = (int64_t)blockIdx.x * XT + threadIdx.x;
+  xgmi_exchange<W, BF16>(a, s_e, t0, stride);
+  const float lr = lr_of(s, step);
+  for (int64_t i = a.off4 + t0; i < a.off4 + a.n4; i += stride) sgd_apply4(s, i, lr, step);
+  if (s.bidx && t0 < s.bidx_n) s.bidx[t0] = order_row(s.next, step + 1, (int)t0);
+  if (s.xnext)
+    for (int r = blockIdx.x; r < s.bidx_n; r += gridDim.x) copy_next_row(s, step, r, threadIdx.x);
+  if (blockIdx.x == 0 && threadIdx.x < 64) publish_step(s, step, lr, threadIdx.x);
+  if (threadIdx.x == 0) st_sys(&self->epoch[blockIdx.x], s_e);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -310,6 +382,41 @@ hipError_t dmlc_xgmi_allreduce(int id, int64_t offset, int64_t numel, int blocks
     DMLC_XGMI_CASE(1) DMLC_XGMI_CASE(2) DMLC_XGMI_CASE(3) DMLC_XGMI_CASE(4)
     DMLC_XGMI_CASE(5) DMLC_XGMI_CASE(6) DMLC_XGMI_CASE(7) DMLC_XGMI_CASE(8)
 #undef DMLC_XGMI_CASE
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t dmlc_xgmi_allreduce_sgd(int id, int blocks, int bf16_wire, const DmlcSgdArgs* sgd, hipStream_t s) {
+  XgmiCtx* c = get(id);
+  if (!c || !c->opened || !sgd) return hipErrorInvalidValue;
+  // the whole flat buffer, apply from the summed gradient (mode 2), the head's step copy, bf16 shadows
+  const int64_t end = (int64_t)sgd->off[9] + 10;
+  if (sgd->mode != 2 || sgd->w2f8 || sgd->step_rd == sgd->step || sgd->grad != c->buf || end > c->numel ||
+      sgd->fc1_fused || sgd->roles != 0 || !sgd->finalize)
+    return hipErrorInvalidValue;
+  XgmiArgs a;
+  for (int p = 0; p < DMLC_XGMI_MAX_RANKS; ++p) {
+    a.bufs[p] = reinterpret_cast<float4*>(c->peer_buf[p]);
+    a.wires[p] = reinterpret_cast<uint2*>(c->peer_wire[p]);
+    a.sigs[p] = c->peer_sig[p];
+  }
+  a.rank = c->rank;
+  a.host_err = c->host_err_dev;
+  a.off4 = 0;
+  a.n4 = (end + 3) / 4;
+  if (blocks <= 0) blocks = DMLC_XGMI_MAX_BLOCKS;        // the epilogue streams the whole buffer
+  blocks = std::min(blocks, DMLC_XGMI_MAX_BLOCKS);
+  if ((int64_t)blocks * XT < sgd->bidx_n) return hipErrorInvalidValue;   // one batch row per thread
+  switch (c->world) {
+#define DMLC_XGMI_SGD_CASE(W)                                                                          \
+    case W:                                                                                            \
+      if (bf16_wire) hipLaunchKernelGGL((k_xgmi_allreduce_sgd<W, true>), dim3(blocks), dim3(XT), 0, s, a, *sgd); \
+      else hipLaunchKernelGGL((k_xgmi_allreduce_sgd<W, false>), dim3(blocks), dim3(XT), 0, s, a, *sgd);         \
+      break;
+    DMLC_XGMI_SGD_CASE(1) DMLC_XGMI_SGD_CASE(2) DMLC_XGMI_SGD_CASE(3) DMLC_XGMI_SGD_CASE(4)
+    DMLC_XGMI_SGD_CASE(5) DMLC_XGMI_SGD_CASE(6) DMLC_XGMI_SGD_CASE(7) DMLC_XGMI_SGD_CASE(8)
+#undef DMLC_XGMI_SGD_CASE
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

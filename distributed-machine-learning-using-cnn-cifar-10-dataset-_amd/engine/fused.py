@@ -85,6 +85,8 @@ VARIANT_DEFAULTS = {
     "wgrad_sgd": True,         # in-launch SGD / slab reduction of the wgrad launch; env DMLC_WGRAD_SGD=0 off
     "wgrad_sgd_fp8": False,    # the same for --dtype fp8 (bit-identical, measured 1.4 % slower at B=1024)
     "fp8_dgrad": True,         # fp8: the conv2 input gradient on e4m3 too
+    "comm_sgd": True,          # data parallel over xGMI: the SGD in the exchange kernel's epilogue
+    "xraw_prefetch": True,     # the step's raw images gathered by the previous step's finalizer
 }
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
@@ -179,6 +181,11 @@ class FusedCifarEngine:
                        else [self._buckets[True], self._buckets[False]])
             self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev, pattern,
                                                  mode=allreduce, group=process_group, wire=comm_dtype)
+        elif dp_force and world_size == 1 and allreduce == "xgmi" and dev.type == "cuda":
+            # a one-rank xGMI context (no peers): the DP step's exchange kernel on a single GPU
+            from ..parallel import xgmi as X
+            self.xgmi = X.XgmiAllReduce(self.master.numel(), 0, 1, None, wire=comm_dtype)
+            self.comm_info = {"allreduce": "xgmi", "wire": comm_dtype}
         if self.xgmi is not None:
             self.grad = self.xgmi.buf[:self.master.numel()]
             self.grad.zero_()
@@ -317,6 +324,15 @@ class FusedCifarEngine:
         # the data-parallel step takes the in-launch reduction exactly when compute_gradients() does
         # (one predicate: the DP step and _conv_backward can never disagree)
         self.wgrad_reduce = self.dp and self._grad_in_launch
+        # data parallel over xGMI, serial schedule: the exchange kernel applies the SGD in its epilogue
+        # (k_xgmi_allreduce_sgd: no SGD launch; bit-identical weights).  bf16 shadows only (fp8 keeps
+        # its SGD launch: the e4m3 shadows need the weight amax of the whole tensor).
+        self.comm_sgd = self.xgmi is not None and not self.fp8 and bool(V["comm_sgd"])
+        # the training forward (conv12_fwd) reads its raw images from xraw, which the previous step's
+        # finalizer (wgrad apply mode, the SGD launch or the xGMI+SGD kernel) filled with the next
+        # step's rows -- one image load instead of index load -> image load at the head of the step;
+        # the host fills it whenever it sets the step (_sync_bidx)
+        self.xraw_prefetch = self.fused_fwd and not self.fp8 and self.conv_split == 1 and bool(V["xraw_prefetch"])
         self.wbar = torch.zeros(WBAR_WORDS, dtype=torch.int32, device=dev)   # barrier words + error word
         # pinned host copy of the barrier error word, refreshed by queue_error_copy() behind each
         # chunk of steps (the trainer checks it at every progress point without a device sync)
@@ -395,6 +411,12 @@ class FusedCifarEngine:
 
     def _sync_bidx(self):
         self.bidx.copy_(self._padded(self.batch_indices(self.host_step)))
+        self._sync_xraw()
+
+    def _sync_xraw(self):
+        """The current step's raw images into xraw (the prefetching forward reads them there)."""
+        if getattr(self, "xraw_prefetch", False):
+            self.xraw.copy_(self.data.index_select(0, self.bidx.long()).view(self.B, 3072))
 
     # --- data order ---------------------------------------------------------------------------
     def epoch_permutation(self, epoch: int) -> torch.Tensor:
@@ -422,8 +444,9 @@ class FusedCifarEngine:
                               self.am1, self.xraw if train else None, self.conv1_split)
             o.conv2_fwd_split(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
         elif self.fused_fwd and not self.fp8:      # conv1 + pool1 + conv2 + pool2 in one launch
+            pre = train and self.xraw_prefetch and idx is self.bidx   # the step's own (prefetched) batch
             o.conv12_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
-                         self.am1, self.w2f, p["conv2_bias"], self.p2, self.am2, self.xraw if train else None)
+                         self.am1, self.w2f, p["conv2_bias"], self.p2, self.am2, self.xraw if train else None, pre)
         else:
             o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
                         self.am1, self.amax_x if self.fp8 else None, self.xraw if train else None)
@@ -511,7 +534,8 @@ class FusedCifarEngine:
                 self.loss_part, self.correct_part, self.stats,
                 *((self.w2f8, self.amax_w, self.scale_w) if self.fp8 else (None, None, None)),
                 roles, finalize, self.Bv, self.bidx, self.order_desc, self.warmup, fc1_fused,
-                None if mode == 3 else self.step_sgd)
+                None if mode == 3 else self.step_sgd,
+                *((self.xraw, self.data) if self.xraw_prefetch and mode in (0, 2) and finalize else (None, None)))
 
     def _sgd(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True, fc1_fused: bool = False):
         self.ops.sgd(*self._sgd_args(mode, scale, roles, finalize, fc1_fused))
@@ -633,8 +657,10 @@ class FusedCifarEngine:
             self._fc_backward()
             if self._grad_in_launch:
                 self._conv_backward(src=(ids, None, 1), reduce=True)
+                self._sync_xraw()                    # the explicit rows went through xraw
                 return self.grad
             self._conv_backward(src=(ids, None, 1))
+            self._sync_xraw()
         self._sgd(mode=1)
         return self.grad
 
@@ -676,9 +702,13 @@ class FusedCifarEngine:
 
     def _serial_dp_step(self, seg):
         """Single-stream data-parallel step: fwd + bwd + conv-grad reduction | ONE all-reduce of the
-        whole flat gradient (4.27 MB fp32; the two buckets are contiguous) | one SGD launch."""
+        whole flat gradient (4.27 MB fp32; the two buckets are contiguous) | one SGD launch -- or, over
+        xGMI (comm_sgd), the exchange kernel that applies the SGD itself."""
         seg[0]()
         n = self.master.numel()
+        if self.comm_sgd:           # (xGMI: the whole step is one graph, seg is never a replay list)
+            self.xgmi.all_reduce_sgd(self._sgd_args(mode=2))
+            return
         if self.xgmi is not None:
             self.xgmi.all_reduce(0, n)
         else:

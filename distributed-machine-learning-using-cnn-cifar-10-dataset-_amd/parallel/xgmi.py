@@ -66,6 +66,12 @@ class XgmiAllReduce:
         """Sum-all-reduce ``buf[offset:offset+numel]`` on the current stream (capturable)."""
         self.ops.xgmi_allreduce(self.ctx, self.buf, int(offset), int(numel), int(blocks), self.bf16)
 
+    def all_reduce_sgd(self, sgd_args: tuple, blocks: int = 0):
+        """Sum-all-reduce the whole buffer (the flat gradient) and apply the SGD step in the same
+        launch (xgmi_allreduce.hip k_xgmi_allreduce_sgd; ``sgd_args`` = the engine's mode-2 SGD
+        arguments, its grad being this buffer).  Capturable."""
+        self.ops.xgmi_allreduce_sgd(self.ctx, int(blocks), self.bf16, *sgd_args)
+
     def error(self) -> int:
         return int(self.ops.xgmi_error(self.ctx))
 

@@ -215,3 +215,39 @@ def test_captured_rccl_allreduce_world1_equals_single_gpu(tmp_path, dtype, B):
         assert r["step"] == steps, sched
         assert r["info"]["captured_comm"] and r["info"]["backend"] == "nccl", r["info"]
         assert torch.equal(r["flat"], ref.flat_params()), sched
+
+
+@pytest.mark.parametrize("B,comm_dtype", [(32, "fp32"), (256, "fp32"), (64, "bf16")])
+def test_xgmi_sgd_epilogue_is_bit_identical(B, comm_dtype):
+    """r5 DP step without an SGD launch: the xGMI exchange kernel applies the SGD in its epilogue
+    (k_xgmi_allreduce_sgd) to the float4s each thread owns in the exchange.  On a one-rank xGMI
+    context (dp_force) the weights, every bf16 shadow, the next batch rows, the stats and the step
+    counter after eager + chained graph replays equal the exchange + SGD-launch step bit for bit --
+    and, for the fp32 wire (a one-rank sum is the identity), the single-GPU step."""
+    from dmlc.engine.fused import FusedCifarEngine
+    x, y = _data()
+    kw = dict(device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dp_force=True, allreduce="xgmi",
+              dp_schedule="serial", comm_dtype=comm_dtype)
+    fused = FusedCifarEngine(B, x, y, **kw)
+    ref = FusedCifarEngine(B, x, y, **kw, variant={"comm_sgd": False})
+    single = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False)
+    assert fused.comm_sgd and not ref.comm_sgd and fused.comm_info["allreduce"] == "xgmi"
+    for eng in (fused, ref, single):
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(8)
+        eng.set_step(eng.global_step() + 2)
+        eng.run(3)
+    torch.cuda.synchronize()
+    assert fused.global_step() == ref.global_step() == 14
+    assert torch.isfinite(ref.master).all()
+    assert torch.equal(fused.master, ref.master)
+    for name in ("w1f", "w2f", "w2d", "fc2t", "fc2n", "fc3t", "fc3d", "bidx"):
+        assert torch.equal(getattr(fused, name), getattr(ref, name)), name
+    assert torch.equal(fused.fc1n_current(), ref.fc1n_current())
+    for s in (10, 11, 14):
+        assert fused.read_stats(s) == ref.read_stats(s), s
+    fused.check_comm()
+    if comm_dtype == "fp32":
+        assert torch.equal(fused.master, single.master)
+        assert torch.equal(fused.fc1n_current(), single.fc1n_current())

@@ -444,3 +444,33 @@ def test_fc_chain_graph_replay_is_deterministic():
     torch.cuda.synchronize()
     assert torch.equal(engs[0].master, engs[1].master)
     assert engs[0].read_stats(24) == engs[1].read_stats(24)
+
+
+@pytest.mark.parametrize("B", [144, 256])
+def test_xraw_prefetch_is_bit_identical(B):
+    """r5: the training forward reads its raw images from xraw, gathered for it by the previous step's
+    finalizer (the wgrad launch's conv1 blocks on one GPU), instead of index -> image loads.  Chained
+    graph replays across an epoch boundary, a host set_step, an explicit-index compute_gradients()
+    and an evaluation in between: weights and stats equal the gathering forward bit for bit."""
+    data, labels = _synthetic(3 * B, seed=81)          # 3 steps per epoch: the chains cross epochs
+    kw = dict(seed=82, lr=1e-4, relu_logits=False)
+    pre = FusedCifarEngine(B, data, labels, **kw)
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"xraw_prefetch": False})
+    assert pre.xraw_prefetch and not ref.xraw_prefetch
+    idx = torch.randperm(3 * B, generator=torch.Generator().manual_seed(7))[:B].to(torch.int32)
+    for eng in (pre, ref):
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(5)
+        eng.compute_gradients(idx)
+        eng.evaluate(data[:B], labels[:B])
+        eng.run(3)
+        eng.set_step(eng.global_step() + 1)
+        eng.run(4)
+    torch.cuda.synchronize()
+    assert pre.global_step() == ref.global_step() == 14
+    assert torch.isfinite(ref.master).all()
+    assert torch.equal(pre.master, ref.master)
+    assert torch.equal(pre.xraw, ref.xraw)
+    for s in (9, 14):
+        assert pre.read_stats(s) == ref.read_stats(s), s
