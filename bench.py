@@ -131,7 +131,17 @@ def parse():
     # at B=256 in every window of the probe): the number does not depend on it, but the run is valid.
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--relu-logits", action="store_true", help="the reference's ReLU on the logits (D4)")
+    ap.add_argument("--variant", default="",
+                    help="engine path choices for A/B runs, key=0|1,... (engine/fused.py VARIANT_DEFAULTS)")
     return ap.parse_args()
+
+
+def _variant(spec: str) -> dict:
+    out = {}
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=")
+        out[k] = bool(int(v))
+    return out
 
 
 def make_data(n, device, seed=0):
@@ -153,7 +163,8 @@ def build_fused(args, info, data, labels):
                            rank=info.rank, seed=0, lr=args.lr, relu_logits=args.relu_logits,
                            comm_dtype=args.comm_dtype, dtype=args.dtype,
                            allreduce=args.allreduce, capture_comm=_capture_comm(args),
-                           dp_schedule="serial" if args.dp_schedule == "auto" else args.dp_schedule)
+                           dp_schedule="serial" if args.dp_schedule == "auto" else args.dp_schedule,
+                           variant=_variant(args.variant))
     step = eng.step
     return eng, step, (None if args.no_graph else lambda: eng.capture(args.steps_per_graph))
 
@@ -309,6 +320,7 @@ def main():
                 "graph_warmup_steps": graph_warm,
                 "network": net,
                 "steps_per_graph": args.steps_per_graph if capture is not None else None,
+                **({"variant": args.variant} if args.variant else {}),
             },
         }
         print(json.dumps(line), flush=True)

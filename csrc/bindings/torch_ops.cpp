@@ -608,7 +608,7 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
 // data parallel: the xGMI exchange of the whole flat gradient with the SGD update in its epilogue
 // (xgmi_allreduce.hip); `grad` must be the xGMI context's buffer
 void xgmi_allreduce_sgd(int64_t ctx, int64_t blocks, bool bf16_wire, DMLC_SGD_PARAMS) {
-  TORCH_CHECK(blocks >= 0 && blocks <= DMLC_XGMI_MAX_BLOCKS, "xgmi_allreduce_sgd: blocks must be in [0,128]");
+  TORCH_CHECK(blocks >= 0 && blocks <= DMLC_XGMI_MAX_BLOCKS, "xgmi_allreduce_sgd: blocks must be in [0,512]");
   TORCH_CHECK(mode == 2 && roles == 0 && finalize && !fc1_fused && !w2f8.has_value() && step_rd.has_value(),
               "xgmi_allreduce_sgd: apply mode (2) over every role, bf16 shadows, the head's step copy");
   DmlcSgdArgs a = make_sgd(DMLC_SGD_ARGS);

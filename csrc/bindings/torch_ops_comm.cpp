@@ -53,7 +53,7 @@ void xgmi_allreduce(int64_t ctx, const Tensor& buf, int64_t offset, int64_t nume
   TORCH_CHECK(buf.data_ptr<float>() == dmlc_xgmi_buffer((int)ctx), "xgmi_allreduce: buf is not the context's buffer");
   TORCH_CHECK(offset >= 0 && numel > 0 && offset % 4 == 0 && numel % 4 == 0 && offset + numel <= buf.numel(),
               "xgmi_allreduce: range must be 16-byte aligned and inside the buffer");
-  TORCH_CHECK(blocks >= 0 && blocks <= DMLC_XGMI_MAX_BLOCKS, "xgmi_allreduce: blocks must be in [0,128]");
+  TORCH_CHECK(blocks >= 0 && blocks <= DMLC_XGMI_MAX_BLOCKS, "xgmi_allreduce: blocks must be in [0,512]");
   c10::DeviceGuard guard(buf.device());
   CHECK_HIP(dmlc_xgmi_allreduce((int)ctx, offset, numel, (int)blocks, bf16_wire ? 1 : 0, stream_of(buf)));
 }

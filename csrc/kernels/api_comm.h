@@ -9,7 +9,7 @@
 #include <stdint.h>
 
 #define DMLC_XGMI_MAX_RANKS 8
-#define DMLC_XGMI_MAX_BLOCKS 128
+#define DMLC_XGMI_MAX_BLOCKS 512
 #define DMLC_XGMI_HANDLE_BYTES 64   // sizeof(hipIpcMemHandle_t)
 #define DMLC_XGMI_HANDLES 3         // per rank: data buffer, signal block, bf16 wire buffer
 

@@ -57,17 +57,22 @@ DEV void pool_emit_c(const bf16* img, bf16* out, uint8_t* am, int c0, int tid) {
     uint32_t key[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) key[j] = 0;
+    // branch-free (see pool_emit): all 9 taps loaded back to back, padding taps masked to key 0
+    uint4 v[9];
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
-      const int y = 2 * py + d / 3, x = 2 * px + d % 3;
-      if ((d / 3 < 2 || y < H) && (d % 3 < 2 || x < H)) {
-        const uint4 v = *reinterpret_cast<const uint4*>(img + swzc<CH>(y * H + x, c));
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w}, tag = 15 - d;
+      const int y = min(2 * py + d / 3, H - 1), x = min(2 * px + d % 3, H - 1);
+      v[d] = *reinterpret_cast<const uint4*>(img + swzc<CH>(y * H + x, c));
+    }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          key[2 * i] = max(key[2 * i], ((wv[i] << 16) & 0x7fff0000u) | tag);
-          key[2 * i + 1] = max(key[2 * i + 1], (wv[i] & 0x7fff0000u) | tag);
-        }
+    for (int d = 0; d < 9; ++d) {
+      const bool ok = (d / 3 < 2 || 2 * py + 2 < H) && (d % 3 < 2 || 2 * px + 2 < H);
+      const uint32_t m = ok ? 0xffffffffu : 0u, tag = 15 - d;
+      const uint32_t wv[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        key[2 * i] = max(key[2 * i], (((wv[i] << 16) & 0x7fff0000u) | tag) & m);
+        key[2 * i + 1] = max(key[2 * i + 1], ((wv[i] & 0x7fff0000u) | tag) & m);
       }
     }
     uint4 o;

@@ -153,13 +153,14 @@ DEV float4 ld_sc1(rsrc_t r, uint32_t off) {
 DEV void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // s_waitcnt vmcnt(0)
 
 // Producer -> next-launch activation stores (the conv kernels' pooled outputs / argmax bytes, the
-// dgrad's dY2 / dP1).  Default: streaming (nt) stores, kept in this XCD's L2 until the kernel
-// boundary writes them back.  -DDMLC_WT_STORES (experiment build): write-through (sc1) buffer
-// stores, which leave no dirty lines for the boundary's write-back.  `base` must be wave-uniform.
-#ifdef DMLC_WT_STORES
-constexpr bool kWtStores = true;
-#else
+// dgrad's dY2 / dP1): write-through (sc1) buffer stores, which leave no dirty lines in this XCD's L2
+// for the kernel boundary's write-back (r5 same-box A/B at B=256: 79.1 / 79.4 vs 79.8 / 80.4 us per
+// step with streaming nt stores, profiles/r5_ab_wt_pool_prefetch.txt).  -DDMLC_NO_WT_STORES builds
+// the streaming form.  `base` must be wave-uniform.
+#ifdef DMLC_NO_WT_STORES
 constexpr bool kWtStores = false;
+#else
+constexpr bool kWtStores = true;
 #endif
 DEV void st_out16(void* base, uint32_t byte_off, const uint4& v) {
   if constexpr (kWtStores)

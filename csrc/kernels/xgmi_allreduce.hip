@@ -405,7 +405,9 @@ hipError_t dmlc_xgmi_allreduce_sgd(int id, int blocks, int bf16_wire, const Dmlc
   a.host_err = c->host_err_dev;
   a.off4 = 0;
   a.n4 = (end + 3) / 4;
-  if (blocks <= 0) blocks = DMLC_XGMI_MAX_BLOCKS;        // the epilogue streams the whole buffer
+  // the epilogue streams the whole buffer (master, gradient, shadows: ~15 MB at this model's size):
+  // two workgroups per CU, as many as the SGD launch it replaces keeps busy (128 measured 2x slower)
+  if (blocks <= 0) blocks = DMLC_XGMI_MAX_BLOCKS;
   blocks = std::min(blocks, DMLC_XGMI_MAX_BLOCKS);
   if ((int64_t)blocks * XT < sgd->bidx_n) return hipErrorInvalidValue;   // one batch row per thread
   switch (c->world) {

@@ -85,7 +85,7 @@ VARIANT_DEFAULTS = {
     "wgrad_sgd": True,         # in-launch SGD / slab reduction of the wgrad launch; env DMLC_WGRAD_SGD=0 off
     "wgrad_sgd_fp8": False,    # the same for --dtype fp8 (bit-identical, measured 1.4 % slower at B=1024)
     "fp8_dgrad": True,         # fp8: the conv2 input gradient on e4m3 too
-    "comm_sgd": True,          # data parallel over xGMI: the SGD in the exchange kernel's epilogue
+    "comm_sgd": False,         # data parallel over xGMI: the SGD in the exchange kernel's epilogue
     "xraw_prefetch": True,     # the step's raw images gathered by the previous step's finalizer
 }
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
@@ -324,10 +324,18 @@ class FusedCifarEngine:
         # the data-parallel step takes the in-launch reduction exactly when compute_gradients() does
         # (one predicate: the DP step and _conv_backward can never disagree)
         self.wgrad_reduce = self.dp and self._grad_in_launch
-        # data parallel over xGMI, serial schedule: the exchange kernel applies the SGD in its epilogue
-        # (k_xgmi_allreduce_sgd: no SGD launch; bit-identical weights).  bf16 shadows only (fp8 keeps
-        # its SGD launch: the e4m3 shadows need the weight amax of the whole tensor).
+        # data parallel over xGMI, serial schedule, variant comm_sgd: the exchange kernel applies the
+        # SGD in its epilogue (k_xgmi_allreduce_sgd: no SGD launch; bit-identical weights; bf16 shadows
+        # only).  Off by default: measured on one GPU (tools/dp1_ab.py, world-1 xGMI context, B=256)
+        # the DP step took 103.0 us with the epilogue on the exchange's 128 workgroups and 142.2 us on
+        # 512 (every workgroup pays the barriers' system-scope release fences) vs 96.2 us for exchange
+        # + the 800-workgroup SGD launch (profiles/r5_dp1_ab_128blocks.jsonl, r5_dp1_ab_512blocks.jsonl).
         self.comm_sgd = self.xgmi is not None and not self.fp8 and bool(V["comm_sgd"])
+        # workgroups of the exchange + SGD kernel: 2 per CU on a GPU of its own (the epilogue streams
+        # the whole flat buffer); ranks sharing one GPU (rehearsals) split the workgroups, since every
+        # workgroup waits at the barriers for the same-index workgroup of every peer
+        share = max(1, -(-int(os.environ.get("LOCAL_WORLD_SIZE", world_size)) // max(1, ndev)))
+        self._comm_blocks = 512 if share == 1 else max(32, 128 // share)
         # the training forward (conv12_fwd) reads its raw images from xraw, which the previous step's
         # finalizer (wgrad apply mode, the SGD launch or the xGMI+SGD kernel) filled with the next
         # step's rows -- one image load instead of index load -> image load at the head of the step;
@@ -707,7 +715,7 @@ class FusedCifarEngine:
         seg[0]()
         n = self.master.numel()
         if self.comm_sgd:           # (xGMI: the whole step is one graph, seg is never a replay list)
-            self.xgmi.all_reduce_sgd(self._sgd_args(mode=2))
+            self.xgmi.all_reduce_sgd(self._sgd_args(mode=2), blocks=self._comm_blocks)
             return
         if self.xgmi is not None:
             self.xgmi.all_reduce(0, n)

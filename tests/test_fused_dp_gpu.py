@@ -228,8 +228,8 @@ def test_xgmi_sgd_epilogue_is_bit_identical(B, comm_dtype):
     x, y = _data()
     kw = dict(device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dp_force=True, allreduce="xgmi",
               dp_schedule="serial", comm_dtype=comm_dtype)
-    fused = FusedCifarEngine(B, x, y, **kw)
-    ref = FusedCifarEngine(B, x, y, **kw, variant={"comm_sgd": False})
+    fused = FusedCifarEngine(B, x, y, **kw, variant={"comm_sgd": True})
+    ref = FusedCifarEngine(B, x, y, **kw)
     single = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False)
     assert fused.comm_sgd and not ref.comm_sgd and fused.comm_info["allreduce"] == "xgmi"
     for eng in (fused, ref, single):

@@ -471,6 +471,8 @@ def test_xraw_prefetch_is_bit_identical(B):
     assert pre.global_step() == ref.global_step() == 14
     assert torch.isfinite(ref.master).all()
     assert torch.equal(pre.master, ref.master)
-    assert torch.equal(pre.xraw, ref.xraw)
+    # the prefetching engine's xraw already holds the NEXT step's images (its bidx rows)
+    assert torch.equal(pre.xraw, pre.data[pre.bidx.long()].view(pre.B, 3072))
+    assert torch.equal(pre.bidx, ref.bidx)
     for s in (9, 14):
         assert pre.read_stats(s) == ref.read_stats(s), s

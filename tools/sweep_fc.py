@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 import dmlc  # noqa: E402,F401
-from dmlc.engine.fused import FusedCifarEngine, head_rows  # noqa: E402
+from dmlc.engine.fused import FusedCifarEngine, head_rows  # noqa: E402  (head_rows: the three-launch head)
 
 
 def main():
