@@ -441,9 +441,11 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
       const float4 gv = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
       float4 v = R.m[u];
       v.x -= f * gv.x; v.y -= f * gv.y; v.z -= f * gv.z; v.w -= f * gv.w;
-      const f32x4 vo = {v.x, v.y, v.z, v.w};
-      st_maybe_nt<kNtX>(reinterpret_cast<f32x4*>(a.gw1 + q), vo);
-      st_maybe_nt<kNtX>(reinterpret_cast<bf16x4*>(S + q), pack4(v.x, v.y, v.z, v.w));
+      // write-through (sc1): 3.5 MB of master + 1.8 MB of shadow per step would otherwise sit dirty
+      // in the L2s for the kernel boundary's write-back (common.h st_out16); 77.7-78.4 vs 79.0-79.3
+      // us/step at B=256 with nt stores (profiles/r5_fc1_epilogue_wt_ab.txt)
+      st_out16(a.gw1, (uint32_t)(q * 4), __builtin_bit_cast(uint4, make_float4(v.x, v.y, v.z, v.w)));
+      st_out8(S, (uint32_t)(q * 2), __builtin_bit_cast(uint2, pack4(v.x, v.y, v.z, v.w)));
     }
     return;
   }
