@@ -188,24 +188,36 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
     load(b + G < last ? b + G : last);
     lds_barrier();
     if (b == b0) DMLC_STAMP(DMLC_TK_W2, 1);
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
+    // k-step s+1's fragments are read into the other register set BEFORE k-step s's MFMAs issue,
+    // so each k-step's LDS latency hides behind the previous one's MFMAs (as conv2_core): MFMA
+    // phase 15.5 -> 14.3 us, 77.8-78.2 -> 76.8-77.1 us/step at B=256 (profiles/r5_w2_kpipe_ab.txt)
+    bf16x8 BF[2][4], AF[2][4];
+    auto frags = [&](int s, bf16x8 (&bf)[4], bf16x8 (&af)[4]) __attribute__((always_inline)) {
       const int rA = 32 * s + 8 * g + q, rB = rA + 4;
-      bf16x8 bf[4];
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
         bf[ct] = tr_frag(dyt + rA * W2_LD + w2_dy_col(rA, 16 * ct + 4 * p), dyt + rB * W2_LD + w2_dy_col(rB, 16 * ct + 4 * p));
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const bf16x8 af = tr_frag(xt + xa[s] + toff[j], xt + xb[s] + toff[j]);
+      for (int j = 0; j < 3; ++j) af[j] = tr_frag(xt + xa[s] + toff[j], xt + xb[s] + toff[j]);
+      if (w < 4) af[3] = tr_frag(xt + xa[s] + T24, xt + xb[s] + T24);
+    };
+    frags(0, BF[0], AF[0]);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[4 * j + ct] = mfma16(af, bf[ct], acc[4 * j + ct]);
-      }
+    for (int s = 0; s < 5; ++s) {
+      const int cur = s & 1;
+      wait_lds();
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < 5) frags(s + 1, BF[cur ^ 1], AF[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[4 * j + ct] = mfma16(AF[cur][j], BF[cur][ct], acc[4 * j + ct]);
       if (w < 4) {                             // tap 24 x co tile w
-        const bf16x8 af = tr_frag(xt + xa[s] + T24, xt + xb[s] + T24);
-        const bf16x8 bw = w == 0 ? bf[0] : w == 1 ? bf[1] : w == 2 ? bf[2] : bf[3];
-        acc[12] = mfma16(af, bw, acc[12]);
+        const bf16x8 bw = w == 0 ? BF[cur][0] : w == 1 ? BF[cur][1] : w == 2 ? BF[cur][2] : BF[cur][3];
+        acc[12] = mfma16(AF[cur][3], bw, acc[12]);
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (b == b0) DMLC_STAMP(DMLC_TK_W2, 4);
   }
