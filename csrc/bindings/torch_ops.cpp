@@ -31,7 +31,7 @@ void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   const int64_t B = out.size(0);
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
-  check(w1f, "w1f", at::kBFloat16, {64, 160});
+  check(w1f, "w1f", at::kBFloat16, {64, 96});
   check_numel(b1, "b1", at::kFloat, 64);
   check(out, "out", at::kBFloat16, {B, 12, 12, 64});
   check(am, "am", at::kByte, {B, 12, 12, 64});
@@ -91,7 +91,7 @@ void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tenso
   TORCH_CHECK(!xraw_in || xraw.has_value(), "conv12_fwd: xraw_in needs the prefetched images");
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
-  check(w1f, "w1f", at::kBFloat16, {64, 160});
+  check(w1f, "w1f", at::kBFloat16, {64, 96});
   check_numel(b1, "b1", at::kFloat, 64);
   check(p1, "p1", at::kBFloat16, {B, 12, 12, 64});
   check(am1, "am1", at::kByte, {B, 12, 12, 64});
@@ -152,7 +152,7 @@ void conv1_fwd_split(const Tensor& data, const Tensor& idx, const c10::optional<
   TORCH_CHECK(nsplit == 2 || nsplit == 4, "conv1 split must be 2 or 4");
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
-  check(w1f, "w1f", at::kBFloat16, {64, 160});
+  check(w1f, "w1f", at::kBFloat16, {64, 96});
   check_numel(b1, "b1", at::kFloat, 64);
   check(out, "out", at::kBFloat16, {B, 12, 12, 64});
   check(am, "am", at::kByte, {B, 12, 12, 64});
@@ -516,7 +516,7 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
   TORCH_CHECK(loss_part.numel() >= 1, "loss partials missing");
   const int64_t B = batch;
   TORCH_CHECK(B >= 1 && B <= 4 * loss_part.numel(), "sgd: batch (valid rows) exceeds the head's rows");
-  check(w1f, "w1f", at::kBFloat16, {64, 160});
+  check(w1f, "w1f", at::kBFloat16, {64, 96});
   check(w2f, "w2f", at::kBFloat16, {64, 1600});
   check(w2d, "w2d", at::kBFloat16, {64, 1600});
   check(fc1n, "fc1n", at::kBFloat16, {2, 2304, 384});          // step-parity double buffer

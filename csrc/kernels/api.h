@@ -36,7 +36,7 @@ struct DmlcConv1FwdArgs {
   const uint8_t* data;      // [N][32][32][3] uint8 (NHWC)
   DmlcIndexSrc src;
   int B, cy, cx;            // crop offsets (center crop = 4,4)
-  const void* w;            // bf16 [64][160]  (k = kh*32 + kw*4 + ci, zero padded)
+  const void* w;            // bf16 [64][96]  (k = kh*16 + kw*3 + ci, zero padded)
   const float* bias;        // [64]
   void* out;                // bf16 [B][12][12][64]
   uint8_t* am;              // [B][12][12][64] argmax (0..8) in the pool window, 255 = no gradient

@@ -13,8 +13,9 @@
 //     (255 encodes "pooled <= 0", i.e. the ReLU mask), so the backward never re-reads activations;
 //   * conv1 gathers its uint8 input directly from the device-resident dataset (index list + center
 //     crop), so the input pipeline (N1-N3) costs no extra launch;
-//   * conv1's K=75 (5x5x3) is laid out as k = kh*32 + kw*4 + ci (kw padded to 8, ci to 4) so that a
-//     k-step of 32 is one kernel row and every fragment is 16 contiguous bytes of the LDS image;
+//   * conv1's K=75 (5x5x3) is laid out as k = kh*16 + kw*3 + ci (K 80, padded to 96 = 3 k-steps):
+//     the LDS input holds 5-tap row windows (conv_common.h stage_conv1_input), so every fragment is
+//     16 contiguous bytes of it (r4 padded K to 160: kw to 8, ci to 4 -- 40 % of those MFMAs were zeros);
 //   * backward: pool/ReLU backward is a *gather* (each input pixel sums the <=4 windows whose argmax
 //     points at it: deterministic, no atomics) fused into the staging of the dgrad/wgrad operands;
 //     weight gradients read both operands from NHWC LDS images with ds_read_b64_tr_b16 (hardware
@@ -26,22 +27,21 @@ namespace dmlc {
 
 
 // conv1 implicit GEMM of one wave: co tiles 2cp, 2cp+1 (weights wa in registers) x pixel tiles
-// 9pq .. 9pq+8.  Software-pipelined: the 5 B fragments of pixel tile t+1 are read from LDS while tile
-// t's 10 MFMAs run (wait_lds retires tile t's reads first; see common.h).
-DEV void conv1_mfma(const bf16* xin, const bf16x8 (&wa)[2][5], f32x4 (&acc)[2][9], int pq, int g, int li) {
-  auto load_tile = [&](int t, bf16x8 (&bx)[5]) {
-    const int px = (pq * 9 + t) * 16 + li;
-    const int y = px / 24, x = px - (px / 24) * 24;
-    const bf16* base = xin + (y * 32 + x + 2 * g) * 4;   // k = 8g..8g+7 -> kw = 2g,2g+1 ; ci 0..3
+// 9pq .. 9pq+8.  Software-pipelined: the 3 B fragments of pixel tile t+1 are read from LDS while tile
+// t's 6 MFMAs run (wait_lds retires tile t's reads first; see common.h).
+// the wave's weight fragments: rows co0 + li (+16 for h = 1) of the [64][96] shadow
+DEV void conv1_wfrags(const void* w, int co0, int g, int li, bf16x8 (&wa)[2][3]) {
+  const bf16* W = reinterpret_cast<const bf16*>(w) + (co0 + li) * C1_K + 8 * g;
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh) {
-      const bf16* p = base + kh * 128;
-      bx[kh] = cat44(*reinterpret_cast<const bf16x4*>(p), *reinterpret_cast<const bf16x4*>(p + 4));
-    }
-  };
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int s = 0; s < 3; ++s) wa[h][s] = glb_b128(W + h * 16 * C1_K + 32 * s);
+}
+DEV void conv1_mfma(const bf16* xin, const bf16x8 (&wa)[2][3], f32x4 (&acc)[2][9], int pq, int g, int li) {
+  auto load_tile = [&](int t, bf16x8 (&bx)[3]) { conv1_frag_tile(xin, (pq * 9 + t) * 16 + li, g, bx); };
 #pragma unroll
   for (int t = 0; t < 9; ++t) { acc[0][t] = zero4(); acc[1][t] = zero4(); }
-  bf16x8 BX[2][5];
+  bf16x8 BX[2][3];
   load_tile(0, BX[0]);
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
@@ -51,9 +51,9 @@ DEV void conv1_mfma(const bf16* xin, const bf16x8 (&wa)[2][5], f32x4 (&acc)[2][9
     if (t + 1 < 9) load_tile(t + 1, BX[cur ^ 1]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh) {
-      acc[0][t] = mfma16(wa[0][kh], BX[cur][kh], acc[0][t]);
-      acc[1][t] = mfma16(wa[1][kh], BX[cur][kh], acc[1][t]);
+    for (int s = 0; s < 3; ++s) {
+      acc[0][t] = mfma16(wa[0][s], BX[cur][s], acc[0][t]);
+      acc[1][t] = mfma16(wa[1][s], BX[cur][s], acc[1][t]);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -69,19 +69,15 @@ __global__ __launch_bounds__(NT, 1) void k_conv1_fwd(DmlcConv1FwdArgs a) {
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 
   const int img = batch_index(a.src, a.B, b);
-  uint8_t* raw = reinterpret_cast<uint8_t*>(cout);          // the conv output region is free until the epilogue
+  uint8_t* raw = reinterpret_cast<uint8_t*>(cout) + 16;     // the conv output region is free until the epilogue
   stage_conv1_raw(raw, a.data + (size_t)img * 3072, a.xraw ? a.xraw + (size_t)b * 3072 : nullptr, tid);
   __syncthreads();
   stage_conv1_input(xin, raw, a.cy, a.cx, tid);
 
-  // A operand: weights [64 co][160 k]; this wave owns co tiles 2cp, 2cp+1 (32 channels) and the
+  // A operand: weights [64 co][96 k]; this wave owns co tiles 2cp, 2cp+1 (32 channels) and the
   // pixel tiles 9pq .. 9pq+8 (of 36): every B fragment read from LDS feeds two MFMAs.
-  const bf16* W = reinterpret_cast<const bf16*>(a.w) + (32 * cp + li) * 160 + 8 * g;
-  bf16x8 wa[2][5];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh) wa[h][kh] = glb_b128(W + h * 16 * 160 + 32 * kh);
+  bf16x8 wa[2][3];
+  conv1_wfrags(a.w, 32 * cp, g, li, wa);
   float b4[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -170,19 +166,19 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad(DmlcConv2DgradArgs a) {
 // conv1 -> pool1 -> conv2 -> pool2 of one image in ONE launch (bf16 path): the images are
 // independent, so the pool1 output goes straight into conv2's zero-padded LDS input instead of
 // round-tripping through global memory and a second launch (p1 / am1 are still written for the
-// backward).  LDS: [0, 80 KB) conv1 input + output, then conv2's two weight-slice buffers;
-// [80, 112 KB) conv2's padded input; [112, 130 KB) conv2's output.
+// backward).  LDS: [0, 80 KB) conv1 output (72 KB), then conv2's two weight-slice buffers;
+// [80, 112 KB) conv2's padded input; [112, 130 KB) conv2's output; [130, 151 KB) conv1's input.
 // Kernel row 0 of the conv2 weights is loaded into registers at entry and stored into the first
 // slice buffer after pool1: its L2 latency hides behind conv1 instead of opening the conv2 core
 // (~1 us of the core's first row, r3 phase stamps).
 constexpr size_t C12_WS = 0, C12_XIN2 = 81920, C12_OUT2 = C12_XIN2 + C2_XIN * 2;
-constexpr size_t C12_LDS = C12_OUT2 + C2_OUT * 2;
-static_assert((C1_XIN + C1_OUT) * 2 <= C12_XIN2 && WS_BYTES <= C12_XIN2, "conv12 LDS map");
+constexpr size_t C12_XIN1 = C12_OUT2 + C2_OUT * 2, C12_LDS = C12_XIN1 + C1_XIN * 2;
+static_assert(C1_OUT * 2 <= C12_XIN2 && WS_BYTES <= C12_XIN2 && C12_LDS <= 160 * 1024, "conv12 LDS map");
 
 __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcConv2FwdArgs a2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* xin = reinterpret_cast<bf16*>(smem);
-  bf16* cout = xin + C1_XIN;
+  bf16* xin = reinterpret_cast<bf16*>(smem + C12_XIN1);
+  bf16* cout = reinterpret_cast<bf16*>(smem);
   bf16* xin2 = reinterpret_cast<bf16*>(smem + C12_XIN2);
   bf16* cout2 = reinterpret_cast<bf16*>(smem + C12_OUT2);
   bf16* ws = reinterpret_cast<bf16*>(smem + C12_WS);
@@ -191,18 +187,14 @@ __global__ __launch_bounds__(NT, 1) void k_conv12_fwd(DmlcConv1FwdArgs a1, DmlcC
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 
   // conv1 weights / biases first: in flight together with the index -> image chain
-  const bf16* W = reinterpret_cast<const bf16*>(a1.w) + (32 * cp + li) * 160 + 8 * g;
-  bf16x8 wa[2][5];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh) wa[h][kh] = glb_b128(W + h * 16 * 160 + 32 * kh);
+  bf16x8 wa[2][3];
+  conv1_wfrags(a1.w, 32 * cp, g, li, wa);
   float b4[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int i = 0; i < 4; ++i) b4[h][i] = a1.bias[32 * cp + 16 * h + 4 * g + i];
-  uint8_t* raw = reinterpret_cast<uint8_t*>(cout);          // the conv1 output region is free until its epilogue
+  uint8_t* raw = reinterpret_cast<uint8_t*>(cout) + 16;     // the conv1 output region is free until its epilogue
   if (a1.xraw_in) {                            // prefetched by the previous step: one load, no index hop
     stage_conv1_raw(raw, a1.xraw + (size_t)b * 3072, nullptr, tid);
   } else {

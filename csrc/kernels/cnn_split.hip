@@ -99,7 +99,7 @@ template <int NCO>
 __global__ __launch_bounds__(SP_NT, 4) void k_conv1_fwd_split(DmlcConv1FwdArgs a) {
   constexpr int S = 64 / NCO, CT = NCO / 16, CH = NCO / 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* xin = reinterpret_cast<bf16*>(smem);                 // [28][32][4]
+  bf16* xin = reinterpret_cast<bf16*>(smem);                 // [28][24][16] row windows
   bf16* img = xin + C1_XIN;                                  // [576][NCO] (swzc)
   int b, h;
   split_index<S>(blockIdx.x, b, h);
@@ -108,15 +108,15 @@ __global__ __launch_bounds__(SP_NT, 4) void k_conv1_fwd_split(DmlcConv1FwdArgs a
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
 
   const int row = batch_index(a.src, a.B, b);
-  uint8_t* raw = reinterpret_cast<uint8_t*>(img);            // free until the epilogue
+  uint8_t* raw = reinterpret_cast<uint8_t*>(img) + 16;       // free until the epilogue (16 B of halo slack)
   stage_conv1_raw(raw, a.data + (size_t)row * 3072, (a.xraw && h == 0) ? a.xraw + (size_t)b * 3072 : nullptr, tid);
   // this slice's weights [co0 + 16 ct + li][k = 32 kh + 8 g ..] and biases, in flight with the image
-  const bf16* W = reinterpret_cast<const bf16*>(a.w) + (co0 + li) * 160 + 8 * g;
-  bf16x8 wa[CT][5];
+  const bf16* W = reinterpret_cast<const bf16*>(a.w) + (co0 + li) * C1_K + 8 * g;
+  bf16x8 wa[CT][3];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh) wa[ct][kh] = glb_b128(W + ct * 16 * 160 + 32 * kh);
+    for (int s = 0; s < 3; ++s) wa[ct][s] = glb_b128(W + ct * 16 * C1_K + 32 * s);
   float b4[CT][4];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
@@ -128,17 +128,8 @@ __global__ __launch_bounds__(SP_NT, 4) void k_conv1_fwd_split(DmlcConv1FwdArgs a
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 1);
 
   // pixel tiles w, w+8, ... (< 36): 5 for waves 0-3, 4 for waves 4-7 (waves w, w+4 share a SIMD)
-  auto load_tile = [&](int t, bf16x8 (&bx)[5]) {
-    const int px = t * 16 + li;
-    const int y = px / 24, x = px - y * 24;
-    const bf16* base = xin + (y * 32 + x + 2 * g) * 4;
-#pragma unroll
-    for (int kh = 0; kh < 5; ++kh) {
-      const bf16* p = base + kh * 128;
-      bx[kh] = cat44(*reinterpret_cast<const bf16x4*>(p), *reinterpret_cast<const bf16x4*>(p + 4));
-    }
-  };
-  bf16x8 BX[2][5];
+  auto load_tile = [&](int t, bf16x8 (&bx)[3]) { conv1_frag_tile(xin, t * 16 + li, g, bx); };
+  bf16x8 BX[2][3];
   load_tile(w, BX[0]);
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -153,9 +144,9 @@ __global__ __launch_bounds__(SP_NT, 4) void k_conv1_fwd_split(DmlcConv1FwdArgs a
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[ct] = zero4();
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh)
+    for (int s = 0; s < 3; ++s)
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wa[ct][kh], BX[cur][kh], acc[ct]);
+      for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma16(wa[ct][s], BX[cur][s], acc[ct]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) store_relu_c<CH>(img, t * 16 + li, 16 * ct + 4 * g, acc[ct], b4[ct]);

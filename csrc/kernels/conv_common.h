@@ -74,9 +74,20 @@ struct PrefetchAll {
   }
 };
 
-// conv1 input image: 24x24 crop of the uint8 NHWC image at (cy,cx), zero halo of 2, stored as
-// [28 rows][32 cols][4 ch] bf16 (col 28..31 and ch 3 zero).  Pixel (iy,ix) -> (iy+2, ix+2).
-constexpr int C1_XIN = 28 * 32 * 4;        // 3584 bf16
+DEV bf16x8 to_bf16x8(const float (&v)[8]) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
+  return o;
+}
+
+// conv1 input as 5-tap row windows: the 24x24 crop of the uint8 NHWC image at (cy,cx) with a zero
+// halo of 2, stored as [28 padded rows r][24 output columns x][16] bf16 where element j = kw*3 + ci
+// (j < 15; j = 15 is zero) is input pixel (r - 2, x + kw - 2), channel ci.  An MFMA B fragment (8
+// consecutive k of the K = 80 layout k = kh*16 + kw*3 + ci) is then ONE 16-B read at row y + kh,
+// half (k >> 3) & 1 -- K padded to 96 (3 k-steps) instead of 160 (5; kw padded to 8 and ci to 4).
+constexpr int C1_XIN = 28 * 24 * 16;       // 10752 bf16
+constexpr int C1_K = 96;                   // conv1 weight shadow row: [64 co][96], k = kh*16 + kw*3 + ci
 constexpr int C1_OUT = 576 * 64;           // 36864 bf16
 
 // The whole 3 KB uint8 image in ONE 16-byte load per thread (threads 0..191) into LDS (`raw`), and
@@ -90,15 +101,38 @@ DEV void stage_conv1_raw(uint8_t* raw, const uint8_t* src, uint8_t* xraw, int ti
   }
 }
 
+// (elements j of a window are consecutive bytes of the raw NHWC row: pixel x + kw - 2, channel ci
+// sits at byte (x - 2) * 3 + j of the crop row, so a half window is the 8 raw bytes at `off`, read
+// as two aligned 8-B words and funnel-shifted -- 8 byte reads per half measured ~0.9 us slower.
+// raw needs 8 readable bytes before it (the left halo reads them and masks them out) and after.
 DEV void stage_conv1_input(bf16* xin, const uint8_t* raw, int cy, int cx, int tid) {
-  for (int p = tid; p < 28 * 32; p += NT) {
-    const int r = p >> 5, c = p & 31;
-    const int iy = r - 2, ix = c - 2;
-    const bool ok = iy >= 0 && iy < 24 && ix >= 0 && ix < 24;
-    const uint8_t* s = raw + (ok ? ((cy + iy) * 32 + (cx + ix)) * 3 : 0);
-    const float c0 = s[0], c1 = s[1], c2 = s[2];
-    *reinterpret_cast<bf16x4*>(xin + p * 4) = ok ? pack4(c0, c1, c2, 0.f) : pack4(0.f, 0.f, 0.f, 0.f);
+  const int h = tid & 1;                       // NT is even: every task of a thread has the same half
+  for (int t = tid; t < 28 * 24 * 2; t += NT) {
+    const int px = t >> 1, r = px / 24, x = px - r * 24, iy = r - 2;
+    const bool rok = iy >= 0 && iy < 24;
+    const int off = rok ? ((cy + iy) * 32 + cx + x - 2) * 3 + 8 * h : 8;
+    const int a0 = off & ~7, sh = (off & 7) * 8;
+    const uint64_t lo = *reinterpret_cast<const uint64_t*>(raw + a0);
+    const uint64_t hi = *reinterpret_cast<const uint64_t*>(raw + a0 + 8);
+    const uint64_t v = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = 8 * h + e, ix = x + j / 3 - 2;
+      f[e] = rok && j < 15 && ix >= 0 && ix < 24 ? (float)((uint32_t)(v >> (8 * e)) & 0xffu) : 0.f;
+    }
+    *reinterpret_cast<bf16x8*>(xin + px * 16 + 8 * h) = to_bf16x8(f);
   }
+}
+
+// conv1 B fragments of pixel px (lane li of its tile): k-step s, lane group g holds k = 32s + 8g ..
+// +7 = kernel row 2s + (g >> 1), window half g & 1; the pad rows k >= 80 (s = 2, g >= 2) re-read
+// row 4 against zero weights.
+DEV void conv1_frag_tile(const bf16* xin, int px, int g, bf16x8 (&bx)[3]) {
+  const int y = px / 24, x = px - y * 24;
+  const bf16* base = xin + (y * 24 + x) * 16 + 8 * (g & 1);
+#pragma unroll
+  for (int s = 0; s < 3; ++s) bx[s] = lds_b128(base + min(2 * s + (g >> 1), 4) * 24 * 16);
 }
 
 // conv2 input / output LDS images: padded [16*16][64] (swzpad) and [144][64] bf16
@@ -151,13 +185,6 @@ DEV void pool_bwd_2x2(const bf16* dp, const uint8_t* am, int py, int px, int c, 
     o[1][j] = (bw == 1 ? fw : 0.f) + (bu == 7 ? fu : 0.f);
     o[0][j] = ((bw == 0 ? fw : 0.f) + (bl == 2 ? fl : 0.f)) + ((bu == 6 ? fu : 0.f) + (bul == 8 ? ful : 0.f));
   }
-}
-
-DEV bf16x8 to_bf16x8(const float (&v)[8]) {
-  bf16x8 o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (bf16)v[j];
-  return o;
 }
 
 // Reduce per-thread channel sums (thread's chunk = tid & 7) over the workgroup: red[waves][64] partials.

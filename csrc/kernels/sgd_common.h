@@ -102,16 +102,16 @@ DEV void conv2_shadow4(const DmlcSgdArgs& a, int krow, int co, const float4& w) 
   }
 }
 
-// bf16 forward shadow w1f[co][160] (k = kh*32 + kw*4 + ci) of 4 updated conv1 weights of HWIO row
+// bf16 forward shadow w1f[co][96] (k = kh*16 + kw*3 + ci; conv_common.h C1_K) of 4 updated conv1 weights of HWIO row
 // `row` = (kh*5+kw)*3 + ci, channels co..co+3
 DEV void conv1_shadow4(const DmlcSgdArgs& a, int row, int co, const float4& w) {
   const int ci = row % 3, khw = row / 3, kh = khw / 5, kw = khw - kh * 5;
-  const int k = kh * 32 + kw * 4 + ci;
+  const int k = kh * 16 + kw * 3 + ci;
   bf16* w1f = reinterpret_cast<bf16*>(a.w1f);
-  w1f[(co + 0) * 160 + k] = (bf16)w.x;
-  w1f[(co + 1) * 160 + k] = (bf16)w.y;
-  w1f[(co + 2) * 160 + k] = (bf16)w.z;
-  w1f[(co + 3) * 160 + k] = (bf16)w.w;
+  w1f[(co + 0) * 96 + k] = (bf16)w.x;
+  w1f[(co + 1) * 96 + k] = (bf16)w.y;
+  w1f[(co + 2) * 96 + k] = (bf16)w.z;
+  w1f[(co + 3) * 96 + k] = (bf16)w.w;
 }
 
 // conv biases: which 0 -> conv1 bias (g1 group partials), 1 -> conv2 bias (g2 group partials).

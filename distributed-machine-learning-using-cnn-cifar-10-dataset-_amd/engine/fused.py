@@ -193,7 +193,7 @@ class FusedCifarEngine:
             self.grad = torch.zeros_like(self.master)
         bf = torch.bfloat16
         z = lambda *s, dt=bf: torch.zeros(*s, dtype=dt, device=dev)
-        self.w1f, self.w2f, self.w2d = z(64, 160), z(64, 1600), z(64, 1600)
+        self.w1f, self.w2f, self.w2d = z(64, 96), z(64, 1600), z(64, 1600)
         # fc1's bf16 shadow is double-buffered by step parity ([2][2304][384]): the kernels of step s
         # read fc1n[s & 1] and the update writes fc1n[(s + 1) & 1], so at N=1 the dW1 GEMM can apply
         # the fc1 update in its epilogue while the dp2 problem of the same launch still reads the
