@@ -54,38 +54,16 @@ DEV void pool_emit_c(const bf16* img, bf16* out, uint8_t* am, int c0, int tid) {
   for (int task = tid; task < HO * HO * CH; task += T) {
     const int q = task / CH, c = task - q * CH;
     const int py = q / HO, px = q - py * HO;
-    uint32_t key[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) key[j] = 0;
-    // branch-free (see pool_emit): all 9 taps loaded back to back, padding taps masked to key 0
+    // branch-free (see pool_emit): all 9 taps loaded back to back
     uint4 v[9];
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
       const int y = min(2 * py + d / 3, H - 1), x = min(2 * px + d % 3, H - 1);
       v[d] = *reinterpret_cast<const uint4*>(img + swzc<CH>(y * H + x, c));
     }
-#pragma unroll
-    for (int d = 0; d < 9; ++d) {
-      const bool ok = (d / 3 < 2 || 2 * py + 2 < H) && (d % 3 < 2 || 2 * px + 2 < H);
-      const uint32_t m = ok ? 0xffffffffu : 0u, tag = 15 - d;
-      const uint32_t wv[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        key[2 * i] = max(key[2 * i], (((wv[i] << 16) & 0x7fff0000u) | tag) & m);
-        key[2 * i + 1] = max(key[2 * i + 1], ((wv[i] & 0x7fff0000u) | tag) & m);
-      }
-    }
     uint4 o;
-    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
-    uint32_t alo = 0, ahi = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ow[i] = (key[2 * i] >> 16) | (key[2 * i + 1] & 0xffff0000u);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t arg = (key[j] >> 16) ? 15 - (key[j] & 15) : 255;
-      if (j < 4) alo |= arg << (8 * j);
-      else ahi |= arg << (8 * (j - 4));
-    }
+    uint32_t alo, ahi, bmax = 0;
+    pool_window(v, o, alo, ahi, bmax);
     st_maybe_nt<kNtX>(reinterpret_cast<uint4*>(out + q * 64 + c0 + c * 8), o);
     st_maybe_nt<kNtX>(reinterpret_cast<uint2*>(am + q * 64 + c0 + c * 8), make_uint2(alo, ahi));
   }

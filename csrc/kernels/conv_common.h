@@ -212,11 +212,46 @@ DEV void store_relu_tile(bf16* cout, int px, int co_base, const f32x4& acc, cons
   *reinterpret_cast<bf16x4*>(cout + swz128(px, chunk) + half * 4) = v;
 }
 
+// The 3x3 window max + first argmax of 8 channels from the window's 9 taps (16-B chunks of 8 bf16).
+// Each candidate is a signed 32-bit key (bits << 16 | 15 - d): post-ReLU values order like their
+// bit patterns, a -0.0 (sign bit set) ranks below the initial key 0, and one integer max per
+// element and tap keeps value AND first argmax (ties -> smallest d).  A tap in the bottom / right
+// TF-SAME padding is read clamped to the last row / column, i.e. it repeats tap d-3 / d-1 (and
+// d-4) with a smaller tag, so it can never win and needs no mask.  (r4 masked the sign bit and the
+// padding taps: ~4 VALU per element and tap; this is 1.5.)  Output bits / argmax bytes (255 =
+// "pooled <= 0", the ReLU mask for the backward).
+DEV void pool_window(const uint4 (&v)[9], uint4& o, uint32_t& alo, uint32_t& ahi, uint32_t& bmax) {
+  int key[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) key[j] = 0;
+#pragma unroll
+  for (int d = 0; d < 9; ++d) {
+    const uint32_t tag = 15 - d;
+    const uint32_t wv[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      key[2 * i] = max(key[2 * i], (int)((wv[i] << 16) | tag));
+      key[2 * i + 1] = max(key[2 * i + 1], (int)((wv[i] & 0xffff0000u) | tag));
+    }
+  }
+  uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ow[i] = ((uint32_t)key[2 * i] >> 16) | ((uint32_t)key[2 * i + 1] & 0xffff0000u);
+  alo = 0;
+  ahi = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t hv = (uint32_t)key[j] >> 16;
+    bmax = max(bmax, hv);
+    const uint32_t arg = hv ? 15 - (key[j] & 15) : 255;
+    if (j < 4) alo |= arg << (8 * j);
+    else ahi |= arg << (8 * (j - 4));
+  }
+}
+
 // TF-SAME 3x3/2 max-pool over an LDS image [H*W][64] (swizzled) -> global out [HO*WO][64] bf16 +
 // argmax bytes.  Padding is bottom/right only (in = 2*out), padded cells never win.
-// The inputs are post-ReLU (>= 0), so bf16 bit patterns order like their values: each candidate is a
-// 32-bit key (bits << 16 | 15 - d) and one integer max per element keeps value AND first argmax
-// (ties -> smallest d, like a strict '>' scan).  Sign bits are masked so a -0.0 ranks as 0.
+// The window max / argmax: pool_window.
 // pad_lds (optional): also writes the pooled image into an LDS [(HO+4) x (HO+4)][64] swizzled image
 // at offset (2, 2) -- the zero-padded input of the next 5x5 conv (fused conv1 -> conv2 forward).
 template <int H>
@@ -228,45 +263,19 @@ DEV void pool_emit(const bf16* cout, bf16* out, uint8_t* am, int tid, uint32_t* 
   for (int task = tid; task < HO * HO * 8; task += NT) {
     const int q = task >> 3, c = task & 7;
     const int py = q / HO, px = q - py * HO;
-    uint32_t key[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) key[j] = 0;
     // Branch-free: all 9 taps are loaded (a tap in the bottom / right TF-SAME padding reads the last
-    // row / column instead and is masked to key 0), so the 9 LDS reads issue back to back and the
-    // task pays one LDS latency.  (With `if (tap valid) load` -- a divergent condition -- hipcc put
-    // each load in its own EXEC-masked block with its own lgkmcnt(0).)  A masked tap contributes key
-    // 0, which never changes the result: if the window's maximum VALUE is 0 the output is 0 with
-    // argmax 255 anyway.
+    // row / column instead: see pool_window), so the 9 LDS reads issue back to back and the task
+    // pays one LDS latency.  (With `if (tap valid) load` -- a divergent condition -- hipcc put each
+    // load in its own EXEC-masked block with its own lgkmcnt(0).)
     uint4 v[9];
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
       const int y = min(2 * py + d / 3, H - 1), x = min(2 * px + d % 3, H - 1);
       v[d] = *reinterpret_cast<const uint4*>(cout + swz128(y * H + x, c));
     }
-#pragma unroll
-    for (int d = 0; d < 9; ++d) {
-      const bool ok = (d / 3 < 2 || 2 * py + 2 < H) && (d % 3 < 2 || 2 * px + 2 < H);
-      const uint32_t m = ok ? 0xffffffffu : 0u, tag = 15 - d;
-      const uint32_t wv[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        key[2 * i] = max(key[2 * i], (((wv[i] << 16) & 0x7fff0000u) | tag) & m);
-        key[2 * i + 1] = max(key[2 * i + 1], ((wv[i] & 0x7fff0000u) | tag) & m);
-      }
-    }
     uint4 o;
-    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
-    uint32_t alo = 0, ahi = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ow[i] = (key[2 * i] >> 16) | (key[2 * i + 1] & 0xffff0000u);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bmax = max(bmax, key[j] >> 16);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t arg = (key[j] >> 16) ? 15 - (key[j] & 15) : 255;
-      if (j < 4) alo |= arg << (8 * j);
-      else ahi |= arg << (8 * (j - 4));
-    }
+    uint32_t alo, ahi;
+    pool_window(v, o, alo, ahi, bmax);
     st_out16(out, (uint32_t)(q * 64 + c * 8) * 2, o);
     st_out8(am, (uint32_t)(q * 64 + c * 8), make_uint2(alo, ahi));
     if (pad_lds) *reinterpret_cast<uint4*>(pad_lds + swzpad((py + 2) * (HO + 4) + px + 2, c)) = o;
