@@ -103,3 +103,37 @@ def head_reads(off):            # (b) b128 row fragments, ideal 4; (f) tr column
 print("gemm k-major b128: KC_LD 136 ->", gemm_kmajor(136), " KC_LD 144 ->", gemm_kmajor(144))
 print("gemm m-major tr: MC_LD 72 ->", gemm_mmajor(lambda r, c: r * 72 + c), " swizzled 64 ->", gemm_mmajor(mswz))
 print("head fc2 (b128, tr): W2_LD 392 ->", head_reads(lambda r, c: r * 392 + c), " swizzled 384 ->", head_reads(w2swz))
+
+
+# --- max-pool reads of a conv output image (conv_common.h pool_emit) ------------------------------
+# r5: the conflict-free variant modelled here (rows px, px ^ 1 swapped for bit 1 of px + two pixels x 8
+# chunks per lane group) measured SLOWER on the GPU (pool1 2.44 -> 2.88 us, step +0.5 us,
+# profiles/r5_pool_swz_ab.txt): the pool is VALU-bound and the permuted lanes cost the stores their
+# contiguity, so the shipped pool keeps lane -> (lane >> 3, lane & 7) and swz128.
+def _pool_swz(p, c, swap):
+    q = p ^ ((p >> 1) & 1) if swap else p
+    return q * 64 + ((c ^ (q & 7)) << 3)
+
+
+_GI = {l: (G, i) for G, grp in enumerate(G128) for i, l in enumerate(grp)}
+
+
+def pool_reads(H, swap, grouped):
+    """LDS cycles per ds_read_b128 of the 9 tap reads; grouped: pool_emit's lane order (two pixels
+    x 8 chunks per lane group) instead of lane -> (lane >> 3, lane & 7)."""
+    HO, res = H // 2, []
+    for wv in range(HO * HO // 8):
+        for d in range(9):
+            addr = []
+            for l in range(64):
+                G, i = _GI[l]
+                ql, c = (2 * G + (i >> 3), i & 7) if grouped else (l >> 3, l & 7)
+                py, px = divmod(8 * wv + ql, HO)
+                y, x = min(2 * py + d // 3, H - 1), min(2 * px + d % 3, H - 1)
+                addr.append(2 * _pool_swz(y * H + x, c, swap))
+            res.append(cycles(addr))
+    return sum(res) / len(res)
+
+
+for H in (24, 12):
+    print(f"pool{1 if H == 24 else 2} reads: r4 {pool_reads(H, False, False):.1f}  swzpool + grouped lanes {pool_reads(H, True, True):.1f}")
