@@ -438,7 +438,7 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
   check_numel(gb2, "gb2", at::kFloat, 192);
   check_numel(gb3, "gb3", at::kFloat, 10);
   check_numel(step, "step", at::kLong, 1);
-  check_min(sync, "sync", at::kInt, 28 * 32);
+  check_min(sync, "sync", at::kInt, 212 * 32);   // fc_common.h SY_END
   check_min(err, "err", at::kInt, 1);
   TORCH_CHECK(sched.size() == 6, "fc_chain: sched = {lr0, decay, decay_steps, staircase, warmup, grad_scale}");
   if (nvalid < 0) nvalid = B;

@@ -20,8 +20,9 @@
 // bytes write-through (sc1 buffer stores), every storing wave drains (vmcnt(0)), the workgroup
 // barriers, ONE lane adds to a counter (agent-scope atomic); the consumer's one lane polls that
 // counter with relaxed atomic loads, the workgroup barriers, and EVERY load of handed-off bytes is an
-// sc1 buffer load.  Counters: one per 64-row tile for the fc1 partials (cntA) and for the head
-// outputs (cntB) plus a total; the last block to finish re-arms them (zero) for the next launch.
+// sc1 buffer load.  Counters (fc_common.h, each seam spread over several words that the consumer's
+// lanes poll side by side): the fc1 partials (cntA), the head outputs (cntB) and the dp2 tiles (cntD);
+// the last block to finish re-arms them (zero) for the next launch.
 // Every spin is bounded and sets the sticky error word (the engine's wgrad barrier error word) --
 // all 256 blocks must be co-resident (one per CU: ~150 KB of LDS each; host-checked).
 #include <string.h>
@@ -116,7 +117,7 @@ DEV void fwd_task(const DmlcFcArgs& a, int t, const FwdRegs& R, char* smem, int 
       st_sc1(out, (uint32_t)(((size_t)s * a.B + row) * 384 + 64 * nt + cc) * 4, v);
     }
   }
-  publish(cntA(a, mt), nullptr);
+  publish(cntA(a, mt, nt));
 }
 
 // =================================================================================================
@@ -188,7 +189,7 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
 
   // --- seam 1: every fc1 forward task of this 64-row tile
   DMLC_STAMP(DMLC_TK_HEAD, 1);
-  consume(cntA(a, mt), 6 * FC_S, a.err);
+  consume(seamA(a, mt), a.err);
   DMLC_STAMP(DMLC_TK_HEAD, 2);
   {
     const rsrc_t part = buf_rsrc(a.h1part);
@@ -332,7 +333,7 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
     else if (qq < 98) st16(rdl, (uint32_t)(b * 16 + 8 * (qq - 96)) * 2, *reinterpret_cast<const uint4*>(dls + rw * DL_LD + 8 * (qq - 96)));
     else st16(rdh1, (uint32_t)(b * 384 + 8 * (qq - 98)) * 2, *reinterpret_cast<const uint4*>(d1 + rw * 384 + 8 * (qq - 98)));
   }
-  publish(cntB(a, mt), cntBall(a));
+  publish(cntB(a, mt, hb & 3));
   DMLC_STAMP(DMLC_TK_HEAD, 5);
 }
 
@@ -394,18 +395,16 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a, DmlcConv2Dgrad
   if (tid == 0) {
     wait_vm_all();
     if (last_arrival(a.sync + 32 * 10, blk, FC_BLOCKS)) {
-      for (int m = 0; m < 4; ++m) {
-        __hip_atomic_store(cntA(a, m), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cntB(a, m), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cntD(a, epoch + 1, m), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __hip_atomic_store(cntBall(a), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int w = SY_A; w < SY_D; ++w)        // cntA, cntB
+        __hip_atomic_store(a.sync + 32 * w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int k = 0; k < 72; ++k)             // the other dp2 set
+        __hip_atomic_store(cntD(a, epoch + 1, 0, 0) + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(epochW(a), epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // the conv2 input gradient of image blk (dg.B = 0: a separate launch does it): its dp2 row tile
   // comes from this launch's dp2 tasks; everything else it reads was written by earlier launches
-  if (blk < dg.B) conv2_dgrad_image<true>(dg, blk, smem, cntD(a, epoch, blk >> 6), DP2_COL_TILES, a.err);
+  if (blk < dg.B) conv2_dgrad_image<true>(dg, blk, smem, seamD(a, epoch, blk >> 6), a.err);
   if (blk < H) DMLC_STAMP(DMLC_TK_HEAD, 7);
   else DMLC_STAMP(DMLC_TK_GEMM, 6);
 }

@@ -224,6 +224,28 @@ DEV bool last_arrival(unsigned int* tk, int blk, int nblk) {
   return true;
 }
 
+// A hand-off seam of n counters 128 B apart (p, p + 32, ...), each of which must reach `target`.
+// Many producers adding to ONE word serialise at the memory side (r5 phase stamps: ~2.4 us for the 48
+// arrivals on one fc1-forward tile counter), so a seam's arrivals are spread over several words and
+// the consumer's lanes 0..n-1 of wave 0 poll them side by side.  Bounded; on give-up the sticky error
+// word gets `errbit`.  Call with every lane of wave 0 (tid < 64); the caller then barriers.
+// (lane_target: this lane's word target, for seams whose words differ -- default s.target)
+struct Seam { unsigned* p; int n; unsigned target; };
+DEV void seam_wait(const Seam& s, int lane, unsigned* err, unsigned errbit, int lane_target = -1) {
+  const bool on = lane < s.n;
+  unsigned* q = s.p + 32 * (on ? lane : 0);
+  const unsigned t = lane_target >= 0 ? (unsigned)lane_target : s.target;
+  for (unsigned it = 0;; ++it) {
+    const bool ok = !on || __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= t;
+    if (__all(ok)) break;
+    if (it > (1u << 20)) {
+      if (lane == 0) __hip_atomic_fetch_or(err, errbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // 32-bit integer mixer (a bijective avalanche hash): the round function of the data-order Feistel
 // network below.  Host twin: dmlc/data/order.py (_mix32).
 DEV uint32_t mix32(uint32_t x) {

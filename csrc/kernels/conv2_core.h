@@ -163,8 +163,8 @@ DEV void conv2_tiles(const bf16* Wg, const bf16* xin, bf16* ws, int w, int g, in
 constexpr size_t DG_LDS = (C2_XIN + C2_OUT) * 2 + 2304 * 3 + WS_BYTES;
 
 template <bool IN_LAUNCH>
-DEV void conv2_dgrad_image(const DmlcConv2DgradArgs& a, int b, char* smem, unsigned* cnt = nullptr,
-                           unsigned target = 0, unsigned* err = nullptr) {
+DEV void conv2_dgrad_image(const DmlcConv2DgradArgs& a, int b, char* smem, Seam seam = Seam{nullptr, 0, 0u},
+                           unsigned* err = nullptr) {
   bf16* dyp = reinterpret_cast<bf16*>(smem);
   bf16* outs = dyp + C2_XIN;
   bf16* dp2 = outs + C2_OUT;                                    // [36][64] staged pool2 grad
@@ -186,15 +186,7 @@ DEV void conv2_dgrad_image(const DmlcConv2DgradArgs& a, int b, char* smem, unsig
     if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(dyp + swzpad(pix, c)) = bf16x8{};
   }
   if (IN_LAUNCH) {
-    if (tid == 0) {
-      for (unsigned it = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it) {
-        if (it > (1u << 20)) {
-          __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
+    if (tid < 64) seam_wait(seam, tid, err, 2u);
     lds_barrier();
     if (tid < 288)
       reinterpret_cast<uint4*>(dp2)[tid] = __builtin_bit_cast(

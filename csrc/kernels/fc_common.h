@@ -43,15 +43,28 @@ constexpr int L_W1_A = 0, L_W1_B = 2 * 256 * 64 * 2;
 constexpr int L_FWD_A = 0, L_FWD_B = 64 * KST_A * 2;
 constexpr int L_RED = L_W1_B + 256 * 64 * 2;   // [8][64] fp32 bias-gradient partials (dW tasks)
 // ---- sync words (DmlcFcArgs::sync, uints, each counter on its own 128-B line) --------------------
-DEV unsigned* cntA(const DmlcFcArgs& a, int m) { return a.sync + 32 * m; }          // m < 4
-DEV unsigned* cntB(const DmlcFcArgs& a, int m) { return a.sync + 32 * (4 + m); }    // m < 4
-DEV unsigned* cntBall(const DmlcFcArgs& a) { return a.sync + 32 * 8; }
-// a.sync + 32 * 10 .. + 32 * 19: the two-level end-of-launch ticket (common.h last_arrival)
-// a.sync + 32 * 9: launch epoch E; dp2 row tile m < 4 counts into set E & 1 (the launch's last
-// arrival re-arms the OTHER set and bumps E, so it can arrive before the dgrad's waits are done)
+// (common.h Seam: each seam's arrivals are spread over several words, polled side by side)
+// a.sync + 32 * 9: launch epoch E; a.sync + 32 * 10 .. + 32 * 19: the two-level end-of-launch ticket
+// (common.h last_arrival)
 DEV unsigned* epochW(const DmlcFcArgs& a) { return a.sync + 32 * 9; }
-DEV unsigned* cntD(const DmlcFcArgs& a, unsigned set, int m) { return a.sync + 32 * (20 + 4 * (set & 1) + m); }
+// fc1 forward task (m, nt, s) -> word (m, nt): FC_S arrivals each; the head blocks of row tile m wait
+// for the tile's 6 words
+constexpr int SY_A = 28, SY_B = SY_A + 24, SY_D = SY_B + 16, SY_END = SY_D + 2 * 4 * 18;
+static_assert(SY_END == 212, "engine/fused.py fc_sync and the binding size the sync words");
+DEV unsigned* cntA(const DmlcFcArgs& a, int m, int nt) { return a.sync + 32 * (SY_A + 6 * m + nt); }
+DEV Seam seamA(const DmlcFcArgs& a, int m) { return Seam{cntA(a, m, 0), 6, (unsigned)FC_S}; }
+// head block hb (row tile m = hb >> 4) -> word (m, hb & 3): a quarter of the tile's head blocks each
+DEV unsigned* cntB(const DmlcFcArgs& a, int m, int q) { return a.sync + 32 * (SY_B + 4 * m + q); }
+DEV unsigned head_quarter(const DmlcFcArgs& a, int m) { return (unsigned)(min(64, a.B - 64 * m) / FC_RB / 4); }
+DEV Seam seamB(const DmlcFcArgs& a, int m) { return Seam{cntB(a, m, 0), 4, head_quarter(a, m)}; }
+// dp2 task (m, j) -> one flag word of set E & 1 (the launch's last arrival re-arms the OTHER set and
+// bumps E, so it can arrive before the dgrad's waits are done); the dgrad of an image in row tile m
+// waits for the tile's 18 words
 constexpr unsigned DP2_COL_TILES = 2304 / 128;
+DEV unsigned* cntD(const DmlcFcArgs& a, unsigned set, int m, int j) {
+  return a.sync + 32 * (SY_D + 72 * (set & 1) + 18 * m + j);
+}
+DEV Seam seamD(const DmlcFcArgs& a, unsigned set, int m) { return Seam{cntD(a, set, m, 0), (int)DP2_COL_TILES, 1u}; }
 
 DEV unsigned ld_relaxed(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 // one lane: spin until *p >= target (bounded; on give-up the sticky error word is set)
@@ -65,17 +78,14 @@ DEV void wait_ge(unsigned* p, unsigned target, unsigned* err) {
   }
 }
 // every storing wave drains its write-through stores, the workgroup meets, one lane signals
-DEV void publish(unsigned* c1, unsigned* c2) {
+DEV void publish(unsigned* c) {
   wait_vm_all();
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(c1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (c2) __hip_atomic_fetch_add(c2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// one lane waits, then the workgroup meets (every later load of the handed-off bytes is sc1)
-DEV void consume(unsigned* c, unsigned target, unsigned* err) {
-  if (threadIdx.x == 0) wait_ge(c, target, err);
+// wave 0 waits, then the workgroup meets (every later load of the handed-off bytes is sc1)
+DEV void consume(const Seam& s, unsigned* err) {
+  if (threadIdx.x < 64) seam_wait(s, threadIdx.x, err, 2u);
   __syncthreads();
 }
 
@@ -247,7 +257,7 @@ DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid, unsi
   bf16* sb = reinterpret_cast<bf16*>(smem + L_DP2_B);
   const int mt = T.i, n0 = 128 * T.j;
   const int rows = min(64, a.B - 64 * mt);
-  consume(cntB(a, mt), (unsigned)(rows / FC_RB), a.err);
+  consume(seamB(a, mt), a.err);
   DMLC_STAMP(DMLC_TK_GEMM, 3);
   {
     const rsrc_t r = buf_rsrc(a.dh1);
@@ -294,7 +304,7 @@ DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid, unsi
       st16(rd, (uint32_t)((64 * mt + rr) * 2304 + n0 + cc) * 2, make_uint4(lo.x, lo.y, hi.x, hi.y));
     }
   }
-  publish(cntD(a, epoch, mt), nullptr);
+  publish(cntD(a, epoch, mt, T.j));
 }
 
 // dW1 / dW2 / dW3: 128 x 64 tile of A^T B over the batch (A, B: bf16 [B][lda], [B][ldb])
@@ -332,10 +342,12 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
   const int M = T.kind == 1 ? 2304 : T.kind == 2 ? 384 : 192;
   const int N = T.kind == 1 ? 384 : T.kind == 2 ? 192 : 10;
   const int ldc = N;
-  // The K (= batch) range arrives one 64-row tile at a time: wait for that tile's head blocks only
-  // (its own counter: the polls spread over mtiles words instead of all hitting the total) and
-  // issue its operand loads before waiting for the next tile.  The barrier between is an s_barrier
-  // (lds_barrier), not __syncthreads: that would drain the loads already in flight.
+  // The K (= batch) range is the head blocks' rows: lanes 0..15 of wave 0 poll the 4 x 4 head words
+  // side by side (one memory round trip per poll round for all of them), then every tile's loads go
+  // out at once.  (r4 waited for each tile's counter in turn, issuing that tile's loads in between --
+  // the head blocks finish together, so that bought no overlap and cost a round trip per tile.)  The
+  // barrier is an s_barrier (lds_barrier), not __syncthreads: that would drain the prefetched loads
+  // already in flight.
   // (the operand of each kind, selected branch-free: the same three loads per tile for every kind)
   // (every candidate made opaque BEFORE the select: a select between two argument fields becomes a
   // load through a selected address into the argument block, and hipcc then copies the whole block
@@ -346,15 +358,16 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
   const int ldb = __builtin_amdgcn_readfirstlane(T.kind == 1 ? 384 : T.kind == 2 ? 192 : 16);
   const int cb = T.kind == 3 ? 0 : n0;
   const bool need_a = T.kind != 1;
-  // (written out per tile: with the spin inside, a loop over the tiles stayed rolled and its register
-  // arrays went to scratch)
+  // (written out per tile: as a loop over the tiles it stayed rolled and its register arrays went
+  // to scratch)
   struct T3 { uint4 a0, a1, b; };
+  if (HANDOFF) {
+    if (tid < 64)                              // lane 4m + q: word (m, q) of row tile m < mtiles
+      seam_wait(Seam{cntB(a, 0, 0), 4 * a.mtiles, 0u}, tid, a.err, 2u, (int)head_quarter(a, min(tid >> 2, 3)));
+    lds_barrier();
+  }
   auto tile = [&](int m) __attribute__((always_inline)) {
     const bool on = m < a.mtiles;
-    if (HANDOFF) {
-      if (on && tid == 0) wait_ge(cntB(a, m), (unsigned)(min(64, a.B - 64 * m) / FC_RB), a.err);
-      lds_barrier();
-    }
     const int Bm = on ? a.B : 0;            // a tile past the batch reads nothing (zeros)
     T3 r;
     r.b = ld_mtile<HANDOFF>(pb, ldb, cb, ldb, Bm, m, tid);

@@ -261,7 +261,7 @@ class FusedCifarEngine:
         self.fc_fused = (fc_ok if V["fc_fused"] is None else bool(V["fc_fused"]) and fc_ok) \
             and os.environ.get("DMLC_FC_FUSED", "1") != "0"
         self.h1part8 = z(8, B, 384, dt=torch.float32) if self.fc_fused else None
-        self.fc_sync = torch.zeros(28 * 32, dtype=torch.int32, device=dev)
+        self.fc_sync = torch.zeros(212 * 32, dtype=torch.int32, device=dev)   # fc_common.h SY_END
         self._fc_src = None
         # head: head_rows(B) batch rows per workgroup (B / rows workgroups share the fc2 weight reads);
         # the fused fc chain's head takes 4 rows per workgroup
