@@ -252,6 +252,7 @@ DEV void mma_128x64(const bf16* sa, const bf16* sb, int ksteps, Acc& acc, int w,
             mfrag(sb, 32 * wn + 16, kk, g, li));
 }
 
+
 DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid, unsigned epoch) {
   bf16* sa = reinterpret_cast<bf16*>(smem + L_DP2_A);
   bf16* sb = reinterpret_cast<bf16*>(smem + L_DP2_B);
@@ -280,10 +281,24 @@ DEV void dp2_task(const DmlcFcArgs& a, const CTask& T, char* smem, int tid, unsi
   const int wm = w & 1, wn = w >> 1;
   Acc acc;
   acc.zero();
-#pragma unroll 4
-  for (int kk = 0; kk < 12; ++kk)
-    acc.mma(kfrag(sa, KST_A, 32 * wm, kk, g, li), kfrag(sa, KST_A, 32 * wm + 16, kk, g, li),
-            kfrag(sb, KST_A, 32 * wn, kk, g, li), kfrag(sb, KST_A, 32 * wn + 16, kk, g, li));
+  bf16x8 F[2][4];                              // software-pipelined as mma_128x64
+  auto frags = [&](int kk, bf16x8 (&f)[4]) __attribute__((always_inline)) {
+    f[0] = kfrag(sa, KST_A, 32 * wm, kk, g, li);
+    f[1] = kfrag(sa, KST_A, 32 * wm + 16, kk, g, li);
+    f[2] = kfrag(sb, KST_A, 32 * wn, kk, g, li);
+    f[3] = kfrag(sb, KST_A, 32 * wn + 16, kk, g, li);
+  };
+  frags(0, F[0]);
+#pragma unroll
+  for (int kk = 0; kk < 12; ++kk) {
+    const int cur = kk & 1;
+    wait_lds();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kk + 1 < 12) frags(kk + 1, F[cur ^ 1]);
+    __builtin_amdgcn_sched_barrier(0);
+    acc.mma(F[cur][0], F[cur][1], F[cur][2], F[cur][3]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   __syncthreads();
   DMLC_STAMP(DMLC_TK_GEMM, 4);
   float* ct = reinterpret_cast<float*>(smem);  // [64][132]
