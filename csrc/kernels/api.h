@@ -273,7 +273,7 @@ struct DmlcWgradArgs {
   DmlcConv2WgradArgs w2;
   int apply;
   unsigned int* bar;
-  int helpers;              // apply mode: idle conv1 blocks help reduce the conv2 slabs (always on)
+  int helpers;              // apply mode: idle conv1 blocks help reduce the conv2 slabs (B > 128)
   DmlcSgdArgs sgd;
   // apply mode with the fc chain (fc_in_launch): the conv1 blocks, whose conv1 work ends ~8 us before
   // the conv2 blocks', also run the fc weight-gradient tiles (dW1 / dW2 / dW3 + bias gradients,
