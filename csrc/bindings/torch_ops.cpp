@@ -138,7 +138,7 @@ void conv2_dgrad(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, const 
   c10::DeviceGuard guard(dp2.device());
   DmlcConv2DgradArgs a;
   a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
-  a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B;
+  a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B; a.split = 0;
   CHECK_HIP(dmlc_conv2_dgrad(&a, stream_of(dp2)));
 }
 
@@ -196,7 +196,7 @@ void conv2_dgrad_split(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, 
   c10::DeviceGuard guard(dp2.device());
   DmlcConv2DgradArgs a;
   a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.wd = w2d.data_ptr();
-  a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B;
+  a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B; a.split = 0;
   CHECK_HIP(dmlc_conv2_dgrad_split(&a, stream_of(dp2)));
 }
 
@@ -483,6 +483,7 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
     check(*dy2, "dy2", at::kBFloat16, {B, 144, 64});
     g.dp2 = dp2.data_ptr(); g.am2 = am2->data_ptr<uint8_t>(); g.wd = w2d->data_ptr();
     g.dp1 = dp1->data_ptr(); g.dy2 = dy2->data_ptr(); g.B = (int)B;
+    g.split = B <= 128 ? 1 : 0;          // the chain's 256 workgroups: two per image at B <= 128
   }
   CHECK_HIP(dmlc_fc_chain(&a, dg_on ? &g : nullptr, stream_of(p2)));
 }

@@ -93,6 +93,7 @@ struct DmlcConv2DgradArgs {
   void* dp1;                // bf16 [B][12][12][64] grad wrt pool1 output
   void* dy2;                // bf16 [B][144][64]   grad wrt conv2 pre-activation (for wgrad)
   int B;
+  int split;                // in the fc chain: 2 workgroups per image (B <= 128), else one
 };
 
 // conv1 weight gradient (pool1/ReLU backward fused; split-K over image groups).

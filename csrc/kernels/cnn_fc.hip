@@ -29,6 +29,7 @@
 
 #include "fc_common.h"
 #include "conv2_core.h"
+#include "split_common.h"
 
 namespace dmlc {
 
@@ -51,6 +52,7 @@ constexpr int FC_LDS = L_DP2_END > HL::BYTES ? L_DP2_END : HL::BYTES;
 static_assert(FC_LDS <= 160 * 1024, "fc chain LDS exceeds a CU");
 constexpr int FC_LDS_ALL = FC_LDS > (int)DG_LDS ? FC_LDS : (int)DG_LDS;   // with the conv2 dgrad
 static_assert(FT == NT && FC_LDS_ALL <= 160 * 1024, "the dgrad runs in the chain's workgroups");
+static_assert(FT == SP_NT && SP_LDS <= (size_t)FC_LDS_ALL, "... and so does the split dgrad");
 static_assert(L_FWD_B + FC_KS * 64 * 2 <= FC_LDS && L_RED + 8 * 64 * 4 <= FC_LDS, "task images");
 
 // =================================================================================================
@@ -404,7 +406,15 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a, DmlcConv2Dgrad
   }
   // the conv2 input gradient of image blk (dg.B = 0: a separate launch does it): its dp2 row tile
   // comes from this launch's dp2 tasks; everything else it reads was written by earlier launches
-  if (blk < dg.B) conv2_dgrad_image<true>(dg, blk, smem, seamD(a, epoch, blk >> 6), a.err);
+  if (dg.split) {                              // B <= 128: image b's input-channel half h
+    if (blk < 2 * dg.B) {
+      int b, h;
+      split_index<2>(blk, b, h);
+      conv2_dgrad_split_image<true>(dg, b, h, smem, seamD(a, epoch, b >> 6), a.err);
+    }
+  } else if (blk < dg.B) {
+    conv2_dgrad_image<true>(dg, blk, smem, seamD(a, epoch, blk >> 6), a.err);
+  }
   if (blk < H) DMLC_STAMP(DMLC_TK_HEAD, 7);
   else DMLC_STAMP(DMLC_TK_GEMM, 6);
 }
@@ -421,6 +431,7 @@ extern "C" hipError_t dmlc_fc_chain(const DmlcFcArgs* a, const DmlcConv2DgradArg
   if (dg) {
     // one image per workgroup of the 256: the batch rows are the chain's, dp2 its own output
     if (dg->B != a->B || dg->dp2 != a->dp2 || !dg->am2 || !dg->wd || !dg->dp1 || !dg->dy2) return hipErrorInvalidValue;
+    if (dg->split && (2 * dg->B > FC_BLOCKS || dg->B % 8)) return hipErrorInvalidValue;
     d = *dg;
   }
   static int cus = 0;

@@ -18,9 +18,9 @@ their inputs from device memory:
                  step's batch rows too)
 
 At B <= 128 launch 1 becomes conv1_fwd_split + conv2_fwd_split (cnn_split.hip, two or four
-workgroups per image so a small batch fills the 256 CUs) and the conv2 input gradient runs as its
-own channel-split launch (conv2_dgrad_split) with the fc weight-gradient tiles in the wgrad launch:
-five launches.  B > 256 (and ranks sharing one GPU) use the three-launch fc path (grouped fc1 GEMM,
+workgroups per image so a small batch fills the 256 CUs), the fc chain's 256 workgroups run the conv2
+input gradient two per image (cnn_split.hip's channel halves) and the fc weight-gradient tiles run in
+the wgrad launch: four launches.  B > 256 (and ranks sharing one GPU) use the three-launch fc path (grouped fc1 GEMM,
 head, grouped backward GEMM).  The fp8 path (BASELINE config 5) runs conv1 and the fp8 conv2 forward
 as two launches, the fp8 conv2 dgrad as its own launch and the SGD as its own launch.
 
@@ -79,7 +79,7 @@ def head_rows(B: int) -> int:
 VARIANT_DEFAULTS = {
     "split_fwd": False,        # conv1 and conv2 forward as two launches (bitwise reference of conv12_fwd)
     "fc_fused": None,          # the persistent fc chain (B <= 256, one rank per GPU); env DMLC_FC_FUSED=0 off
-    "fc_dgrad": None,          # conv2 dgrad inside the fc chain (default: when the dgrad is one WG per image)
+    "fc_dgrad": None,          # conv2 dgrad inside the fc chain (default: on; two workgroups per image at B <= 128)
     "fc_dw_in_wgrad": None,    # fc dW tiles in the wgrad launch (default: when the dgrad is not in the chain)
     "fc1_epilogue": True,      # single GPU: the fc1 update in the dW1 epilogue
     "wgrad_sgd": True,         # in-launch SGD / slab reduction of the wgrad launch; env DMLC_WGRAD_SGD=0 off
@@ -350,11 +350,11 @@ class FusedCifarEngine:
         # once its dp2 row tile is published: one launch boundary less, but the hand-off (publish ->
         # poll -> sc1 dp2 loads) costs ~2 us of it back.  With the fc dW tiles kept in the chain (below)
         # it measured 1.8-2.5 us/step faster at B = 144 / 160 / 192 / 224 / 256 (profiles/
-        # r4_v8_fc_dgrad_b144_256_ab.txt); at B <= 128 the split dgrad (2 workgroups per image) stays
-        # its own launch.  Variant fc_dgrad forces it on / off.
+        # r4_v8_fc_dgrad_b144_256_ab.txt); at B <= 128 the chain's 256 workgroups run the split dgrad
+        # (two per image, cnn_split.hip's halves) instead of its own launch (r5, profiles/
+        # r5_fc_split_dgrad_b128_ab.txt).  Variant fc_dgrad forces it on / off.
         fdg = V["fc_dgrad"]
-        self.fc_dgrad = (self.fc_fused and not self.fp8_dgrad
-                         and (bool(fdg) if fdg is not None else self.dgrad_split != 2))
+        self.fc_dgrad = self.fc_fused and not self.fp8_dgrad and (bool(fdg) if fdg is not None else True)
         self._dgrad_done = False
         # single GPU, fused fc chain + apply mode: the fc weight-gradient tiles and every fc SGD can run
         # in the wgrad launch's conv1 blocks (between their barrier arrival and the conv1 reduction),
@@ -362,9 +362,11 @@ class FusedCifarEngine:
         # r4_v7_fc_dgrad_dw_ab.txt, us/step): chain dgrad off: dW in chain 81.8, in wgrad 80.4; chain
         # dgrad on: dW in chain 79.8, in wgrad 80.2 -- so by default the dW tiles move to the wgrad
         # launch only when the dgrad is not in the chain.  Variant fc_dw_in_wgrad forces it.
+        # At B <= 128 (the chain's split dgrad) the dW tiles are better in the wgrad launch too: 64.2-64.4
+        # vs 65.6-65.9 us/step at B = 128 (profiles/r5_fc_split_dgrad_b128_ab.txt).
         fdw = V["fc_dw_in_wgrad"]
         self.fc_dw_in_wgrad = (self.fc_fused and self.wgrad_apply
-                               and (bool(fdw) if fdw is not None else not self.fc_dgrad))
+                               and (bool(fdw) if fdw is not None else (not self.fc_dgrad or B <= 128)))
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
                                                                         s_par=FC1_NUMEL)

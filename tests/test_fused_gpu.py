@@ -383,12 +383,13 @@ def test_fc_chain_launch_matches_three_launch_path(B):
     assert abs(fused.read_stats(10)["loss"] - ref.read_stats(10)["loss"]) < 3e-2 * max(1.0, abs(ref.read_stats(10)["loss"]))
 
 
-@pytest.mark.parametrize("B", [160, 256])
+@pytest.mark.parametrize("B", [64, 128, 160, 256])
 def test_dgrad_in_fc_chain_is_bit_identical(B):
-    """The conv2 input gradient inside the fc chain launch (each workgroup's image once its dp2 row
-    tile's 18 column tasks have published) against the separate dgrad launch: dP1, dY2, every
-    gradient segment and the weights after eager + graph-replayed steps are bit-identical (the same
-    device function on the same operands; only the hand-off differs)."""
+    """The conv2 input gradient inside the fc chain launch (each workgroup's image -- at B <= 128 each
+    pair of workgroups' image halves, as the split dgrad launch -- once its dp2 row tile's 18 column
+    tasks have published) against the separate dgrad launch: dP1, dY2, every gradient segment and the
+    weights after eager + graph-replayed steps are bit-identical (the same device function on the
+    same operands; only the hand-off differs)."""
     data, labels = _synthetic(8 * B, seed=63)
     kw = dict(seed=64, lr=1e-3, relu_logits=False)
     fused = FusedCifarEngine(B, data, labels, **kw, variant={"fc_dgrad": True})
