@@ -80,7 +80,7 @@ VARIANT_DEFAULTS = {
     "split_fwd": False,        # conv1 and conv2 forward as two launches (bitwise reference of conv12_fwd)
     "fc_fused": None,          # the persistent fc chain (B <= 256, one rank per GPU); env DMLC_FC_FUSED=0 off
     "fc_dgrad": None,          # conv2 dgrad inside the fc chain (default: on; two workgroups per image at B <= 128)
-    "fc_dw_in_wgrad": None,    # fc dW tiles in the wgrad launch (default: when the dgrad is not in the chain)
+    "fc_dw_in_wgrad": None,    # fc dW tiles in the wgrad launch (default: dgrad not in the chain, or B <= 128)
     "fc1_epilogue": True,      # single GPU: the fc1 update in the dW1 epilogue
     "wgrad_sgd": True,         # in-launch SGD / slab reduction of the wgrad launch; env DMLC_WGRAD_SGD=0 off
     "wgrad_sgd_fp8": False,    # the same for --dtype fp8 (bit-identical, measured 1.4 % slower at B=1024)
