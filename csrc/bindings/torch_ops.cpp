@@ -86,9 +86,13 @@ void fp8_roundtrip(const Tensor& x, const Tensor& y, double scale) {
 void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period,
                 int64_t cy, int64_t cx, const Tensor& w1f, const Tensor& b1, const Tensor& p1, const Tensor& am1,
                 const Tensor& w2f, const Tensor& b2, const Tensor& p2, const Tensor& am2,
-                const c10::optional<Tensor>& xraw, bool xraw_in) {
+                const c10::optional<Tensor>& xraw, bool xraw_in, const c10::optional<Tensor>& split_flags,
+                const c10::optional<Tensor>& err) {
   const int64_t B = p1.size(0);
   TORCH_CHECK(!xraw_in || xraw.has_value(), "conv12_fwd: xraw_in needs the prefetched images");
+  const bool split = split_flags.has_value();
+  TORCH_CHECK(!split || (err.has_value() && !xraw_in && B <= 128),
+              "conv12_fwd split (two workgroups per image): B <= 128, the error word, no prefetched images");
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
   check(w1f, "w1f", at::kBFloat16, {64, 96});
@@ -111,7 +115,14 @@ void conv12_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tenso
   DmlcConv2FwdArgs a2;
   a2.in = p1.data_ptr(); a2.w = w2f.data_ptr(); a2.bias = b2.data_ptr<float>();
   a2.out = p2.data_ptr(); a2.am = am2.data_ptr<uint8_t>(); a2.B = (int)B;
-  CHECK_HIP(dmlc_conv12_fwd(&a1, &a2, stream_of(p1)));
+  if (split) {
+    check_min(*split_flags, "split_flags", at::kInt, 32 * 2 * B);
+    check_numel(*err, "err", at::kInt, 1);
+    CHECK_HIP(dmlc_conv12_fwd_split(&a1, &a2, reinterpret_cast<unsigned*>(split_flags->data_ptr<int>()),
+                                    reinterpret_cast<unsigned*>(err->data_ptr<int>()), stream_of(p1)));
+  } else {
+    CHECK_HIP(dmlc_conv12_fwd(&a1, &a2, stream_of(p1)));
+  }
 }
 
 void conv2_fwd(const Tensor& in, const Tensor& w2f, const Tensor& b2, const Tensor& out, const Tensor& am) {
@@ -689,7 +700,7 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("conv2_fwd(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("conv12_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
         "Tensor(a!) p1, Tensor(b!) am1, Tensor w2f, Tensor b2, Tensor(c!) p2, Tensor(d!) am2, "
-        "Tensor(e!)? xraw=None, bool xraw_in=False) -> ()");
+        "Tensor(e!)? xraw=None, bool xraw_in=False, Tensor(f!)? split_flags=None, Tensor(g!)? err=None) -> ()");
   m.def("conv2_dgrad(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
   m.def("conv1_fwd_split(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
         "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? xraw, int nsplit) -> ()");

@@ -290,6 +290,10 @@ hipError_t dmlc_conv12_fwd(const DmlcConv1FwdArgs* a1, const DmlcConv2FwdArgs* a
 // channel-split variants (cnn_split.hip): nsplit workgroups per image (B % 8 == 0), each owning
 // 64 / nsplit output channels (conv1: nsplit 2 or 4; conv2 forward / input gradient: 2)
 hipError_t dmlc_conv1_fwd_split(const DmlcConv1FwdArgs* a, int nsplit, hipStream_t s);
+// conv1 + pool1 + conv2 + pool2 with two workgroups per image exchanging their pool1 halves in the
+// launch (B <= 128; flags: 32 * 2B zeroed uints, err: the sticky error word)
+hipError_t dmlc_conv12_fwd_split(const DmlcConv1FwdArgs* a1, const DmlcConv2FwdArgs* a2, unsigned* flags,
+                                 unsigned* err, hipStream_t s);
 hipError_t dmlc_conv2_fwd_split(const DmlcConv2FwdArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_dgrad_split(const DmlcConv2DgradArgs* a, hipStream_t s);
 hipError_t dmlc_conv2_fwd_fp8(const DmlcConv2FwdFp8Args* a, hipStream_t s);

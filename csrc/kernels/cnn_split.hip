@@ -23,9 +23,11 @@
 namespace dmlc {
 
 // TF-SAME 3x3/2 max pool (pool_emit of conv_common.h) over an LDS image [H*H][CH*8] -> global
-// out[q][64] / am[q][64] at channels c0 + 8c, for a workgroup of T threads.
+// out[q][64] / am[q][64] at channels c0 + 8c, for a workgroup of T threads.  pad_lds (conv12 split):
+// the pooled values also go into the zero-padded conv2 input image (swzpad, its channels c0 ..) and
+// the global stores are sc1 (write-through: the partner workgroup reads them in the same launch).
 template <int H, int CH, int T>
-DEV void pool_emit_c(const bf16* img, bf16* out, uint8_t* am, int c0, int tid) {
+DEV void pool_emit_c(const bf16* img, bf16* out, uint8_t* am, int c0, int tid, bf16* pad_lds = nullptr) {
   constexpr int HO = H / 2;
   for (int task = tid; task < HO * HO * CH; task += T) {
     const int q = task / CH, c = task - q * CH;
@@ -40,21 +42,24 @@ DEV void pool_emit_c(const bf16* img, bf16* out, uint8_t* am, int c0, int tid) {
     uint4 o;
     uint32_t alo, ahi, bmax = 0;
     pool_window(v, o, alo, ahi, bmax);
-    st_maybe_nt<kNtX>(reinterpret_cast<uint4*>(out + q * 64 + c0 + c * 8), o);
-    st_maybe_nt<kNtX>(reinterpret_cast<uint2*>(am + q * 64 + c0 + c * 8), make_uint2(alo, ahi));
+    if (pad_lds) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), buf_rsrc(out), (uint32_t)(q * 64 + c0 + c * 8) * 2, 0, kSC1);
+      st_out8(am, (uint32_t)(q * 64 + c0 + c * 8), make_uint2(alo, ahi));
+      *reinterpret_cast<uint4*>(pad_lds + swzpad((py + 2) * (HO + 4) + px + 2, (c0 >> 3) + c)) = o;
+    } else {
+      st_maybe_nt<kNtX>(reinterpret_cast<uint4*>(out + q * 64 + c0 + c * 8), o);
+      st_maybe_nt<kNtX>(reinterpret_cast<uint2*>(am + q * 64 + c0 + c * 8), make_uint2(alo, ahi));
+    }
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 // conv1 (+ uint8 gather / center crop, bias, ReLU, pool1) of NCO output channels of one image.
+// (body shared with the fused conv12 split kernel below: xin [28][24][16] row windows, img
+// [576][NCO] (swzc); pad_lds: see pool_emit_c)
 template <int NCO>
-__global__ __launch_bounds__(SP_NT, 4) void k_conv1_fwd_split(DmlcConv1FwdArgs a) {
-  constexpr int S = 64 / NCO, CT = NCO / 16, CH = NCO / 8;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16* xin = reinterpret_cast<bf16*>(smem);                 // [28][24][16] row windows
-  bf16* img = xin + C1_XIN;                                  // [576][NCO] (swzc)
-  int b, h;
-  split_index<S>(blockIdx.x, b, h);
+DEV void conv1_split_body(const DmlcConv1FwdArgs& a, int b, int h, bf16* xin, bf16* img, bf16* pad_lds = nullptr) {
+  constexpr int CT = NCO / 16, CH = NCO / 8;
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15;
   const int co0 = NCO * h;
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 0);
@@ -105,8 +110,34 @@ __global__ __launch_bounds__(SP_NT, 4) void k_conv1_fwd_split(DmlcConv1FwdArgs a
   }
   __syncthreads();
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 2);
-  pool_emit_c<24, CH, SP_NT>(img, reinterpret_cast<bf16*>(a.out) + (size_t)b * 9216, a.am + (size_t)b * 9216, co0, tid);
+  pool_emit_c<24, CH, SP_NT>(img, reinterpret_cast<bf16*>(a.out) + (size_t)b * 9216, a.am + (size_t)b * 9216, co0, tid,
+                             pad_lds);
   DMLC_STAMP(DMLC_TK_CONV1_FWD, 3);
+}
+template <int NCO>
+__global__ __launch_bounds__(SP_NT, 4) void k_conv1_fwd_split(DmlcConv1FwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int b, h;
+  split_index<64 / NCO>(blockIdx.x, b, h);
+  bf16* xin = reinterpret_cast<bf16*>(smem);
+  conv1_split_body<NCO>(a, b, h, xin, xin + C1_XIN);
+}
+
+// conv2 (padded input complete in xin) + bias + ReLU + pool2 of output channels 32h .. 32h+31 of image b
+DEV void conv2_split_rest(const DmlcConv2FwdArgs& a, int b, int h, bf16* xin, bf16* ws) {
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15;
+  bf16* img = xin;                                       // [144][32] conv output, after the core
+  float b4[2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b4[c][i] = a.bias[32 * h + 16 * c + 4 * g + i];
+  split_tiles(reinterpret_cast<const bf16*>(a.w) + (size_t)32 * h * 1600, xin, ws, w, g, li, lane, DMLC_TK_CONV2_FWD,
+              [&](int c, int t, const f32x4& acc) { store_relu_c<4>(img, 16 * t + li, 16 * c + 4 * g, acc, b4[c]); });
+  __syncthreads();
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 2);
+  pool_emit_c<12, 4, SP_NT>(img, reinterpret_cast<bf16*>(a.out) + (size_t)b * 2304, a.am + (size_t)b * 2304, 32 * h, tid);
+  DMLC_STAMP(DMLC_TK_CONV2_FWD, 3);
 }
 
 // conv2 + bias + ReLU + pool2 of 32 output channels of one image (S = 2 workgroups per image)
@@ -114,10 +145,9 @@ __global__ __launch_bounds__(SP_NT, 4) void k_conv2_fwd_split(DmlcConv2FwdArgs a
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* xin = reinterpret_cast<bf16*>(smem + SP_XIN);
   bf16* ws = reinterpret_cast<bf16*>(smem + SP_WS0);
-  bf16* img = xin;                                       // [144][32] conv output, after the core
   int b, h;
   split_index<2>(blockIdx.x, b, h);
-  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), g = lane >> 4, li = lane & 15;
+  const int tid = threadIdx.x;
   DMLC_STAMP(DMLC_TK_CONV2_FWD, 0);
   const bf16* in = reinterpret_cast<const bf16*>(a.in) + (size_t)b * 9216;
   uint4 v[4];
@@ -133,17 +163,60 @@ __global__ __launch_bounds__(SP_NT, 4) void k_conv2_fwd_split(DmlcConv2FwdArgs a
     const int s = tid + i * SP_NT;
     *reinterpret_cast<uint4*>(xin + swzpad(s >> 3, s & 7)) = v[i];
   }
-  float b4[2][4];
-#pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) b4[c][i] = a.bias[32 * h + 16 * c + 4 * g + i];
-  split_tiles(reinterpret_cast<const bf16*>(a.w) + (size_t)32 * h * 1600, xin, ws, w, g, li, lane, DMLC_TK_CONV2_FWD,
-              [&](int c, int t, const f32x4& acc) { store_relu_c<4>(img, 16 * t + li, 16 * c + 4 * g, acc, b4[c]); });
+  conv2_split_rest(a, b, h, xin, ws);
+}
+
+// conv1 -> pool1 -> conv2 -> pool2 of image b in ONE launch, two workgroups per image (B <= 128): half
+// h computes conv1 / pool1 channels 32h.. straight into its padded conv2 input, stores them write-
+// through (sc1) for the backward AND for its partner, raises its flag, waits for the partner's flag,
+// reads the partner's 32 channels (sc1) and runs conv2 / pool2 of output channels 32h..  -- the p1
+// round trip and the launch boundary between conv1_fwd_split and conv2_fwd_split go away.
+// flags[32 * (2b + h)]: zero between launches (the reader resets the flag it consumed).  Both halves
+// of an image must be co-resident: grid 2B <= the CU count (one workgroup per CU at this LDS size,
+// host-checked); the spin is bounded (the sticky error word) like every other hand-off.
+// LDS: [0, 32 KB) the padded conv2 input; then conv1's row windows + output [576][32] (58 KB), which
+// conv2's weight slices (40 KB, after pool1) overwrite.
+constexpr size_t C12S_X1 = (size_t)C2_XIN * 2, C12S_LDS = C12S_X1 + (size_t)(C1_XIN + 576 * 32) * 2;
+static_assert(C12S_LDS <= 160 * 1024 && SP_LDS <= C12S_LDS, "conv12 split LDS map");
+__global__ __launch_bounds__(SP_NT, 1) void k_conv12_fwd_split(DmlcConv1FwdArgs a1, DmlcConv2FwdArgs a2,
+                                                                unsigned* flags, unsigned* err) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* xin2 = reinterpret_cast<bf16*>(smem);
+  bf16* xin1 = reinterpret_cast<bf16*>(smem + C12S_X1);
+  int b, h;
+  split_index<2>(blockIdx.x, b, h);
+  const int tid = threadIdx.x;
+  for (int s = tid; s < 2048; s += SP_NT) {             // halo of the padded conv2 input
+    const int pix = s >> 3, c = s & 7, r = pix >> 4, col = pix & 15;
+    if (r < 2 || r >= 14 || col < 2 || col >= 14) *reinterpret_cast<bf16x8*>(xin2 + swzpad(pix, c)) = bf16x8{};
+  }
+  conv1_split_body<32>(a1, b, h, xin1, xin1 + C1_XIN, xin2);
+  wait_vm_all();                                         // this thread's sc1 p1 stores are acknowledged
   __syncthreads();
-  DMLC_STAMP(DMLC_TK_CONV2_FWD, 2);
-  pool_emit_c<12, 4, SP_NT>(img, reinterpret_cast<bf16*>(a.out) + (size_t)b * 2304, a.am + (size_t)b * 2304, 32 * h, tid);
-  DMLC_STAMP(DMLC_TK_CONV2_FWD, 3);
+  unsigned* mine = flags + 32 * (2 * b + h);
+  unsigned* theirs = flags + 32 * (2 * b + (h ^ 1));
+  if (tid == 0) {
+    __hip_atomic_store(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned it = 0; __hip_atomic_load(theirs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u; ++it) {
+      if (it > (1u << 20)) {
+        __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_store(theirs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed for the next launch
+  }
+  __syncthreads();
+  // the partner's 32 channels: 144 pixels x 4 chunks of 16 B
+  const rsrc_t p1 = buf_rsrc(reinterpret_cast<const bf16*>(a1.out) + (size_t)b * 9216);
+  const int c0 = 4 * (h ^ 1);
+  for (int s = tid; s < 144 * 4; s += SP_NT) {
+    const int q = s >> 2, c = c0 + (s & 3), py = q / 12, px = q - py * 12;
+    const uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(p1, (uint32_t)(q * 64 + c * 8) * 2, 0, kSC1));
+    *reinterpret_cast<uint4*>(xin2 + swzpad((py + 2) * 16 + px + 2, c)) = v;
+  }
+  __syncthreads();
+  conv2_split_rest(a2, b, h, xin2, reinterpret_cast<bf16*>(smem + C12S_X1));
 }
 
 __global__ __launch_bounds__(SP_NT, 4) void k_conv2_dgrad_split(DmlcConv2DgradArgs a) {
@@ -177,6 +250,21 @@ hipError_t dmlc_conv2_fwd_split(const DmlcConv2FwdArgs* a, hipStream_t s) {
   if (a->B % 8) return hipErrorInvalidValue;
   DMLC_LDS_OPTIN(&k_conv2_fwd_split, SP_LDS);
   hipLaunchKernelGGL(k_conv2_fwd_split, dim3(a->B * 2), dim3(SP_NT), SP_LDS, s, *a);
+  return hipGetLastError();
+}
+
+hipError_t dmlc_conv12_fwd_split(const DmlcConv1FwdArgs* a1, const DmlcConv2FwdArgs* a2, unsigned* flags,
+                                 unsigned* err, hipStream_t s) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return hipErrorInvalidValue;
+  }
+  // both workgroups of an image co-resident: one per CU at this LDS size
+  if (a1->B != a2->B || a1->B % 8 || a1->amax || 2 * a1->B > cus || !flags || !err) return hipErrorInvalidValue;
+  DMLC_LDS_OPTIN(&k_conv12_fwd_split, C12S_LDS);
+  hipLaunchKernelGGL(k_conv12_fwd_split, dim3(a1->B * 2), dim3(SP_NT), C12S_LDS, s, *a1, *a2, flags, err);
   return hipGetLastError();
 }
 

@@ -87,6 +87,7 @@ VARIANT_DEFAULTS = {
     "fp8_dgrad": True,         # fp8: the conv2 input gradient on e4m3 too
     "comm_sgd": False,         # data parallel over xGMI: the SGD in the exchange kernel's epilogue
     "xraw_prefetch": True,     # the step's raw images gathered by the previous step's finalizer
+    "fwd12_split": True,       # B <= 128: conv1 + conv2 forward in one launch, two workgroups per image
 }
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
@@ -341,6 +342,12 @@ class FusedCifarEngine:
         # step's rows -- one image load instead of index load -> image load at the head of the step;
         # the host fills it whenever it sets the step (_sync_bidx)
         self.xraw_prefetch = self.fused_fwd and not self.fp8 and self.conv_split == 1 and bool(V["xraw_prefetch"])
+        # B <= 128 (channel-split convs, conv1 in halves): conv1 -> conv2 in ONE launch whose two
+        # workgroups per image swap their pool1 halves through sc1 stores + a flag (cnn_split.hip
+        # k_conv12_fwd_split) -- one launch boundary and the conv2 input's global round trip less
+        self.fwd12_split = (self.conv_split == 2 and self.conv1_split == 2 and not self.fp8
+                            and B * 2 <= cus and local_ <= max(1, ndev_) and bool(V["fwd12_split"]))
+        self.c12_flags = torch.zeros(32 * 2 * B if self.fwd12_split else 1, dtype=torch.int32, device=dev)
         self.wbar = torch.zeros(WBAR_WORDS, dtype=torch.int32, device=dev)   # barrier words + error word
         # pinned host copy of the barrier error word, refreshed by queue_error_copy() behind each
         # chunk of steps (the trainer checks it at every progress point without a device sync)
@@ -449,7 +456,11 @@ class FusedCifarEngine:
     # --- kernels ------------------------------------------------------------------------------
     def _forward(self, idx, counter, period, train=True, logits_out=None):
         o, p = self.ops, self.pv
-        if self.conv_split == 2 and not self.fp8:  # channel-split: B * nsplit workgroups per conv
+        if self.fwd12_split:                       # one launch, two workgroups per image (cnn_split.hip)
+            o.conv12_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
+                         self.am1, self.w2f, p["conv2_bias"], self.p2, self.am2, self.xraw if train else None, False,
+                         self.c12_flags, self.wbar[10 * 32:10 * 32 + 1])
+        elif self.conv_split == 2 and not self.fp8:  # channel-split: B * nsplit workgroups per conv
             o.conv1_fwd_split(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
                               self.am1, self.xraw if train else None, self.conv1_split)
             o.conv2_fwd_split(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)

@@ -383,6 +383,36 @@ def test_fc_chain_launch_matches_three_launch_path(B):
     assert abs(fused.read_stats(10)["loss"] - ref.read_stats(10)["loss"]) < 3e-2 * max(1.0, abs(ref.read_stats(10)["loss"]))
 
 
+@pytest.mark.parametrize("B", [64, 128])
+def test_fused_split_forward_is_bit_identical(B):
+    """B <= 128: conv1 -> conv2 forward as ONE launch whose two workgroups per image swap their pool1
+    halves in-launch (cnn_split.hip k_conv12_fwd_split) against the two channel-split launches: p1,
+    am1, p2, am2, the gradients and the weights after eager + graph-replayed steps are bit-identical
+    (the same conv1 / conv2 split bodies; only the hand-off of the pool1 halves differs)."""
+    data, labels = _synthetic(8 * B, seed=67)
+    kw = dict(seed=68, lr=1e-3, relu_logits=False)
+    fused = FusedCifarEngine(B, data, labels, **kw, variant={"fwd12_split": True})
+    ref = FusedCifarEngine(B, data, labels, **kw, variant={"fwd12_split": False})
+    assert fused.fwd12_split and not ref.fwd12_split and ref.conv_split == 2
+    idx = torch.randperm(8 * B, generator=torch.Generator().manual_seed(7))[:B].to(torch.int32)
+    for explicit in (None, idx):
+        g_ref = ref.compute_gradients(explicit).clone()
+        g_fus = fused.compute_gradients(explicit).clone()
+        torch.cuda.synchronize()
+        fused.check_barriers()
+        for name in ("p1", "am1", "p2", "am2"):
+            assert torch.equal(getattr(fused, name), getattr(ref, name)), name
+        assert torch.equal(g_fus, g_ref)
+    for eng in (fused, ref):
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(9)
+    torch.cuda.synchronize()
+    fused.check_barriers()
+    assert torch.equal(fused.master, ref.master)
+    assert int(fused.c12_flags.abs().sum()) == 0          # every flag re-armed
+
+
 @pytest.mark.parametrize("B", [64, 128, 160, 256])
 def test_dgrad_in_fc_chain_is_bit_identical(B):
     """The conv2 input gradient inside the fc chain launch (each workgroup's image -- at B <= 128 each
