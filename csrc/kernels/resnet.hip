@@ -32,6 +32,20 @@ constexpr int RT = 256;
 // streaming (nt) stores for the activations / gradients / slabs the next launches read (common.h:
 // fewer dirty L2 lines to write back at every one of the ~58 kernel boundaries): 0.695 -> 0.682 ms
 constexpr bool kNtRn = kNtDefault;
+// activation stores (z, a, g_y -> the next launch): write-through (common.h st_out16 / st_out8) unless
+// -DDMLC_RN_NT (the r3 streaming form); the fp32 slabs stay streaming (4-B write-through stores are
+// one fabric write each)
+#ifdef DMLC_RN_NT
+DEV void st_rn16(void* base, uint32_t off, const uint4& v) {
+  st_maybe_nt<kNtRn>(reinterpret_cast<uint4*>(reinterpret_cast<char*>(base) + off), v);
+}
+DEV void st_rn8(void* base, uint32_t off, const bf16x4& v) {
+  st_maybe_nt<kNtRn>(reinterpret_cast<bf16x4*>(reinterpret_cast<char*>(base) + off), v);
+}
+#else
+DEV void st_rn16(void* base, uint32_t off, const uint4& v) { st_out16(base, off, v); }
+DEV void st_rn8(void* base, uint32_t off, const bf16x4& v) { st_out8(base, off, __builtin_bit_cast(uint2, v)); }
+#endif
 constexpr int NSLOT = DMLC_RN_NSLOT;          // fp64 statistics copies per layer: [NSLOT][2][64]
 constexpr double BN_EPS = 1e-3;
 
@@ -308,7 +322,7 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
         }
         const uint4 o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         reinterpret_cast<uint4*>(xs)[e] = o;
-        if (ok) st_maybe_nt<kNtRn>(ao + (iy * HIN + ix) * C8 + c8, o);
+        if (ok) st_rn16(ao, (uint32_t)((iy * HIN + ix) * C8 + c8) * 16, o);
       }
     }
   }
@@ -341,7 +355,7 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
 #pragma unroll
   for (int i = 0; i < F::NPT; ++i) {
     const int px = 16 * (pt0 + F::WPC * i) + li;
-    st_maybe_nt<kNtRn>(reinterpret_cast<bf16x4*>(zo + px * COUT + 16 * ct + 4 * g), pack4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
+    st_rn8(zo, (uint32_t)(px * COUT + 16 * ct + 4 * g) * 2, pack4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s1[r] += acc[i][r]; s2[r] += acc[i][r] * acc[i][r]; }
   }
@@ -516,7 +530,7 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
         s1[r] += gy[r];
         s2[r] = __builtin_fmaf(gy[r] * (zv4[r] - mean[r]), rstd[r], s2[r]);   // pinned (bitwise across kernels)
       }
-      st_maybe_nt<kNtRn>(reinterpret_cast<bf16x4*>(gyo + px * CIN + c0), pack4(gy[0], gy[1], gy[2], gy[3]));
+      st_rn8(gyo, (uint32_t)(px * CIN + c0) * 2, pack4(gy[0], gy[1], gy[2], gy[3]));
     }
     if (c + EC < D::NPT) {
 #pragma unroll
@@ -927,7 +941,7 @@ __global__ __launch_bounds__(RT, 2) void k_rn_bwd_img(DmlcRnDgradArgs a, DmlcRnW
         s1[r] += gy[r];
         s2[r] = __builtin_fmaf(gy[r] * (zv4[r] - mean[r]), rstd[r], s2[r]);   // pinned (bitwise across kernels)
       }
-      st_maybe_nt<kNtRn>(reinterpret_cast<bf16x4*>(gyo + px * CIN + c0), pack4(gy[0], gy[1], gy[2], gy[3]));
+      st_rn8(gyo, (uint32_t)(px * CIN + c0) * 2, pack4(gy[0], gy[1], gy[2], gy[3]));
     }
     if (c + EC < D::NPT) {
 #pragma unroll
