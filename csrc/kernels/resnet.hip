@@ -33,8 +33,8 @@ constexpr int RT = 256;
 // fewer dirty L2 lines to write back at every one of the ~58 kernel boundaries): 0.695 -> 0.682 ms
 constexpr bool kNtRn = kNtDefault;
 // activation stores (z, a, g_y -> the next launch): write-through (common.h st_out16 / st_out8) unless
-// -DDMLC_RN_NT (the r3 streaming form); the fp32 slabs stay streaming (4-B write-through stores are
-// one fabric write each)
+// -DDMLC_RN_NT (the r3 streaming form); the fp32 slabs stay streaming (their 4-B write-through
+// stores are one fabric write each: 375 vs 401 k images/s, r5 same-box A/B)
 #ifdef DMLC_RN_NT
 DEV void st_rn16(void* base, uint32_t off, const uint4& v) {
   st_maybe_nt<kNtRn>(reinterpret_cast<uint4*>(reinterpret_cast<char*>(base) + off), v);
