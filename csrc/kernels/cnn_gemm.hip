@@ -212,6 +212,8 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
     // nvalid == N, checked by the binding)
     const float f = lr_sched(G.lr0, G.decay, G.decay_steps, G.staircase, G.warmup, st) * G.grad_scale;
     bf16* S = reinterpret_cast<bf16*>(P.S) + (((st + 1) & 1) ? P.s_par : 0);
+    void* cbase = const_cast<void*>(uni(P.C));   // buffer descriptors live in SGPRs
+    void* sbase = const_cast<void*>(uni(S));
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (!ok[u]) continue;
@@ -220,9 +222,10 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
       const float4 g = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
       float4 v = wv[u];
       v.x -= f * g.x; v.y -= f * g.y; v.z -= f * g.z; v.w -= f * g.w;
-      const f32x4 vo = {v.x, v.y, v.z, v.w};
-      st_maybe_nt<kNtX>(reinterpret_cast<f32x4*>(reinterpret_cast<float*>(P.C) + q), vo);
-      st_maybe_nt<kNtX>(reinterpret_cast<bf16x4*>(S + q), pack4(v.x, v.y, v.z, v.w));
+      // write-through: no dirty master / shadow lines for the kernel-boundary write-back (as the fc
+      // chain's epilogue, fc_common.h)
+      st_out16(cbase, (uint32_t)(q * 4), __builtin_bit_cast(uint4, make_float4(v.x, v.y, v.z, v.w)));
+      st_out8(sbase, (uint32_t)(q * 2), __builtin_bit_cast(uint2, pack4(v.x, v.y, v.z, v.w)));
     }
     DMLC_STAMP(DMLC_TK_GEMM, 2);
     return;

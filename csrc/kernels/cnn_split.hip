@@ -47,8 +47,8 @@ DEV void pool_emit_c(const bf16* img, bf16* out, uint8_t* am, int c0, int tid, b
       st_out8(am, (uint32_t)(q * 64 + c0 + c * 8), make_uint2(alo, ahi));
       *reinterpret_cast<uint4*>(pad_lds + swzpad((py + 2) * (HO + 4) + px + 2, (c0 >> 3) + c)) = o;
     } else {
-      st_maybe_nt<kNtX>(reinterpret_cast<uint4*>(out + q * 64 + c0 + c * 8), o);
-      st_maybe_nt<kNtX>(reinterpret_cast<uint2*>(am + q * 64 + c0 + c * 8), make_uint2(alo, ahi));
+      st_out16(out, (uint32_t)(q * 64 + c0 + c * 8) * 2, o);           // write-through (common.h)
+      st_out8(am, (uint32_t)(q * 64 + c0 + c * 8), make_uint2(alo, ahi));
     }
   }
 }

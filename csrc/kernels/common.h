@@ -162,6 +162,14 @@ constexpr bool kWtStores = false;
 #else
 constexpr bool kWtStores = true;
 #endif
+// A pointer the compiler cannot prove wave-uniform, made so (buffer descriptors live in SGPRs; a
+// VGPR descriptor makes hipcc wrap every buffer op in a waterfall loop -- guide T20)
+DEV const void* uni(const void* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  // (through uint32_t: readfirstlane returns int, which would sign-extend into the high word)
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo);
+}
 DEV void st_out16(void* base, uint32_t byte_off, const uint4& v) {
   if constexpr (kWtStores)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), buf_rsrc(base), byte_off, 0, kSC1);

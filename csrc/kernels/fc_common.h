@@ -89,13 +89,6 @@ DEV void consume(const Seam& s, unsigned* err) {
   __syncthreads();
 }
 
-// a pointer the compiler cannot prove wave-uniform, made so (buffer descriptors live in SGPRs; a
-// VGPR descriptor makes hipcc wrap every buffer op in a waterfall loop -- guide T20)
-DEV const void* uni(const void* p) {
-  const uint64_t v = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return reinterpret_cast<const void*>(((uint64_t)hi << 32) | lo);
-}
 DEV uint4 ld16(rsrc_t r, uint32_t off) {      // sc1 16-B load (hand-off bytes)
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSC1));
 }

@@ -172,7 +172,7 @@ DEV void conv2_dgrad_split_image(const DmlcConv2DgradArgs& a, int b, int h, char
       const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
       const bf16x8 v = to_bf16x8(o[k]);
       *reinterpret_cast<bf16x8*>(dyp + swzpad((y + 2) * 16 + x + 2, c)) = v;
-      if ((c >> 2) == h) st_maybe_nt<kNtX>(reinterpret_cast<bf16x8*>(dy2 + (y * 12 + x) * 64 + c * 8), v);
+      if ((c >> 2) == h) st_out16(dy2, (uint32_t)((y * 12 + x) * 64 + c * 8) * 2, __builtin_bit_cast(uint4, v));
     }
   }
   lds_barrier();   // dyp published (dy2's global stores need not drain); dp2 / am2 reads done
@@ -187,7 +187,7 @@ DEV void conv2_dgrad_split_image(const DmlcConv2DgradArgs& a, int b, int h, char
   bf16* dp1 = reinterpret_cast<bf16*>(a.dp1) + (size_t)b * 9216 + 32 * h;
   for (int s = tid; s < 144 * 4; s += SP_NT) {
     const int p = s >> 2, c = s & 3;
-    st_maybe_nt<kNtX>(reinterpret_cast<bf16x8*>(dp1 + p * 64 + c * 8), lds_b128(img + swzc<4>(p, c)));
+    st_out16(dp1, (uint32_t)(p * 64 + c * 8) * 2, __builtin_bit_cast(uint4, lds_b128(img + swzc<4>(p, c))));
   }
   DMLC_STAMP(DMLC_TK_DGRAD, 3);
 }
