@@ -565,7 +565,7 @@ class FusedCifarEngine:
     def barriers_in_use(self) -> bool:
         """The wgrad launch meets at sub-grid barriers: apply mode (single-GPU SGD) or the in-launch
         conv-slab reduction (data parallel / compute_gradients)."""
-        return bool(self.wgrad_apply or self._grad_in_launch or self.fc_fused)
+        return bool(self.wgrad_apply or self._grad_in_launch or self.fc_fused or self.fwd12_split)
 
     def queue_error_copy(self):
         """Enqueue a copy of the barrier error word into pinned host memory (stream-ordered: valid once
@@ -588,7 +588,8 @@ class FusedCifarEngine:
             if e & 1:
                 parts.append(f"k_wgrad ({mode} mode): a sub-grid barrier timed out; rerun with DMLC_WGRAD_SGD=0")
             if e & 2:
-                parts.append("k_fc_chain: a hand-off wait timed out; rerun with DMLC_FC_FUSED=0")
+                parts.append("k_fc_chain / k_conv12_fwd_split: a hand-off wait timed out; rerun with "
+                             "DMLC_FC_FUSED=0 / variant fwd12_split=0")
             raise RuntimeError("; ".join(parts) + f" (blocks not co-resident, error word {e})")
 
     def _allreduce(self, t: torch.Tensor):
