@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Per-phase timing of every fused-step kernel from in-kernel s_memrealtime stamps (100 MHz).
 
-  DMLC_TIMING=1 python tools/ktiming.py [--batch 256]
-Builds/loads the diagnostic library (libdmlc_hip_timing.so), runs a few eager steps, and prints for
+  DMLC_TIMING=1 python tools/ktiming.py [--batch 256] [--eager]
+Builds/loads the diagnostic library (libdmlc_hip_timing.so), replays a 2-step graph chain (bench.py's
+launch pattern; --eager: one eager step), and prints for
 each kernel: span (first entry -> last stamp), and per slot the median / max over blocks of the time
 since the block's own entry stamp.  Slot meanings are documented at each DMLC_STAMP call site.
 """
@@ -31,8 +32,11 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--raw", default="", help="comma list of kernel names whose per-block stamps (us since "
                     "the step's first stamp, -1 = not stamped) are dumped too, as raw_<name>")
-    ap.add_argument("--graph", action="store_true",
-                    help="time the second step of a 2-step graph chain (kernels back to back, as in bench.py)")
+    ap.add_argument("--eager", action="store_true",
+                    help="time an eager step instead of the second step of a 2-step graph chain (eager "
+                         "launches leave host gaps: the first kernel's workgroups then enter up to ~4 us "
+                         "apart, 0.4 us in the graph)")
+    ap.add_argument("--graph", action="store_true", help="(the default; kept for old command lines)")
     a = ap.parse_args()
     g = torch.Generator().manual_seed(0)
     data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
@@ -43,7 +47,7 @@ def main():
     for _ in range(5):
         eng.step()
     torch.cuda.synchronize()
-    if a.graph:
+    if not a.eager:
         eng.capture(steps_per_graph=2)
         eng.run(4)
         torch.cuda.synchronize()
