@@ -650,9 +650,10 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   a.sgd = make_sgd(DMLC_SGD_ARGS);
   a.apply = 1;
   a.bar = reinterpret_cast<unsigned int*>(bar.data_ptr<int>());
-  // conv1 blocks help reduce the conv2 slabs only above B = 128: same-box A/B (profiles/
-  // r5_wgrad_helpers_ab.txt) 75.0 vs 75.7 us/step at B=256 with them, 65.8 vs 67.2 at B=128 without
-  a.helpers = a.w1.B > 128 ? 1 : 0;
+  // conv1 blocks help reduce the conv2 slabs unless they also carry the fc dW tiles at B <= 128 (then
+  // they arrive too late: 65.8 vs 67.2 us at B=128 without helpers, profiles/r5_wgrad_helpers_ab.txt;
+  // with helpers 75.0 vs 75.7 at B=256)
+  a.helpers = (a.w1.B > 128 || !fc_acts.has_value()) ? 1 : 0;
   a.fc_in_launch = 0;
   memset(&a.fc, 0, sizeof(a.fc));
   if (fc_acts.has_value()) {

@@ -80,7 +80,7 @@ VARIANT_DEFAULTS = {
     "split_fwd": False,        # conv1 and conv2 forward as two launches (bitwise reference of conv12_fwd)
     "fc_fused": None,          # the persistent fc chain (B <= 256, one rank per GPU); env DMLC_FC_FUSED=0 off
     "fc_dgrad": None,          # conv2 dgrad inside the fc chain (default: on; two workgroups per image at B <= 128)
-    "fc_dw_in_wgrad": None,    # fc dW tiles in the wgrad launch (default: dgrad not in the chain, or B <= 128)
+    "fc_dw_in_wgrad": None,    # fc dW tiles in the wgrad launch (default: only when the dgrad is not in the chain)
     "fc1_epilogue": True,      # single GPU: the fc1 update in the dW1 epilogue
     "wgrad_sgd": True,         # in-launch SGD / slab reduction of the wgrad launch; env DMLC_WGRAD_SGD=0 off
     "wgrad_sgd_fp8": False,    # the same for --dtype fp8 (bit-identical, measured 1.4 % slower at B=1024)
@@ -369,11 +369,15 @@ class FusedCifarEngine:
         # r4_v7_fc_dgrad_dw_ab.txt, us/step): chain dgrad off: dW in chain 81.8, in wgrad 80.4; chain
         # dgrad on: dW in chain 79.8, in wgrad 80.2 -- so by default the dW tiles move to the wgrad
         # launch only when the dgrad is not in the chain.  Variant fc_dw_in_wgrad forces it.
-        # At B <= 128 (the chain's split dgrad) the dW tiles are better in the wgrad launch too: 64.2-64.4
-        # vs 65.6-65.9 us/step at B = 128 (profiles/r5_fc_split_dgrad_b128_ab.txt).
+        # At B <= 128 (the chain's split dgrad) the dW tiles once measured better in the wgrad launch
+        # (64.2-64.4 vs 65.6-65.9 us at B = 128, profiles/r5_fc_split_dgrad_b128_ab.txt) -- with the
+        # conv1 blocks then too busy to help reduce the conv2 slabs.  With the tiles in the chain the
+        # conv1 blocks help again (torch_ops.cpp: helpers whenever they carry no fc tiles): B = 32 71.6
+        # -> 64.0, 64 65.3 -> 62.7, 96 65.8 -> 64.7, 112 67.5 -> 65.5, 128 63.6 -> 63.6 us
+        # (profiles/r5_dw_placement_helpers_ab.txt).
         fdw = V["fc_dw_in_wgrad"]
         self.fc_dw_in_wgrad = (self.fc_fused and self.wgrad_apply
-                               and (bool(fdw) if fdw is not None else (not self.fc_dgrad or B <= 128)))
+                               and (bool(fdw) if fdw is not None else not self.fc_dgrad))
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
                                                                         s_par=FC1_NUMEL)
