@@ -105,6 +105,74 @@ def test_dp_matches_mean_of_rank_gradients(tmp_path, world, graph, comm_dtype, a
         assert torch.equal(rs[0]["flat"], want)           # same sums, same order, same kernels
 
 
+def _rank_node(rank, world, port, out, B, steps, lockfile):
+    """One rank of a node rehearsal: the engine is told it has a GPU of its own (LOCAL_WORLD_SIZE=1),
+    so it takes the paths an 8-GPU node runs -- the persistent fc chain with the conv2 dgrad, the
+    wgrad launch reducing the conv slabs into the flat gradient, the split forward at B <= 128 --
+    and the ranks take turns on the shared card (a file lock around each rank's GPU work) so every
+    persistent launch has the chip to itself, as on its own GPU."""
+    os.environ["LOCAL_WORLD_SIZE"] = "1"
+    sys.path.insert(0, REPO)
+    import datetime
+    import fcntl
+    import torch.distributed as dist
+    import dmlc  # noqa: F401
+    from dmlc.engine.fused import FusedCifarEngine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    x, y = _data()
+    eng = FusedCifarEngine(B, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
+                           relu_logits=False, comm_dtype="fp32", allreduce="rccl", dp_schedule="serial",
+                           staircase=False)
+    flags = {"fc_fused": eng.fc_fused, "fc_dgrad": eng.fc_dgrad, "wgrad_reduce": eng.wgrad_reduce,
+             "fwd12_split": eng.fwd12_split}
+    n = eng.master.numel()
+
+    def gpu(fn):
+        with open(lockfile, "a") as f:
+            fcntl.flock(f, fcntl.LOCK_EX)
+            try:
+                fn()
+                torch.cuda.synchronize()
+            finally:
+                fcntl.flock(f, fcntl.LOCK_UN)
+
+    for _ in range(steps):                     # _serial_dp_step, with the GPU turns made explicit
+        gpu(eng._seg_compute_ab)
+        eng.check_barriers()
+        eng._allreduce(eng.grad[:n])
+        gpu(eng._seg_apply)
+        eng.host_step += 1
+    torch.save({"flat": eng.flat_params(), "step": eng.global_step(), "flags": flags,
+                "batches": [eng.batch_indices(s) for s in range(steps)]}, os.path.join(out, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,B", [(2, 32), (2, 160), (4, 64)])
+def test_dp_node_kernels_match_mean_of_rank_gradients(tmp_path, world, B):
+    """The data-parallel step with the kernels a node with one GPU per rank runs (fc chain + dgrad,
+    reduce-mode wgrad with 1/(B*W) loss scale, split forward) -- which ranks sharing one GPU cannot
+    run concurrently -- rehearsed with the ranks taking turns on the card, 6 steps, against the exact
+    replay of the DP semantics on one engine with the same kernels (_dp_reference, fc chain on)."""
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    steps = 6
+    mp.spawn(_rank_node, args=(world, free_port(), str(tmp_path), B, steps, str(tmp_path / "gpu.lock")),
+             nprocs=world, join=True)
+    rs = [torch.load(tmp_path / f"r{k}.pt", weights_only=True) for k in range(world)]
+    f = rs[0]["flags"]
+    assert f["fc_fused"] and f["fc_dgrad"] and f["wgrad_reduce"], f
+    assert f["fwd12_split"] == (B <= 128), f
+    assert all(r["step"] == steps for r in rs)
+    for r in rs[1:]:
+        assert torch.equal(rs[0]["flat"], r["flat"])      # replicas identical
+    init, want = _dp_reference(world, B, steps, [r["batches"] for r in rs], "fp32", "rccl", fc_fused=True)
+    d_dp, d_ref = rs[0]["flat"] - init, want - init
+    rel = float((d_dp - d_ref).norm() / d_ref.norm())
+    assert rel <= 1e-5, rel
+
+
 def test_dp_reference_union_batch_consistency():
     """The generated order makes the W ranks' batches of a step exactly the union batch a single
     process with batch W*B trains on (data/order.py), in rank order."""
