@@ -257,7 +257,7 @@ static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10
   a.w1.xraw = xraw_ptr(xraw, B);
   a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr();
   a.w2.partb2 = partb2.data_ptr<float>(); a.w2.g2 = (int)g2; a.w2.B = (int)B;
-  a.apply = 0; a.bar = nullptr; a.helpers = 0;
+  a.apply = 0; a.bar = nullptr; a.helpers = 0; a.fc_done = 0;
   memset(&a.sgd, 0, sizeof(a.sgd));
   return a;
 }
@@ -420,7 +420,7 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
               const Tensor& gb3, bool fuse_sgd, at::ArrayRef<double> sched, int64_t nvalid, const Tensor& step,
               const c10::optional<Tensor>& step_copy, const Tensor& sync, const Tensor& err, bool dw_tasks,
               const c10::optional<Tensor>& am2, const c10::optional<Tensor>& w2d, const c10::optional<Tensor>& dp1,
-              const c10::optional<Tensor>& dy2) {
+              const c10::optional<Tensor>& dy2, const c10::optional<Tensor>& fc2n) {
   const int64_t B = p2.size(0);
   TORCH_CHECK(B >= 16 && B <= 256 && B % 16 == 0, "fc_chain: batch must be a multiple of 16 in [16, 256]");
   check(p2, "p2", at::kBFloat16, {B, 2304});
@@ -471,6 +471,17 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
   a.gb1 = gb1.data_ptr<float>(); a.gb2 = gb2.data_ptr<float>(); a.gb3 = gb3.data_ptr<float>();
   a.fuse_sgd = fuse_sgd ? 1 : 0;
   a.dw_tasks = dw_tasks ? 1 : 0;
+  if (fc2n.has_value()) {
+    // every fc parameter's SGD in the dW tiles' epilogues (fuse_sgd 2, as the wgrad launch runs them):
+    // gw2 / gw3 / gb1..3 are then the fp32 MASTER views and w2t / w3t / w3d + fc2n the bf16 shadows the
+    // epilogues rewrite (the head has read them before the dW tiles' seam)
+    TORCH_CHECK(fuse_sgd && dw_tasks, "fc_chain: the fc SGD in the chain needs fuse_sgd and the dW tiles");
+    check(*fc2n, "fc2n", at::kBFloat16, {384, 192});
+    a.fuse_sgd = 2;
+    a.mw2 = gw2.data_ptr<float>(); a.mw3 = gw3.data_ptr<float>();
+    a.mb1 = gb1.data_ptr<float>(); a.mb2 = gb2.data_ptr<float>(); a.mb3 = gb3.data_ptr<float>();
+    a.fc2n = fc2n->data_ptr(); a.fc2t = w2t.data_ptr(); a.fc3t = w3t.data_ptr(); a.fc3d = w3d.data_ptr();
+  }
   a.lr0 = (float)sched[0]; a.decay = (float)sched[1]; a.decay_steps = (float)sched[2];
   a.staircase = sched[3] != 0.0; a.warmup = (float)sched[4]; a.grad_scale = (float)sched[5];
   a.step = step.data_ptr<int64_t>();
@@ -640,7 +651,7 @@ void sgd(DMLC_SGD_PARAMS) {
 void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
                int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& p1, const Tensor& dy2,
                int64_t groups2, const Tensor& xraw, const Tensor& bar, DMLC_SGD_PARAMS,
-               const c10::optional<at::TensorList> fc_acts) {
+               const c10::optional<at::TensorList> fc_acts, bool fc_sgd_done) {
   DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
                                groups2, xraw);
   TORCH_CHECK((mode == 0 && fc1_fused && step_rd.has_value() && roles == 0 && finalize &&
@@ -655,6 +666,8 @@ void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
   // with helpers 75.0 vs 75.7 at B=256)
   a.helpers = (a.w1.B > 128 || !fc_acts.has_value()) ? 1 : 0;
   a.fc_in_launch = 0;
+  a.fc_done = fc_sgd_done ? 1 : 0;             // the fc chain applied every fc SGD: no fc roles here
+  TORCH_CHECK(!fc_sgd_done || (mode == 0 && !fc_acts.has_value()), "wgrad_sgd: fc_sgd_done is the chain's mode-0 step");
   memset(&a.fc, 0, sizeof(a.fc));
   if (fc_acts.has_value()) {
     // the fc weight-gradient tiles + every fc SGD run in this launch (fc_common.h): fc_acts = the fc
@@ -723,7 +736,7 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(h!) loss_part, Tensor(i!) correct_part, Tensor(j!) dp2, Tensor(k!) gw1, Tensor(l!) gw2, "
         "Tensor(m!) gw3, Tensor(n!) gb1, Tensor(o!) gb2, Tensor(p!) gb3, bool fuse_sgd, float[] sched, "
         "int nvalid, Tensor step, Tensor(q!)? step_copy, Tensor(r!) sync, Tensor(s!) err, bool dw_tasks=True, "
-        "Tensor? am2=None, Tensor? w2d=None, Tensor(t!)? dp1=None, Tensor(u!)? dy2=None) -> ()");
+        "Tensor? am2=None, Tensor? w2d=None, Tensor(t!)? dp1=None, Tensor(u!)? dy2=None, Tensor(v!)? fc2n=None) -> ()");
   m.def("wgrad_sgd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor p1, Tensor dy2, int groups2, Tensor xraw, Tensor(z!) bar, "
         "Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor(r!) part1, Tensor(s!) partb1, "
@@ -733,7 +746,7 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
         "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
         "bool fc1_fused=False, Tensor? step_rd=None, Tensor(v!)? xnext=None, Tensor? xdata=None, "
-        "Tensor[]? fc_acts=None) -> ()");
+        "Tensor[]? fc_acts=None, bool fc_sgd_done=False) -> ()");
   m.def("sgd(Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor part1, Tensor partb1, "
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "

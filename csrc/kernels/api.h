@@ -281,6 +281,7 @@ struct DmlcWgradArgs {
   // fc_common.h) with every fc parameter's SGD in their epilogues (fc.fuse_sgd = 2): no fc SGD roles
   int fc_in_launch;
   DmlcFcArgs fc;
+  int fc_done;              // apply mode: the fc chain already applied every fc SGD (fuse_sgd 2): no fc roles
 };
 
 hipError_t dmlc_conv1_fwd(const DmlcConv1FwdArgs* a, hipStream_t s);

@@ -464,7 +464,7 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
   const float lr = lr_of(s, step);
   // reduce-only (data parallel): conv grads only; fc_in_launch: the fc parameters are updated in
   // the dW tiles' epilogues (below, after this function)
-  const int nfc = s.mode == 1 || A.fc_in_launch ? 0 : fc_role_count(s);
+  const int nfc = s.mode == 1 || A.fc_in_launch || A.fc_done ? 0 : fc_role_count(s);
   for (int r = grp; r < nfc; r += n) {
     fc_role(s, r, lr, step, lds, tid);
     lds_barrier();                             // the fc2 transpose tile is reused by the next role

@@ -88,6 +88,7 @@ VARIANT_DEFAULTS = {
     "comm_sgd": False,         # data parallel over xGMI: the SGD in the exchange kernel's epilogue
     "xraw_prefetch": True,     # the step's raw images gathered by the previous step's finalizer
     "fwd12_split": True,       # B <= 128: conv1 + conv2 forward in one launch, two workgroups per image
+    "fc_sgd_in_chain": None,   # single GPU, dW tiles in the fc chain: every fc SGD in their epilogues (default B < 256)
 }
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
@@ -378,6 +379,15 @@ class FusedCifarEngine:
         fdw = V["fc_dw_in_wgrad"]
         self.fc_dw_in_wgrad = (self.fc_fused and self.wgrad_apply
                                and (bool(fdw) if fdw is not None else not self.fc_dgrad))
+        # ... and with the tiles in the chain, the chain can apply every fc SGD in their epilogues (fc2 /
+        # fc3 / fc biases too, as the wgrad launch does when it runs them): the wgrad launch's conv1
+        # blocks then have no fc SGD roles before their conv1 reduction and conv2 help, while the
+        # chain's dW2 / dW3 tiles (whose images' dgrads end the chain) carry the transposed-shadow
+        # epilogues.  Same-box A/B (profiles/r5_fc_sgd_in_chain_ab.txt): B = 64 / 128 / 160 / 192 / 224
+        # -0.9 / -0.3 / -0.5 / -0.9 / -0.7 us, B = 256 +0.9 us -- on below B = 256.
+        fsc = V["fc_sgd_in_chain"]
+        self.fc_sgd_in_chain = (self.fc_fused and self.wgrad_apply and not self.fc_dw_in_wgrad
+                                and (bool(fsc) if fsc is not None else B < 256))
         self._fc_bwd_sgd = dict(fb, C=[fb["C"][0], p["full_weight_1"]] + fb["C"][2:],
                                 params=fb["params"][:14] + _gemm_params(2304, 384, B, 2304, 0, 384, 0, 384, 4,
                                                                         s_par=FC1_NUMEL)
@@ -513,15 +523,18 @@ class FusedCifarEngine:
         self._fc_src = None
         p, gv = self.pv, self.gv
         sched = [self.lr0, self.decay, self.decay_steps, 1.0 if self.staircase else 0.0, self.warmup, 1.0]
+        all_sgd = fused_sgd and self.fc_sgd_in_chain
+        g = p if all_sgd else gv                 # every fc SGD here: the master views, else the gradients
         self.ops.fc_chain(self.p2.view(self.B, 2304), self.fc1n, self.h1part8, p["full_bias_1"], self.fc2t,
                           p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d, self.labels, idx, counter, period,
                           1.0 / (self.Bv * self.world_size), self.relu_logits, self.h1, self.h2, self.dl, self.dh1,
                           self.dh2, self.loss_part, self.correct_part, self.dp2.view(self.B, 2304),
-                          p["full_weight_1"] if fused_sgd else gv["full_weight_1"], gv["full_weight_2"],
-                          gv["full_weight_3"], gv["full_bias_1"], gv["full_bias_2"], gv["full_bias_3"], fused_sgd,
+                          p["full_weight_1"] if fused_sgd else gv["full_weight_1"], g["full_weight_2"],
+                          g["full_weight_3"], g["full_bias_1"], g["full_bias_2"], g["full_bias_3"], fused_sgd,
                           sched, self.Bv, self.step_t, self.step_sgd, self.fc_sync, self.wbar[10 * 32:10 * 32 + 1],
                           not (fused_sgd and self.fc_dw_in_wgrad),
-                          *((self.am2, self.w2d, self.dp1, self.dy2) if self.fc_dgrad else ()))
+                          *((self.am2, self.w2d, self.dp1, self.dy2) if self.fc_dgrad else (None, None, None, None)),
+                          self.fc2n if all_sgd else None)
         self._dgrad_done = self.fc_dgrad
 
     def _conv_backward(self, src=None, apply: bool = False, reduce: bool = False):
@@ -546,7 +559,7 @@ class FusedCifarEngine:
             o.wgrad_sgd(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1, self.p1, self.dy2,
                         self.groups2, self.xraw, self.wbar,
                         *(self._sgd_args(mode=0, fc1_fused=True) if apply else self._sgd_args(mode=1)),
-                        fc_acts=fc_acts)
+                        fc_acts=fc_acts, fc_sgd_done=bool(apply and self.fc_sgd_in_chain))
             return
         o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
                 self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw)

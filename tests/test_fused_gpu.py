@@ -290,7 +290,7 @@ def test_fc1_update_in_gemm_epilogue_is_bit_identical(B):
     assert torch.equal(ref.forward_logits(idx), fused.forward_logits(idx))
 
 
-@pytest.mark.parametrize("B", [16, 100, 128, 256, 1024])
+@pytest.mark.parametrize("B", [16, 100, 128, 192, 256, 1024])
 def test_sgd_in_wgrad_launch_is_bit_identical(B):
     """Single GPU: the merged weight-gradient launch also runs the SGD (cnn_wgrad.hip apply mode:
     sub-grid barriers per slab family, each block reduces its share of the slabs in the SGD kernel's
@@ -411,6 +411,29 @@ def test_fused_split_forward_is_bit_identical(B):
     fused.check_barriers()
     assert torch.equal(fused.master, ref.master)
     assert int(fused.c12_flags.abs().sum()) == 0          # every flag re-armed
+
+
+@pytest.mark.parametrize("B", [64, 256])
+def test_fc_sgd_in_chain_is_bit_identical(B):
+    """Every fc SGD in the fc chain's dW tile epilogues (fc2 / fc3 / biases too, variant fc_sgd_in_chain)
+    vs as SGD roles of the wgrad launch: parameters, every shadow and the stats bit for bit after eager
+    and graph-replayed steps."""
+    data, labels = _synthetic(8 * B, seed=73)
+    kw = dict(seed=74, lr=1e-3, relu_logits=False)
+    on = FusedCifarEngine(B, data, labels, **kw, variant={"fc_sgd_in_chain": True})
+    off = FusedCifarEngine(B, data, labels, **kw, variant={"fc_sgd_in_chain": False})
+    assert on.fc_sgd_in_chain and not off.fc_sgd_in_chain
+    for eng in (on, off):
+        eng.step()
+        eng.capture(steps_per_graph=4)
+        eng.run(6)
+    torch.cuda.synchronize()
+    on.check_barriers()
+    assert torch.equal(on.master, off.master)
+    for name in ("fc2t", "fc2n", "fc3t", "fc3d", "w1f", "w2f", "w2d"):
+        assert torch.equal(getattr(on, name), getattr(off, name)), name
+    assert torch.equal(on.fc1n_current(), off.fc1n_current())
+    assert torch.equal(on.stats, off.stats)
 
 
 @pytest.mark.parametrize("B", [64, 128, 160, 256])
