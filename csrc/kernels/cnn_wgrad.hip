@@ -510,7 +510,7 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
   }
 #ifndef DMLC_C1_BIAS_ON_1
   // the conv1 bias on the LAST conv1 block: the first ones also run the fc SGD roles (block 1, which
-  // had both, ended the launch ~1 us after the rest at B=256, profiles/r5_final2_ktiming_b256_graph.json)
+  // had both, ended the launch ~1 us after the rest at B=256, profiles/r5_ktiming_b256_wgrad_raw.json)
   if (grp == n - 1) conv_bias(s, 0, lr, lds, tid, true);
 #else
   if (grp == (n > 1 ? 1 : 0)) conv_bias(s, 0, lr, lds, tid, true);
