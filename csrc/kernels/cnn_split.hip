@@ -197,14 +197,18 @@ __global__ __launch_bounds__(SP_NT, 1) void k_conv12_fwd_split(DmlcConv1FwdArgs 
   unsigned* theirs = flags + 32 * (2 * b + (h ^ 1));
   if (tid == 0) {
     __hip_atomic_store(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool seen = true;
     for (unsigned it = 0; __hip_atomic_load(theirs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u; ++it) {
       if (it > (1u << 20)) {
         __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        seen = false;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __hip_atomic_store(theirs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed for the next launch
+    // re-armed for the next launch -- only after a successful wait: a timed-out waiter must not clear
+    // a flag its late partner has not raised yet (the engine re-zeroes every flag after an error)
+    if (seen) __hip_atomic_store(theirs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   // the partner's 32 channels: 144 pixels x 4 chunks of 16 B

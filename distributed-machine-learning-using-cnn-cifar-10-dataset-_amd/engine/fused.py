@@ -17,12 +17,13 @@ their inputs from device memory:
                  order and applies the update + bf16 shadows; the stats, global_step and the next
                  step's batch rows too)
 
-At B <= 128 launch 1 becomes conv1_fwd_split + conv2_fwd_split (cnn_split.hip, two or four
-workgroups per image so a small batch fills the 256 CUs), the fc chain's 256 workgroups run the conv2
-input gradient two per image (cnn_split.hip's channel halves) and the fc weight-gradient tiles run in
-the wgrad launch: four launches.  B > 256 (and ranks sharing one GPU) use the three-launch fc path (grouped fc1 GEMM,
-head, grouped backward GEMM).  The fp8 path (BASELINE config 5) runs conv1 and the fp8 conv2 forward
-as two launches, the fp8 conv2 dgrad as its own launch and the SGD as its own launch.
+At B <= 128 launch 1 is k_conv12_fwd_split (cnn_split.hip: conv1 -> pool1 -> conv2 -> pool2 in ONE
+launch with two workgroups per image that swap their pool1 channel halves through write-through
+stores + a flag, so a small batch fills the 256 CUs) and the fc chain's 256 workgroups run the conv2
+input gradient two per image (cnn_split.hip's channel halves): three launches as well.  B > 256 (and
+ranks sharing one GPU) use the three-launch fc path (grouped fc1 GEMM, head, grouped backward GEMM).
+The fp8 path (BASELINE config 5) runs conv1 and the fp8 conv2 forward as two launches, the fp8 conv2
+dgrad as its own launch and the SGD as its own launch.
 
 Data parallel (N > 1): the wgrad launch reduces the conv slabs into the flat gradient instead of
 applying them, then the gradient is exchanged and applied -- serial schedule: one all-reduce of the
@@ -37,9 +38,11 @@ the head gives padding rows zero loss weight (their gradients are exactly zero).
 
 Variants: every default below is the measured-fastest path of its configuration; the alternatives
 that stay are the bitwise references the tests compare against, selected with the ``variant``
-dict of the constructor (VARIANT_DEFAULTS).  Two environment switches turn a persistent,
-co-residency-dependent launch off without code changes: DMLC_FC_FUSED=0 (the fc chain) and
-DMLC_WGRAD_SGD=0 (the in-launch SGD / slab reduction of the wgrad launch).
+dict of the constructor (VARIANT_DEFAULTS).  Three environment switches turn a persistent,
+co-residency-dependent launch off without code changes (a training run builds the engine without a
+``variant``): DMLC_FC_FUSED=0 (the fc chain), DMLC_WGRAD_SGD=0 (the in-launch SGD / slab reduction of
+the wgrad launch) and DMLC_FWD12_SPLIT=0 (the B <= 128 forward whose two workgroups per image wait on
+each other).
 """
 from __future__ import annotations
 
@@ -87,7 +90,8 @@ VARIANT_DEFAULTS = {
     "fp8_dgrad": True,         # fp8: the conv2 input gradient on e4m3 too
     "comm_sgd": False,         # data parallel over xGMI: the SGD in the exchange kernel's epilogue
     "xraw_prefetch": True,     # the step's raw images gathered by the previous step's finalizer
-    "fwd12_split": True,       # B <= 128: conv1 + conv2 forward in one launch, two workgroups per image
+    "fwd12_split": True,       # B <= 128: conv1 + conv2 forward in one launch, two workgroups per image;
+                               # env DMLC_FWD12_SPLIT=0 off
     "fc_sgd_in_chain": None,   # single GPU, dW tiles in the fc chain: every fc SGD in their epilogues (default B < 256)
 }
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
@@ -347,7 +351,8 @@ class FusedCifarEngine:
         # workgroups per image swap their pool1 halves through sc1 stores + a flag (cnn_split.hip
         # k_conv12_fwd_split) -- one launch boundary and the conv2 input's global round trip less
         self.fwd12_split = (self.conv_split == 2 and self.conv1_split == 2 and not self.fp8
-                            and B * 2 <= cus and local_ <= max(1, ndev_) and bool(V["fwd12_split"]))
+                            and B * 2 <= cus and local_ <= max(1, ndev_) and bool(V["fwd12_split"])
+                            and os.environ.get("DMLC_FWD12_SPLIT", "1") != "0")
         self.c12_flags = torch.zeros(32 * 2 * B if self.fwd12_split else 1, dtype=torch.int32, device=dev)
         self.wbar = torch.zeros(WBAR_WORDS, dtype=torch.int32, device=dev)   # barrier words + error word
         # pinned host copy of the barrier error word, refreshed by queue_error_copy() behind each
@@ -606,7 +611,9 @@ class FusedCifarEngine:
                 parts.append(f"k_wgrad ({mode} mode): a sub-grid barrier timed out; rerun with DMLC_WGRAD_SGD=0")
             if e & 2:
                 parts.append("k_fc_chain / k_conv12_fwd_split: a hand-off wait timed out; rerun with "
-                             "DMLC_FC_FUSED=0 / variant fwd12_split=0")
+                             "DMLC_FC_FUSED=0 / DMLC_FWD12_SPLIT=0")
+            if self.fwd12_split:
+                self.c12_flags.zero_()     # a timed-out hand-off can leave a partner's flag raised
             raise RuntimeError("; ".join(parts) + f" (blocks not co-resident, error word {e})")
 
     def _allreduce(self, t: torch.Tensor):
@@ -676,8 +683,10 @@ class FusedCifarEngine:
     def compute_gradients(self, idx: Optional[torch.Tensor] = None, check: bool = True):
         """Forward + backward only (no update); the full gradient lands in ``self.grad``.
         ``idx``: explicit dataset rows (int32 [Bv]) instead of this step's generated batch.
-        ``check``: synchronise and raise if a persistent launch's hand-off timed out (the gradient
-        would be partial); pass False to keep the call asynchronous and call check_barriers() later."""
+        ``check`` (default True): SYNCHRONISES the device (one read of the error word) and raises if a
+        persistent launch's hand-off timed out (the gradient would be partial); loops that call this
+        repeatedly should pass False -- the call is then asynchronous -- and call check_barriers() at
+        their own sync point."""
         g = self._compute_gradients(idx)
         if check:
             self.check_barriers()
@@ -708,6 +717,8 @@ class FusedCifarEngine:
         interrupted capture): the next step starts clean instead of failing the pairing checks."""
         self._fc_src = None
         self._dgrad_done = False
+        if self.fwd12_split and not torch.cuda.is_current_stream_capturing():
+            self.c12_flags.zero_()         # stream-ordered: no half-finished hand-off carries over
 
     def _eager_step(self):
         try:

@@ -37,11 +37,13 @@ def main():
                          "launches leave host gaps: the first kernel's workgroups then enter up to ~4 us "
                          "apart, 0.4 us in the graph)")
     ap.add_argument("--graph", action="store_true", help="(the default; kept for old command lines)")
+    ap.add_argument("--variant", default="", help="engine variant keys, key=0|1,... (bench.py --variant)")
     a = ap.parse_args()
     g = torch.Generator().manual_seed(0)
     data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
     labels = torch.randint(0, 10, (50000,), dtype=torch.int32, generator=g)
-    eng = FusedCifarEngine(a.batch, data, labels, device="cuda", lr=1e-4)
+    var = {k: bool(int(v)) for k, v in (kv.split("=") for kv in filter(None, a.variant.split(",")))}
+    eng = FusedCifarEngine(a.batch, data, labels, device="cuda", lr=1e-4, variant=var)
     lib = ctypes.CDLL(_build.HIP_LIB)
     assert lib.dmlc_timing_enabled() == 1, "not a timing build"
     for _ in range(5):
