@@ -21,9 +21,11 @@
 //     the kernel drains instead of hanging the GPU.  The word is mirrored into mapped pinned host
 //     memory, so the training loop polls it with a plain load (no HIP call, no sync) and exits for
 //     a restart; once it is set, later launches skip their barriers (drain at once).
-// Memory model: writer side = system-scope release fence before a flag store (writes back the L2
-// of this XCD), reader side = system-scope acquire after the flag wait (invalidates non-local L2
-// lines), per the AMDGPU memory model for multi-L2 agents.
+// Memory model: writer side = every wave drains its stores, then ONE wave per workgroup issues the
+// system-scope release fence (writes back the L2 of this XCD) before the flag stores; reader side =
+// that wave's system-scope acquire after the flag wait (invalidates this CU's non-local lines), then a
+// workgroup barrier before any load -- per the AMDGPU memory model for multi-L2 agents.  (r5 fenced
+// in every wave: 4x the write-backs per workgroup; the world-1 DP step paid +16 us for the exchange.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -64,13 +66,20 @@ __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
 }
 
 // Cross-GPU barrier of workgroup b: lane p < W publishes epoch e into peer p's slot [which][b][rank]
-// and waits for peer p's epoch in its own slot [which][b][p].  All threads fence first (each wave's
-// stores drained and written back), so everything this workgroup wrote is visible to the peers.
+// and waits for peer p's epoch in its own slot [which][b][p].  Every wave drains its own stores
+// (s_waitcnt vmcnt(0)), the workgroup meets, and ONE wave releases at system scope (writes back this
+// XCD's L2) before its lanes signal; after the waits that wave alone acquires (invalidates this CU's
+// caches) and the workgroup meets again before any thread loads peer data -- one fence pair per
+// workgroup instead of one per wave (MI355X_MICROARCH.md, Valid forms: producer / consumer).
 template <int W>
 __device__ __forceinline__ void peer_barrier(const XgmiArgs& a, int which, uint32_t e) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int t = threadIdx.x, b = blockIdx.x;
+  if (t < 64) {                        // wave 0: one release for the whole workgroup's stores
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the write-back completes before any flag
+  }
   if (t < W) {
     st_sys(&a.sigs[t]->flag[which][b][a.rank], e);
     XgmiSignal* self = a.sigs[a.rank];
@@ -86,8 +95,11 @@ __device__ __forceinline__ void peer_barrier(const XgmiArgs& a, int which, uint3
       __builtin_amdgcn_s_sleep(2);
     }
   }
+  if (t < 64) {                        // wave 0 (the pollers): one acquire for the workgroup's CU
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
 __device__ __forceinline__ uint2 pack_bf16x4(float4 v) {
