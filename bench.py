@@ -105,7 +105,9 @@ def parse():
     ap.add_argument("--eager-graph", action="store_true",
                     help="capture the eager (PyTorch-op) step into a HIP graph (ResNet-20 path; the "
                          "framework-default comparison line is measured without it)")
-    ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="fp32")
+    # the gradient wire of N > 1 (bf16 since r6: half the link bytes; 300-step DP-2 loss-curve parity
+    # with the fp32 wire, tests/test_fused_dp_gpu.py::test_dp2_bf16_wire_loss_curve_tracks_fp32_wire)
+    ap.add_argument("--comm-dtype", choices=["fp32", "bf16"], default="bf16")
     ap.add_argument("--allreduce", choices=["auto", "rccl", "xgmi"], default="auto",
                     help="gradient all-reduce (N>1): auto = xGMI peer-to-peer kernel when it self-tests "
                          "and measures faster than RCCL, else RCCL")
