@@ -54,7 +54,8 @@ void conv1_fwd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor
 }
 
 void conv2_fwd_fp8(const Tensor& in, const Tensor& w8, const Tensor& b2, const Tensor& amax_x, const Tensor& scale_w,
-                   const c10::optional<Tensor>& counter, const Tensor& out, const Tensor& am) {
+                   const c10::optional<Tensor>& counter, const Tensor& out, const Tensor& am,
+                   const c10::optional<Tensor>& x8out, const c10::optional<Tensor>& sx_out) {
   const int64_t B = in.size(0);
   check(in, "in", at::kBFloat16, {B, 12, 12, 64});
   check(w8, "w8", at::kByte, {64, 1600});
@@ -73,6 +74,13 @@ void conv2_fwd_fp8(const Tensor& in, const Tensor& w8, const Tensor& b2, const T
     a.counter = counter->data_ptr<int64_t>();
   }
   a.out = out.data_ptr(); a.am = am.data_ptr<uint8_t>(); a.B = (int)B;
+  TORCH_CHECK(x8out.has_value() == sx_out.has_value(), "conv2_fwd_fp8: x8out and sx_out go together");
+  a.x8out = nullptr; a.sx_out = nullptr;
+  if (x8out.has_value()) {
+    check(*x8out, "x8out", at::kByte, {B, 144, 64});
+    check_numel(*sx_out, "sx_out", at::kFloat, 1);
+    a.x8out = x8out->data_ptr<uint8_t>(); a.sx_out = sx_out->data_ptr<float>();
+  }
   CHECK_HIP(dmlc_conv2_fwd_fp8(&a, stream_of(in)));
 }
 
@@ -212,7 +220,7 @@ void conv2_dgrad_split(const Tensor& dp2, const Tensor& am2, const Tensor& w2d, 
 }
 
 void conv2_dgrad_fp8(const Tensor& dp2, const Tensor& am2, const Tensor& w2d8, const Tensor& scale_w, const Tensor& dp1,
-                     const Tensor& dy2) {
+                     const Tensor& dy2, const c10::optional<Tensor>& dy8out, const c10::optional<Tensor>& sy_img) {
   const int64_t B = dp2.size(0);
   check(dp2, "dp2", at::kBFloat16, {B, 6, 6, 64});
   check(am2, "am2", at::kByte, {B, 6, 6, 64});
@@ -224,6 +232,13 @@ void conv2_dgrad_fp8(const Tensor& dp2, const Tensor& am2, const Tensor& w2d8, c
   DmlcConv2DgradFp8Args a;
   a.dp2 = dp2.data_ptr(); a.am2 = am2.data_ptr<uint8_t>(); a.w8 = w2d8.data_ptr<uint8_t>();
   a.scale_w = scale_w.data_ptr<float>(); a.dp1 = dp1.data_ptr(); a.dy2 = dy2.data_ptr(); a.B = (int)B;
+  TORCH_CHECK(dy8out.has_value() == sy_img.has_value(), "conv2_dgrad_fp8: dy8out and sy_img go together");
+  a.dy8out = nullptr; a.sy_img = nullptr;
+  if (dy8out.has_value()) {
+    check(*dy8out, "dy8out", at::kByte, {B, 144, 64});
+    check_numel(*sy_img, "sy_img", at::kFloat, B);
+    a.dy8out = dy8out->data_ptr<uint8_t>(); a.sy_img = sy_img->data_ptr<float>();
+  }
   CHECK_HIP(dmlc_conv2_dgrad_fp8(&a, stream_of(dp2)));
 }
 
@@ -232,7 +247,8 @@ static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10
                                 int64_t period, int64_t cy, int64_t cx, const Tensor& dp1, const Tensor& am1,
                                 const Tensor& part1, const Tensor& partb1, const Tensor& p1, const Tensor& dy2,
                                 const Tensor& part2, const Tensor& partb2, int64_t groups2,
-                                const c10::optional<Tensor>& xraw) {
+                                const c10::optional<Tensor>& xraw,
+                                const c10::optional<at::TensorList>& fp8 = c10::nullopt) {
   const int64_t B = p1.size(0), g1 = part1.size(0), g2 = groups2;
   check_data(data);
   TORCH_CHECK(cy >= 0 && cy <= 8 && cx >= 0 && cx <= 8, "crop offsets must be in [0,8]");
@@ -257,6 +273,17 @@ static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10
   a.w1.xraw = xraw_ptr(xraw, B);
   a.w2.p1 = p1.data_ptr(); a.w2.dy2 = dy2.data_ptr(); a.w2.part2 = part2.data_ptr();
   a.w2.partb2 = partb2.data_ptr<float>(); a.w2.g2 = (int)g2; a.w2.B = (int)B;
+  if (fp8.has_value()) {
+    // the fp8 conv2 weight gradient's operands: {x8 [B][144][64] e4m3, y8 (same), sx [1], sy_img [B]}
+    const at::TensorList f = *fp8;
+    TORCH_CHECK(f.size() == 4, "wgrad: fp8 = {x8, y8, sx, sy_img}");
+    check(f[0], "x8", at::kByte, {B, 144, 64});
+    check(f[1], "y8", at::kByte, {B, 144, 64});
+    check_numel(f[2], "sx", at::kFloat, 1);
+    check_numel(f[3], "sy_img", at::kFloat, B);
+    a.w2.x8 = f[0].data_ptr<uint8_t>(); a.w2.y8 = f[1].data_ptr<uint8_t>();
+    a.w2.sx = f[2].data_ptr<float>(); a.w2.sy_img = f[3].data_ptr<float>();
+  }
   a.apply = 0; a.bar = nullptr; a.helpers = 0; a.fc_done = 0;
   memset(&a.sgd, 0, sizeof(a.sgd));
   return a;
@@ -265,9 +292,9 @@ static DmlcWgradArgs make_wgrad(const Tensor& data, const Tensor& idx, const c10
 void wgrad(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
            int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& part1, const Tensor& partb1,
            const Tensor& p1, const Tensor& dy2, const Tensor& part2, const Tensor& partb2, int64_t groups2,
-           const c10::optional<Tensor>& xraw) {
+           const c10::optional<Tensor>& xraw, const c10::optional<at::TensorList> fp8) {
   DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
-                               groups2, xraw);
+                               groups2, xraw, fp8);
   c10::DeviceGuard guard(dp1.device());
   CHECK_HIP(dmlc_wgrad(&a, stream_of(dp1)));
 }
@@ -651,9 +678,9 @@ void sgd(DMLC_SGD_PARAMS) {
 void wgrad_sgd(const Tensor& data, const Tensor& idx, const c10::optional<Tensor>& counter, int64_t period, int64_t cy,
                int64_t cx, const Tensor& dp1, const Tensor& am1, const Tensor& p1, const Tensor& dy2,
                int64_t groups2, const Tensor& xraw, const Tensor& bar, DMLC_SGD_PARAMS,
-               const c10::optional<at::TensorList> fc_acts, bool fc_sgd_done) {
+               const c10::optional<at::TensorList> fc_acts, bool fc_sgd_done, const c10::optional<at::TensorList> fp8) {
   DmlcWgradArgs a = make_wgrad(data, idx, counter, period, cy, cx, dp1, am1, part1, partb1, p1, dy2, part2, partb2,
-                               groups2, xraw);
+                               groups2, xraw, fp8);
   TORCH_CHECK((mode == 0 && fc1_fused && step_rd.has_value() && roles == 0 && finalize &&
                grad_scale == 1.0) || (mode == 1 && roles == 0),
               "wgrad_sgd: the single-GPU mode-0 step (fc1 epilogue, the head's step copy) or mode 1 (reduce only)");
@@ -709,7 +736,7 @@ TORCH_LIBRARY(dmlc, m) {
   m.def("conv1_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
         "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? amax=None, Tensor(d!)? xraw=None) -> ()");
   m.def("conv2_fwd_fp8(Tensor inp, Tensor w8, Tensor b2, Tensor amax_x, Tensor scale_w, Tensor? counter, "
-        "Tensor(a!) out, Tensor(b!) am) -> ()");
+        "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? x8out=None, Tensor(d!)? sx_out=None) -> ()");
   m.def("fp8_roundtrip(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("conv2_fwd(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("conv12_fwd(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor w1f, Tensor b1, "
@@ -720,10 +747,11 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(a!) out, Tensor(b!) am, Tensor(c!)? xraw, int nsplit) -> ()");
   m.def("conv2_fwd_split(Tensor inp, Tensor w2f, Tensor b2, Tensor(a!) out, Tensor(b!) am) -> ()");
   m.def("conv2_dgrad_split(Tensor dp2, Tensor am2, Tensor w2d, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
-  m.def("conv2_dgrad_fp8(Tensor dp2, Tensor am2, Tensor w2d8, Tensor scale_w, Tensor(a!) dp1, Tensor(b!) dy2) -> ()");
+  m.def("conv2_dgrad_fp8(Tensor dp2, Tensor am2, Tensor w2d8, Tensor scale_w, Tensor(a!) dp1, Tensor(b!) dy2, "
+        "Tensor(c!)? dy8out=None, Tensor(d!)? sy_img=None) -> ()");
   m.def("wgrad(Tensor data, Tensor idx, Tensor? counter, int period, int cy, int cx, Tensor dp1, Tensor am1, "
         "Tensor(a!) part1, Tensor(b!) partb1, Tensor p1, Tensor dy2, Tensor(c!) part2, Tensor(d!) partb2, "
-        "int groups2, Tensor? xraw=None) -> ()");
+        "int groups2, Tensor? xraw=None, Tensor[]? fp8=None) -> ()");
   m.def("gemm_grouped(Tensor[] A, Tensor[] B, Tensor(a!)[] C, Tensor?[] bias, int[] params, Tensor? step=None, "
         "Tensor(b!)? shadow=None, float[] sched=[]) -> ()");
   m.def("head(Tensor h1part, Tensor b1, Tensor w2t, Tensor b2, Tensor w3t, Tensor b3, Tensor w3d, Tensor w2d, "
@@ -746,7 +774,7 @@ TORCH_LIBRARY(dmlc, m) {
         "Tensor(m!) stats, Tensor(n!)? w2f8, Tensor(o!)? amax_w, Tensor(p!)? scale_w, int roles, "
         "bool finalize, int batch, Tensor(q!)? bidx=None, Tensor? order=None, float warmup=0.0, "
         "bool fc1_fused=False, Tensor? step_rd=None, Tensor(v!)? xnext=None, Tensor? xdata=None, "
-        "Tensor[]? fc_acts=None, bool fc_sgd_done=False) -> ()");
+        "Tensor[]? fc_acts=None, bool fc_sgd_done=False, Tensor[]? fp8=None) -> ()");
   m.def("sgd(Tensor(a!) master, Tensor(b!) grad, int mode, float grad_scale, int[] off, Tensor part1, Tensor partb1, "
         "Tensor part2, Tensor partb2, Tensor(c!) w1f, Tensor(d!) w2f, Tensor(e!) w2d, Tensor(f!) fc1n, "
         "Tensor(g!) fc2t, Tensor(h!) fc2n, Tensor(i!) fc3t, Tensor(j!) fc3d, Tensor(k!) step, float lr0, float decay, "

@@ -70,6 +70,8 @@ struct DmlcConv2FwdFp8Args {
   void* out;                // bf16 [B][6][6][64]
   uint8_t* am;              // [B][6][6][64]
   int B;
+  uint8_t* x8out;           // nullable: the quantised input e4m3 [B][144][64] (the fp8 weight gradient's X)
+  float* sx_out;            // nullable (with x8out): its per-batch scale sx, float[1]
 };
 
 // conv2 input gradient on fp8 MFMA operands (BASELINE config 5 backward): w8 = the flipped, ci-major
@@ -83,6 +85,8 @@ struct DmlcConv2DgradFp8Args {
   void* dp1;                // bf16 [B][12][12][64]
   void* dy2;                // bf16 [B][144][64]
   int B;
+  uint8_t* dy8out;          // nullable: the quantised dY2 e4m3 [B][144][64] (the fp8 weight gradient's dY)
+  float* sy_img;            // nullable (with dy8out): float[B], image b's power-of-two dY2 scale
 };
 
 // conv2 input-gradient with the pool2/ReLU backward fused into the operand staging.
@@ -118,6 +122,13 @@ struct DmlcConv2WgradArgs {
   float* partb2;            // [g2][64] conv2 bias-grad partials (written by the c4 == 0 blocks)
   int g2;
   int B;
+  // fp8 (BASELINE config 5): the conv2 weight gradient on v_mfma_scale_f32_16x16x128_f8f6f4 over the
+  // e4m3 copies the fp8 forward (X, per-batch scale sx) and the fp8 dgrad (dY2, a power-of-two scale
+  // per image, applied as the MFMA's E8M0 block scale) wrote; x8 == null: bf16 MFMA on p1 / dy2
+  const uint8_t* x8;        // e4m3 [B][144][64]
+  const uint8_t* y8;        // e4m3 [B][144][64]
+  const float* sx;          // float[1]
+  const float* sy_img;      // float[B]
 };
 
 

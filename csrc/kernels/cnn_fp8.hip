@@ -18,7 +18,9 @@
 // conv2 input gradient (k_conv2_dgrad_fp8): the same weight-stationary core on the flipped, ci-major
 // weights (w2d8, quantised by the SGD kernel with the same scale as w2f8) and the pool2/ReLU-backward
 // gradient dY2 quantised per IMAGE with sy = 448 / amax(dY2 of that image), reduced in-block from the
-// values the block just produced.  The weight gradients stay bf16 (they read the bf16 p1 and dY2).
+// values the block just produced, rounded down to a power of two (r6); the quantised dY2 and its
+// scale are also stored (dy8out, sy_img) for the fp8 conv2 weight gradient (cnn_wgrad.hip w2_fp8_main),
+// as the forward stores its quantised input and sx (x8out, sx_out).
 #include "conv_common.h"
 
 namespace dmlc {
@@ -128,6 +130,7 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd_fp8(DmlcConv2FwdFp8Args a) 
   for (int i = 1; i < NT / 64; ++i) mx = fmaxf(mx, red[i]);
   const float sx = 448.f / fmaxf(mx, 1e-20f);
   const float inv = 1.f / (sx * sw);
+  if (a.sx_out && blockIdx.x == 0 && tid == 0) a.sx_out[0] = sx;   // (every block computes the same sx)
   float b4[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -157,6 +160,10 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_fwd_fp8(DmlcConv2FwdFp8Args a) 
       const uint32_t lo = pk_fp8x4(bf16_lo(wv[0]) * sx, bf16_hi(wv[0]) * sx, bf16_lo(wv[1]) * sx, bf16_hi(wv[1]) * sx);
       const uint32_t hi = pk_fp8x4(bf16_lo(wv[2]) * sx, bf16_hi(wv[2]) * sx, bf16_lo(wv[3]) * sx, bf16_hi(wv[3]) * sx);
       *reinterpret_cast<uint2*>(x8 + x8_addr(s >> 3, (s & 7) >> 1) + (s & 1) * 8) = make_uint2(lo, hi);
+      // the fp8 weight gradient's X: the same bytes, unpadded [b][144][64] (interior pixels)
+      const int pix = s >> 3, iy = (pix >> 4) - 2, ix = (pix & 15) - 2;
+      if (a.x8out && iy >= 0 && iy < 12 && ix >= 0 && ix < 12)
+        *reinterpret_cast<uint2*>(a.x8out + ((size_t)b * 144 + iy * 12 + ix) * 64 + (s & 7) * 8) = make_uint2(lo, hi);
     }
     if (b + G < a.B) load(b + G);              // next image's input in flight under this one
     __syncthreads();
@@ -241,7 +248,11 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_fp8(DmlcConv2DgradFp8Args
     float amax = red[0];
 #pragma unroll
     for (int i = 1; i < NT / 64; ++i) amax = fmaxf(amax, red[i]);
-    const float sy = amax > 0.f ? 448.f / amax : 1.f;
+    // a power of two (round 6): the fp8 weight gradient applies it as the MFMA's E8M0 block scale --
+    // kept within 2^+-126 (finite, representable): a saturated softmax leaves images whose largest dY2
+    // is denormal (448 / amax overflows); their e4m3 values then flush to zero
+    const float sy = amax > 0.f ? exp2f(fminf(fmaxf(floorf(log2f(448.f / amax)), -126.f), 126.f)) : 1.f;
+    if (tid == 0 && a.sy_img) a.sy_img[b] = sy;
     if (tid < 288) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -249,6 +260,10 @@ __global__ __launch_bounds__(NT, 1) void k_conv2_dgrad_fp8(DmlcConv2DgradFp8Args
         const uint32_t lo = pk_fp8x4(o[k][0] * sy, o[k][1] * sy, o[k][2] * sy, o[k][3] * sy);
         const uint32_t hi = pk_fp8x4(o[k][4] * sy, o[k][5] * sy, o[k][6] * sy, o[k][7] * sy);
         *reinterpret_cast<uint2*>(x8 + x8_addr(P, c >> 1) + (c & 1) * 8) = make_uint2(lo, hi);
+        if (a.dy8out) {                      // the fp8 weight gradient's dY: the same bytes, [b][144][64]
+          const int y = 2 * py + (k >> 1), x = 2 * px + (k & 1);
+          *reinterpret_cast<uint2*>(a.dy8out + ((size_t)b * 144 + y * 12 + x) * 64 + c * 8) = make_uint2(lo, hi);
+        }
       }
     }
     __syncthreads();

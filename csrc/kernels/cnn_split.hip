@@ -199,7 +199,7 @@ __global__ __launch_bounds__(SP_NT, 1) void k_conv12_fwd_split(DmlcConv1FwdArgs 
     __hip_atomic_store(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool seen = true;
     for (unsigned it = 0; __hip_atomic_load(theirs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u; ++it) {
-      if (it > (1u << 20)) {
+      if (it >= DMLC_SPIN_LIMIT) {
         __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         seen = false;
         break;

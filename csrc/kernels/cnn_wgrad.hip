@@ -121,6 +121,169 @@ DEV void w2_block_pos(const DmlcConv2WgradArgs& a, int blk, int base, int& c4, i
   grp = xcd ? (blk & 7) + 8 * (blk >> 5) : blk >> 2;
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp8 conv2 weight gradient (BASELINE config 5; a.x8 set): the same blocks, accumulators and epilogue
+// as the bf16 body below, with the MFMA on v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3: twice the
+// bf16 rate per clock) over the e4m3 operands the producers already quantised -- X by the fp8 forward
+// (per-batch scale sx), dY2 by the fp8 dgrad (a power-of-two scale per image) -- so the staging is a
+// plain copy of half the bf16 bytes.
+//   * K = output pixels of a UNIT of two images, each laid out as a 12 x 16 grid whose columns 12..15
+//     carry dY = 0: a 16-wide K row makes every tap's input rows a LINEAR shift of the output rows
+//     (padded pixel = k + 16 kh + kw), and 2 x 192 = 384 = three K chunks of 128;
+//   * dY's per-image scale rides on the MFMA's E8M0 block scales: lane l's scale byte covers K rows
+//     {0..15, 32..47} + 64 ((l >> 4) & 1) + 16 (l >> 5) of the chunk (tools/probes/mx_scale_probe.hip),
+//     so a block never straddles the image boundary at row 192; acc / sx at the end;
+//   * the conv2 bias gradient from the same dY bytes: one extra MFMA against an all-ones A per chunk
+//     on waves 4-7 of the c4 == 0 blocks (they carry one MFMA less than waves 0-3);
+//   * fragments by ds_read_b64_tr_b8 (lane 2q+p addresses row q, bytes 8p..; lane i receives column i
+//     of the 8-row x 16-byte block -- tools/probes/fp8_wgrad_probe.hip).  Lane group g's four reads
+//     j take the 8-row K segments g + 4j (the MFMA's K order only has to agree between A and B): the
+//     two groups of a half-wave then read rows 8 apart, so the 16-B X rows are conflict-free as they
+//     stand and the 64-B dY rows need only an XOR of the 16-B co tile with row bits 2 and 3 -- both
+//     per-lane constants, as is the image of every read (the boundary at row 192 falls between reads
+//     j = 1 and 2 of chunk 1): every fragment address is a lane base + an immediate offset.  LDS is
+//     double-buffered per unit, the next unit's 16-B chunks in registers under this unit's MFMAs; one
+//     barrier per unit.
+typedef int w8x32 __attribute__((ext_vector_type(8)));
+typedef int w8x2 __attribute__((ext_vector_type(2)));
+constexpr int W8_XROWS = 272;                  // padded 16 x 16 input grid + 16 zero rows (garbage-column reads)
+constexpr int W8_XIMG = W8_XROWS * 16;         // bytes per image: [row][16 ci] e4m3
+constexpr int W8_YIMG = 192 * 64;              // [12 x 16 output grid][64 co] e4m3
+constexpr int W8_XU = 2 * W8_XIMG, W8_BUF = 2 * (W8_XIMG + W8_YIMG);
+constexpr size_t W8_LDS = 2 * (size_t)W8_BUF + 64 * 4;   // double buffer + the bias tile
+DEV int w8_ychunk(int r, int ct) { return ct ^ (((r >> 2) & 1) | (((r >> 3) & 1) << 1)); }
+DEV w8x2 tr8(const uint8_t* p) { return __builtin_amdgcn_ds_read_tr8_b64_v2i32((LDS_AS w8x2*)(p)); }
+DEV f32x4 mfma8(const w8x32& a, const w8x32& b, const f32x4& c, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, sb);
+}
+
+DEV void w2_fp8_main(const DmlcConv2WgradArgs& a, int c4, int grp, char* smem, f32x4 (&acc)[13], float (&bsum)[8]) {
+  uint8_t* lds = reinterpret_cast<uint8_t*>(smem);
+  float* btile = reinterpret_cast<float*>(smem + 2 * W8_BUF);
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int g = lane >> 4, q = (lane & 15) >> 1, p = lane & 1, half = (lane >> 4) & 1;
+  const int G = a.g2, nimg = grp < a.B ? (a.B - 1 - grp) / G + 1 : 0, nunits = (nimg + 1) >> 1;
+  const bool bias = c4 == 0 && w >= 4;         // wave 4 + ct: the bias gradient of co tile ct
+  // zero both buffers once: halo / slack X rows and dY columns 12..15 are never written again
+  for (int i = tid; i < 2 * W8_BUF / 16; i += W2T) reinterpret_cast<uint4*>(lds)[i] = make_uint4(0u, 0u, 0u, 0u);
+
+  // staging map (16-B chunks): X chunk s < 288 (image s / 144, pixel s % 144: this quarter's 16 ci),
+  // thread s = tid; dY chunk s < 1152 (image s / 576, pixel (s % 576) >> 2, co tile s & 3), s = tid +
+  // 512 m for m < 3 (the last for tid < 128)
+  uint4 vx, vy[3];
+  float syv[2];                                // the unit's two dY scales (prefetched with its chunks)
+  int ey[2];                                   // ... as E8M0 block scales, 127 - log2 sy
+  auto img_of = [&](int u, int i) { return grp + G * (2 * u + i); };
+  auto load = [&](int u, uint4& vx, uint4 (&vy)[3], float (&syv)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int b = img_of(u, i);
+      syv[i] = load_sel(a.sy_img + b, a.sy_img, b < a.B);
+    }
+    {
+      const int i = tid >= 144, px = tid - 144 * i, b = img_of(u, i);
+      vx = load_sel(reinterpret_cast<const uint4*>(a.x8 + ((size_t)b * 144 + px) * 64 + 16 * c4),
+                    reinterpret_cast<const uint4*>(a.x8), tid < 288 && b < a.B);
+    }
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int s = tid + 512 * m, i = s >= 576, k = s - 576 * i, b = img_of(u, i);
+      vy[m] = load_sel(reinterpret_cast<const uint4*>(a.y8 + ((size_t)b * 144 + (k >> 2)) * 64 + 16 * (k & 3)),
+                       reinterpret_cast<const uint4*>(a.y8), (m < 2 || tid < 128) && b < a.B);
+    }
+  };
+  auto store = [&](int buf, const uint4& vx, const uint4 (&vy)[3]) __attribute__((always_inline)) {
+    uint8_t* X8 = lds + buf * W8_BUF;
+    uint8_t* Y8 = X8 + W8_XU;
+    if (tid < 288) {
+      const int i = tid >= 144, px = tid - 144 * i, y = px / 12, x = px - 12 * y;
+      *reinterpret_cast<uint4*>(X8 + i * W8_XIMG + ((y + 2) * 16 + x + 2) * 16) = vx;
+    }
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      if (m == 2 && tid >= 128) break;
+      const int s = tid + 512 * m, i = s >= 576, k = s - 576 * i, px = k >> 2, y = px / 12, x = px - 12 * y;
+      const int r = i * 192 + y * 16 + x;
+      *reinterpret_cast<uint4*>(Y8 + r * 64 + 16 * w8_ychunk(r, k & 3)) = vy[m];
+    }
+  };
+  auto scales = [&](const float (&syv)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) ey[i] = syv[i] > 0.f ? 127 - (int)log2f(syv[i]) : 127;   // (exact powers of two)
+  };
+  // fragment bases: dY row (8 g + q) of chunk 0, tile ct (swizzle f = row bits 2, 3: per lane); X row
+  // (8 g + q) + the wave's tap offsets (16 kh + kw rows); chunk c, read j, image 1 by immediates
+  const int f = ((q >> 2) & 1) | ((g & 1) << 1);
+  const int yl = (8 * g + q) * 64 + 8 * p, xl = (8 * g + q) * 16 + 8 * p;
+  int xt[4];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) xt[t] = xl + ((3 * w + t) / 5 * 16 + (3 * w + t) % 5) * 16;
+  xt[3] = xl + (4 * 16 + 4) * 16;
+  const w8x32 ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838,   // e4m3 1.0
+                      0x38383838, 0x38383838, 0x38383838, 0x38383838};
+  f32x4 accb = zero4();
+  __syncthreads();                             // the zeroing is done before any staging store
+  // (loads two units ahead -- a second register set -- spill at this kernel's register budget)
+  if (nunits > 0) load(0, vx, vy, syv);
+  for (int u = 0; u < nunits; ++u) {
+    const int buf = u & 1;
+    store(buf, vx, vy);                        // (buffer buf was last read two units ago)
+    scales(syv);
+    if (u + 1 < nunits) load(u + 1, vx, vy, syv);   // the next unit's operands in flight under the MFMAs
+    lds_barrier();
+    if (u == 0) DMLC_STAMP(DMLC_TK_W2, 1);
+    const uint8_t* Y8 = lds + buf * W8_BUF + W8_XU + yl;
+    const uint8_t* X8 = lds + buf * W8_BUF;
+    // chunk c's fragments: rows 128 c + 8 g + 32 j + q; image 1 for c == 2 and for j >= 2 of c == 1
+    // (one set of fragments: a second set for a read-ahead spills -- the partner wave of the SIMD
+    // covers this wave's read latency with its MFMAs)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      w8x32 bf[4], af[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int img = c == 2 || (c == 1 && j >= 2);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const w8x2 v = tr8(Y8 + 16 * (ct ^ f) + c * 8192 + j * 2048);
+          bf[ct][2 * j] = v.x; bf[ct][2 * j + 1] = v.y;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (t == 3 && w >= 4) break;
+          const w8x2 v = tr8(X8 + xt[t] + c * 2048 + j * 512 + img * (W8_XIMG - 192 * 16));
+          af[t][2 * j] = v.x; af[t][2 * j + 1] = v.y;
+        }
+      }
+      // this lane's dY block scale: its block is image 1 for c == 2, and for the upper half-wave's
+      // blocks (reads j >= 2) of c == 1
+      const int sb = c == 0 ? ey[0] : c == 2 ? ey[1] : lane >= 32 ? ey[1] : ey[0];
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) acc[4 * t + ct] = mfma8(af[t], bf[ct], acc[4 * t + ct], sb);
+      if (w < 4) {
+        const w8x32 bw = w == 0 ? bf[0] : w == 1 ? bf[1] : w == 2 ? bf[2] : bf[3];
+        acc[12] = mfma8(af[3], bw, acc[12], sb);
+      } else if (bias) {
+        const w8x32 bw = w == 4 ? bf[0] : w == 5 ? bf[1] : w == 6 ? bf[2] : bf[3];
+        accb = mfma8(ones, bw, accb, sb);
+      }
+    }
+    if (u == 0) DMLC_STAMP(DMLC_TK_W2, 4);
+  }
+  const float inv = 1.f / a.sx[0];
+#pragma unroll
+  for (int j = 0; j < 13; ++j) acc[j] *= inv;
+  // the bias tile (row 0 of the ones product: lanes 0..15) -> bsum of threads 0..7 in the layout
+  // block_chunk_sum reduces (thread t < 8, j: channel 8 t + j; every other thread 0)
+  __syncthreads();                             // every MFMA read of LDS is done
+  if (bias && lane < 16) btile[16 * (w - 4) + lane] = accb[0];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bsum[j] = c4 == 0 && tid < 8 ? btile[8 * tid + j] : 0.f;
+}
+
 // coh: the slabs and bias partials are reduced by other blocks of the same launch (apply mode):
 // agent-coherent stores instead of streaming ones
 DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int base, char* smem, bool coh = false) {
@@ -133,14 +296,16 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
   const int G = a.g2, b0 = grp, last = grp < a.B ? grp + (a.B - 1 - grp) / G * G : grp;
   DMLC_STAMP(DMLC_TK_W2, 0);
 
-  // zero the whole padded input once (the interior is overwritten per image) and the 16 pad dY rows
-  *reinterpret_cast<bf16x8*>(xt + tid * 8) = bf16x8{};
-  if (tid < 128) *reinterpret_cast<bf16x8*>(dyt + (144 + (tid >> 3)) * W2_LD + (tid & 7) * 8) = bf16x8{};
-
   f32x4 acc[13];
 #pragma unroll
   for (int j = 0; j < 13; ++j) acc[j] = zero4();
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // conv2 bias grad (c4 == 0 blocks)
+  if (a.x8) {
+    w2_fp8_main(a, c4, grp, smem, acc, bsum);
+  } else {
+  // zero the whole padded input once (the interior is overwritten per image) and the 16 pad dY rows
+  *reinterpret_cast<bf16x8*>(xt + tid * 8) = bf16x8{};
+  if (tid < 128) *reinterpret_cast<bf16x8*>(dyt + (144 + (tid >> 3)) * W2_LD + (tid & 7) * 8) = bf16x8{};
 
   // prefetch per image: 1 chunk of this quarter's input (288 chunks: pixel k >> 1, half k & 1;
   // threads >= 288 duplicate chunks of lower threads) and 3 of dY (1152 chunks; in the third,
@@ -220,6 +385,7 @@ DEV void conv2_wgrad_block(const DmlcConv2WgradArgs& a, const int blk, const int
       __builtin_amdgcn_sched_barrier(0);
     }
     if (b == b0) DMLC_STAMP(DMLC_TK_W2, 4);
+  }
   }
   DMLC_STAMP(DMLC_TK_W2, 2);
   // slab element e of this group (fp32 partial sum over G-th of the batch)
@@ -522,6 +688,7 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
 // the conv1 body, the next 4 * g2 the conv2 body.  One block per CU (LDS): g1 + 4 * g2 <= 256 keeps
 // every block resident in one wave of blocks.
 constexpr size_t WG_LDS = W1_LDS > W2_LDS ? W1_LDS : W2_LDS;
+static_assert(WG_LDS >= W8_LDS, "the fp8 conv2 body's double buffer fits the launch's LDS");
 static_assert(WG_LDS >= (size_t)L_RED + 8 * 64 * 4 && WG_LDS >= 40960 + 64 * 136 * 2,
               "the fc dW tiles reuse the weight-gradient launch's LDS");
 static_assert(W1T == FT, "the fc dW tiles run with the weight-gradient launch's block size");

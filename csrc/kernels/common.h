@@ -183,6 +183,14 @@ DEV void st_out8(void* base, uint32_t byte_off, const uint2& v) {
     st_maybe_nt<kNtDefault>(reinterpret_cast<uint2*>(reinterpret_cast<char*>(base) + byte_off), v);
 }
 
+// Spin bound of every in-launch wait (sub-grid barriers, hand-off seams, split-forward flags): past it
+// the waiter sets the sticky error word and goes on.  A diagnostic build with -DDMLC_SPIN_LIMIT=0
+// (DMLC_VARIANT="spin0:-DDMLC_SPIN_LIMIT=0") gives up at the first unsatisfied poll, which forces the
+// timeout paths on purpose (tests/test_health.py::test_forced_spin_timeouts_name_kernel_and_switch).
+#ifndef DMLC_SPIN_LIMIT
+#define DMLC_SPIN_LIMIT (1u << 20)
+#endif
+
 // Sub-grid barrier among the n co-resident blocks sharing (cnt, gen) (each on its own 128-B line,
 // zero-initialised; they re-arm themselves).  Thread 0 reads the generation BEFORE its block can
 // arrive (bar_gen), arrives once the block's coherent stores are acknowledged (bar_arrive) and spins
@@ -197,7 +205,7 @@ DEV void bar_arrive(unsigned* cnt, unsigned* gen, unsigned g0, unsigned n) {
 }
 DEV void bar_wait(unsigned* gen, unsigned g0, unsigned* err) {
   for (unsigned it = 0; bar_gen(gen) == g0; ++it) {
-    if (it > (1u << 20)) {
+    if (it >= DMLC_SPIN_LIMIT) {
       __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
@@ -246,7 +254,7 @@ DEV void seam_wait(const Seam& s, int lane, unsigned* err, unsigned errbit, int 
   for (unsigned it = 0;; ++it) {
     const bool ok = !on || __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= t;
     if (__all(ok)) break;
-    if (it > (1u << 20)) {
+    if (it >= DMLC_SPIN_LIMIT) {
       if (lane == 0) __hip_atomic_fetch_or(err, errbit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }

@@ -70,7 +70,7 @@ DEV unsigned ld_relaxed(unsigned* p) { return __hip_atomic_load(p, __ATOMIC_RELA
 // one lane: spin until *p >= target (bounded; on give-up the sticky error word is set)
 DEV void wait_ge(unsigned* p, unsigned target, unsigned* err) {
   for (unsigned it = 0; ld_relaxed(p) < target; ++it) {
-    if (it > (1u << 20)) {
+    if (it >= DMLC_SPIN_LIMIT) {
       __hip_atomic_fetch_or(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }

@@ -88,6 +88,7 @@ VARIANT_DEFAULTS = {
     "wgrad_sgd": True,         # in-launch SGD / slab reduction of the wgrad launch; env DMLC_WGRAD_SGD=0 off
     "wgrad_sgd_fp8": False,    # the same for --dtype fp8 (bit-identical, measured 1.4 % slower at B=1024)
     "fp8_dgrad": True,         # fp8: the conv2 input gradient on e4m3 too
+    "fp8_wgrad": True,         # fp8 (with fp8_dgrad): the conv2 weight gradient on e4m3 MFMA (per-batch scales)
     "comm_sgd": False,         # data parallel over xGMI: the SGD in the exchange kernel's epilogue
     "xraw_prefetch": True,     # the step's raw images gathered by the previous step's finalizer
     "fwd12_split": True,       # B <= 128: conv1 + conv2 forward in one launch, two workgroups per image;
@@ -216,6 +217,14 @@ class FusedCifarEngine:
             self.amax_x = z(B, dt=torch.float32)      # per-image activation maxima (conv1 -> conv2)
             self.amax_w = z(2, 400, dt=torch.float32)  # [slot][SGD conv2-row block] weight maxima
             self.scale_w = z(2, dt=torch.float32)
+        # fp8 conv2 weight gradient (cnn_wgrad.hip w2_fp8_main): the e4m3 X the fp8 forward quantised
+        # (per-batch scale sx) and the e4m3 dY2 the fp8 dgrad quantised (a power-of-two scale per
+        # image, the MFMA's E8M0 block scale), written by those kernels next to their bf16 outputs
+        self.fp8_wgrad = self.fp8_dgrad and bool(V["fp8_wgrad"])
+        if self.fp8_wgrad:
+            self.p1f8, self.dy2f8 = z(B, 144, 64, dt=torch.uint8), z(B, 144, 64, dt=torch.uint8)
+            self.sx8, self.sy_img = z(1, dt=torch.float32), torch.ones(B, dtype=torch.float32, device=dev)
+        self._w8 = dict(fp8=[self.p1f8, self.dy2f8, self.sx8, self.sy_img]) if self.fp8_wgrad else {}
 
         # --- activations / workspaces -------------------------------------------------------
         self.fc1_split = fc1_split or self._pick_fc1_split(B)
@@ -491,7 +500,8 @@ class FusedCifarEngine:
             o.conv1_fwd(self.data, idx, counter, period, self.cy, self.cx, self.w1f, p["conv1_bias"], self.p1,
                         self.am1, self.amax_x if self.fp8 else None, self.xraw if train else None)
         if self.fp8:
-            o.conv2_fwd_fp8(self.p1, self.w2f8[0], p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2)
+            o.conv2_fwd_fp8(self.p1, self.w2f8[0], p["conv2_bias"], self.amax_x, self.scale_w, counter, self.p2, self.am2,
+                            *((self.p1f8, self.sx8) if train and self.fp8_wgrad else (None, None)))
         elif not self.fused_fwd and self.conv_split == 1:
             o.conv2_fwd(self.p1, self.w2f, p["conv2_bias"], self.p2, self.am2)
         if train and self.fc_fused:
@@ -552,7 +562,8 @@ class FusedCifarEngine:
         if self._dgrad_done:
             self._dgrad_done = False                 # the fc chain launch did it (fc_dgrad)
         elif self.fp8_dgrad:
-            o.conv2_dgrad_fp8(self.dp2, self.am2, self.w2f8[1], self.scale_w, self.dp1, self.dy2)
+            o.conv2_dgrad_fp8(self.dp2, self.am2, self.w2f8[1], self.scale_w, self.dp1, self.dy2,
+                              *((self.dy2f8, self.sy_img) if self.fp8_wgrad else (None, None)))
         elif self.dgrad_split == 2:
             o.conv2_dgrad_split(self.dp2, self.am2, self.w2d, self.dp1, self.dy2)
         else:
@@ -564,10 +575,11 @@ class FusedCifarEngine:
             o.wgrad_sgd(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1, self.p1, self.dy2,
                         self.groups2, self.xraw, self.wbar,
                         *(self._sgd_args(mode=0, fc1_fused=True) if apply else self._sgd_args(mode=1)),
-                        fc_acts=fc_acts, fc_sgd_done=bool(apply and self.fc_sgd_in_chain))
+                        fc_acts=fc_acts, fc_sgd_done=bool(apply and self.fc_sgd_in_chain), **self._w8)
             return
         o.wgrad(self.data, idx, counter, period, self.cy, self.cx, self.dp1, self.am1,
-                self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw)
+                self.part1, self.partb1, self.p1, self.dy2, self.part2, self.partb2, self.groups2, self.xraw,
+                **self._w8)
 
     def _sgd_args(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True,
                   fc1_fused: bool = False) -> tuple:

@@ -87,6 +87,39 @@ def test_fp8_dgrad_matches_reference(B):
     assert cos > 0.995, out
 
 
+@pytest.mark.parametrize("B", [64, 100, 1024])
+def test_fp8_wgrad_matches_reference(B):
+    """The fp8 conv2 weight gradient (cnn_wgrad.hip w2_fp8_main: e4m3 operands quantised in the
+    staging with per-batch scales from the per-image maxima, scaled 16x16x128 MFMA over units of two
+    images) against fp32 PyTorch fed with the kernel's own bf16 p1 and dY2; the bf16 weight gradient
+    on the same inputs sets the scale of the comparison.  B = 100 leaves groups with an odd image count
+    (a half-empty last unit); B = 1024 runs 16 units per block."""
+    data, labels = _synthetic(2048, seed=14)
+    eng = FusedCifarEngine(B, data, labels, seed=12, dtype="fp8")
+    assert eng.fp8_wgrad
+    g8 = eng.compute_gradients().clone()
+    torch.cuda.synchronize()
+    Bv = eng.Bv
+    x = eng.p1[:Bv].float().permute(0, 3, 1, 2)
+    dy = eng.dy2[:Bv].float().view(Bv, 12, 12, 64).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(x, (64, 64, 5, 5), dy, padding=2).permute(2, 3, 1, 0).reshape(-1)   # HWIO
+    refb = dy.sum(dim=(0, 2, 3))
+    s2, sb = M.PARAM_SPECS[2], M.PARAM_SPECS[3]
+    got = g8[s2.offset:s2.offset + s2.numel]
+    gotb = g8[sb.offset:sb.offset + sb.numel]
+    eng._w8 = {}                                   # the bf16 conv2 weight gradient, same batch
+    gbf = eng.compute_gradients().clone()[s2.offset:s2.offset + s2.numel]
+    torch.cuda.synchronize()
+    out = {"B": B, "rel_fp8": _rel(got, ref), "rel_bf16": _rel(gbf, ref), "rel_bias": _rel(gotb, refb),
+           "cos_fp8": float(torch.nn.functional.cosine_similarity(got, ref, dim=0))}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(f"gpurun_out/fp8_wgrad_numerics_b{B}.json", "w") as f:
+        json.dump(out, f)
+    assert out["rel_bf16"] < 1e-2, out
+    assert out["rel_fp8"] < 6e-2 and out["cos_fp8"] > 0.998, out
+    assert out["rel_bias"] < 2e-2, out             # (from the e4m3 dY bytes, one ones-MFMA per chunk)
+
+
 def test_fp8_training_tracks_scales_and_reduces_loss():
     from dmlc.data import synthetic
     data, labels = synthetic(2048, seed=9, learnable=True)

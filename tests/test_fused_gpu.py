@@ -534,3 +534,67 @@ def test_xraw_prefetch_is_bit_identical(B):
     assert torch.equal(pre.bidx, ref.bidx)
     for s in (9, 14):
         assert pre.read_stats(s) == ref.read_stats(s), s
+
+
+_SPIN0 = "spin0:-DDMLC_SPIN_LIMIT=0"
+_SPIN0_SCRIPT = r"""
+import json, sys, torch
+sys.path.insert(0, sys.argv[1])
+import dmlc  # noqa: F401
+from dmlc.engine.fused import FusedCifarEngine
+B = int(sys.argv[2])
+g = torch.Generator().manual_seed(0)
+x = torch.randint(0, 256, (4 * B, 32, 32, 3), dtype=torch.uint8, generator=g)
+y = torch.randint(0, 10, (4 * B,), dtype=torch.int32, generator=g)
+eng = FusedCifarEngine(B, x, y, device="cuda", lr=1e-4, relu_logits=False)
+flags = {"fc_fused": eng.fc_fused, "wgrad_apply": eng.wgrad_apply, "fwd12_split": eng.fwd12_split}
+for _ in range(3):
+    eng.step()
+torch.cuda.synchronize()
+word = int(eng.wbar[320])
+try:
+    eng.check_barriers()
+    msg = ""
+except RuntimeError as e:
+    msg = str(e)
+print(json.dumps({"flags": flags, "word": word, "msg": msg, "flags_rezeroed": int(eng.c12_flags.abs().sum())}))
+"""
+
+
+def _spin0(B, **env):
+    import json
+    import os
+    import subprocess
+    import sys
+    from dmlc import _build
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(_build.LIB_DIR, "libdmlc_hip_spin0.so")
+    if not os.path.exists(lib):
+        pytest.skip("diagnostic library not built: DMLC_VARIANT='" + _SPIN0 + "' python -c 'import __graft_entry__'"
+                    " ... _build.build()")
+    r = subprocess.run([sys.executable, "-c", _SPIN0_SCRIPT, repo, str(B)], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, DMLC_VARIANT=_SPIN0, **env))
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("B", [256, 64])
+def test_forced_spin_timeouts_name_kernel_and_switch(B):
+    """Round-6 hardening: a diagnostic build whose in-launch waits give up at the first
+    unsatisfied poll (-DDMLC_SPIN_LIMIT=0: the wgrad sub-grid barriers, the fc chain seams, the split
+    forward's flags) drives the REAL timeout paths.  The sticky error word then carries the wgrad bit
+    (1) and the hand-off bit (2), check_barriers() names the kernels and the environment switch that
+    turns each persistent launch off -- and with those three switches set the same library runs the
+    step with no wait left to time out (error word 0).  The kernels then read partial data: the
+    weights are garbage, which is what the error reports."""
+    got = _spin0(B)
+    f = got["flags"]
+    assert f["fc_fused"] and f["wgrad_apply"] and f["fwd12_split"] == (B <= 128), got
+    assert got["word"] & 1 and got["word"] & 2, got
+    m = got["msg"]
+    assert "k_wgrad" in m and "DMLC_WGRAD_SGD=0" in m, m
+    assert "k_fc_chain" in m and "DMLC_FC_FUSED=0" in m and "DMLC_FWD12_SPLIT=0" in m, m
+    assert got["flags_rezeroed"] == 0, got                 # check_barriers re-armed the split flags
+    off = _spin0(B, DMLC_FC_FUSED="0", DMLC_WGRAD_SGD="0", DMLC_FWD12_SPLIT="0")
+    assert not any(off["flags"].values()), off
+    assert off["word"] == 0 and off["msg"] == "", off

@@ -38,12 +38,13 @@ def main():
                          "apart, 0.4 us in the graph)")
     ap.add_argument("--graph", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--variant", default="", help="engine variant keys, key=0|1,... (bench.py --variant)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     a = ap.parse_args()
     g = torch.Generator().manual_seed(0)
     data = torch.randint(0, 256, (50000, 32, 32, 3), dtype=torch.uint8, generator=g)
     labels = torch.randint(0, 10, (50000,), dtype=torch.int32, generator=g)
     var = {k: bool(int(v)) for k, v in (kv.split("=") for kv in filter(None, a.variant.split(",")))}
-    eng = FusedCifarEngine(a.batch, data, labels, device="cuda", lr=1e-4, variant=var)
+    eng = FusedCifarEngine(a.batch, data, labels, device="cuda", lr=1e-4, variant=var, dtype=a.dtype)
     lib = ctypes.CDLL(_build.HIP_LIB)
     assert lib.dmlc_timing_enabled() == 1, "not a timing build"
     for _ in range(5):
