@@ -340,6 +340,16 @@ DEV void head_task(const DmlcFcArgs& a, int hb, char* smem, int tid) {
 }
 
 
+// Each block's second phase (backward tasks, ticket, conv2 dgrad) reads its arguments through
+// late_kernarg (common.h), so the entry block loads only what the head / forward tasks need; the
+// launch epoch's load is in flight through the first phase.
+#ifdef DMLC_EAGER_ARGS                         // A/B build: every field loaded in the entry block
+#define late_fc() a
+#define late_dg() dg
+#else
+#define late_fc() late_kernarg<DmlcFcArgs>(0)
+#define late_dg() late_kernarg<DmlcConv2DgradArgs>(kernarg_second<DmlcFcArgs, DmlcConv2DgradArgs>())
+#endif
 __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a, DmlcConv2DgradArgs dg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, blk = blockIdx.x;
@@ -347,22 +357,22 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a, DmlcConv2Dgrad
   const int64_t step = a.step ? *a.step : 0;   // fc1 shadow parity, LR of the fused SGD
   const int parity = (int)(step & 1);
   if (blk == 0 && tid == 0 && a.step_copy) *a.step_copy = step;
-  const int nc = ctask_count(a);
   __shared__ unsigned s_epoch;
-  if (tid == 0) s_epoch = ld_relaxed(epochW(a));
-  __syncthreads();                             // (in hand before this block can arrive below)
-  const unsigned epoch = s_epoch;
+  unsigned e0 = 0;
+  if (tid == 0) e0 = ld_relaxed(epochW(a));   // (in hand before this block can arrive below)
   if (blk < H) {
     // head block: its rows, then (after every head) the C tasks past the GEMM blocks' share
     head_task(a, blk, smem, tid);
-    const int G = FC_BLOCKS - H;
+    if (tid == 0) s_epoch = e0;
+    const DmlcFcArgs& L = late_fc();
+    const int G = FC_BLOCKS - H, nc = ctask_count(L);
     for (int t = G + blk; t < nc; t += H) {
       __syncthreads();
       PreRegs R;
-      const CTask T = ctask(a, t);
-      pre_issue(a, T, parity, R, tid);
-      pre_store(a, T, R, smem, tid);
-      c_task(a, T, R, step, smem, tid, epoch);
+      const CTask T = ctask(L, t);
+      pre_issue(L, T, parity, R, tid);
+      pre_store(L, T, R, smem, tid);
+      c_task(L, T, R, step, smem, tid, s_epoch);
     }
     DMLC_STAMP(DMLC_TK_HEAD, 6);
   } else {
@@ -375,18 +385,20 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a, DmlcConv2Dgrad
       fwd_issue(a, j, true, parity, F, tid);
       fwd_task(a, j, F, smem, tid);
     }
+    if (tid == 0) s_epoch = e0;
     DMLC_STAMP(DMLC_TK_GEMM, 1);
     // the backward task's seam-independent operands, issued only once the forward task has
     // published: its loads would otherwise share this CU's fabric rate with the forward's operands
     // (and the publish's vmcnt(0) would wait for them); the head's ~9 us covers their latency
-    const CTask T = ctask(a, j);
+    const DmlcFcArgs& L = late_fc();
+    const CTask T = ctask(L, j);
     if (T.kind >= 0) {
       PreRegs R;
-      pre_issue(a, T, parity, R, tid);
+      pre_issue(L, T, parity, R, tid);
       __syncthreads();                         // the forward's LDS staging is dead
-      pre_store(a, T, R, smem, tid);
+      pre_store(L, T, R, smem, tid);
       DMLC_STAMP(DMLC_TK_GEMM, 2);
-      c_task(a, T, R, step, smem, tid, epoch);
+      c_task(L, T, R, step, smem, tid, s_epoch);
       DMLC_STAMP(DMLC_TK_GEMM, 5);
     }
   }
@@ -394,26 +406,29 @@ __global__ __launch_bounds__(FT, 1) void k_fc_chain(DmlcFcArgs a, DmlcConv2Dgrad
   // ticket: one counter taking 256 arrivals in a row serialises them at the memory side); the
   // dgrad's dp2 counters are the epoch's set, so the ticket need not wait for the dgrad
   __syncthreads();
+  const unsigned epoch = s_epoch;
+  const DmlcFcArgs& L = late_fc();
   if (tid == 0) {
     wait_vm_all();
-    if (last_arrival(a.sync + 32 * 10, blk, FC_BLOCKS)) {
+    if (last_arrival(L.sync + 32 * 10, blk, FC_BLOCKS)) {
       for (int w = SY_A; w < SY_D; ++w)        // cntA, cntB
-        __hip_atomic_store(a.sync + 32 * w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(L.sync + 32 * w, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (int k = 0; k < 72; ++k)             // the other dp2 set
-        __hip_atomic_store(cntD(a, epoch + 1, 0, 0) + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(epochW(a), epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cntD(L, epoch + 1, 0, 0) + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(epochW(L), epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // the conv2 input gradient of image blk (dg.B = 0: a separate launch does it): its dp2 row tile
   // comes from this launch's dp2 tasks; everything else it reads was written by earlier launches
-  if (dg.split) {                              // B <= 128: image b's input-channel half h
-    if (blk < 2 * dg.B) {
+  const DmlcConv2DgradArgs& D = late_dg();
+  if (D.split) {                               // B <= 128: image b's input-channel half h
+    if (blk < 2 * D.B) {
       int b, h;
       split_index<2>(blk, b, h);
-      conv2_dgrad_split_image<true>(dg, b, h, smem, seamD(a, epoch, b >> 6), a.err);
+      conv2_dgrad_split_image<true>(D, b, h, smem, seamD(L, epoch, b >> 6), L.err);
     }
-  } else if (blk < dg.B) {
-    conv2_dgrad_image<true>(dg, blk, smem, seamD(a, epoch, blk >> 6), a.err);
+  } else if (blk < D.B) {
+    conv2_dgrad_image<true>(D, blk, smem, seamD(L, epoch, blk >> 6), L.err);
   }
   if (blk < H) DMLC_STAMP(DMLC_TK_HEAD, 7);
   else DMLC_STAMP(DMLC_TK_GEMM, 6);

@@ -684,6 +684,15 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
   DMLC_STAMP(DMLC_TK_SGD, 2);
 }
 
+// The late phases (fc dW tiles, reductions + SGD, helpers, next-batch copy) read their arguments
+// through late_kernarg (common.h): the entry block loads only what the conv bodies need (same-box
+// A/B, 300 steps: B=256 3.40 -> 3.55 M img/s, B=128 2.02 -> 2.11 M; profiles/r6_late_args_ab.txt).
+#ifdef DMLC_EAGER_ARGS                         // A/B build: every field loaded in the entry block
+#define late_args() a
+#else
+#define late_args() late_kernarg<DmlcWgradArgs>(0)
+#endif
+
 // Both weight gradients in ONE launch (no stream fork/join in the step graph): blocks [0, g1) run
 // the conv1 body, the next 4 * g2 the conv2 body.  One block per CU (LDS): g1 + 4 * g2 <= 256 keeps
 // every block resident in one wave of blocks.
@@ -712,7 +721,8 @@ __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
   }
   if (conv1) {
     conv1_wgrad_block(a.w1, blockIdx.x, smem, a.apply != 0);
-    if (a.apply && a.fc_in_launch) {
+    const DmlcWgradArgs& L = late_args();
+    if (a.apply && L.fc_in_launch) {
       // arrive at the conv1 barrier, then the fc weight gradients + their SGD (inputs from earlier
       // launches: no waits) while the rest of the family arrives, then the conv1 reduction + SGD;
       // the conv2 help comes last, when the conv2 slabs are ready anyway (running the fc tiles
@@ -720,30 +730,30 @@ __global__ __launch_bounds__(W1T, 1) void k_wgrad(DmlcWgradArgs a) {
       // (the first task's operand loads go out before the slab stores are drained: the arrival
       // waits for both at once)
       const int parity = (int)(step & 1);
-      if (blockIdx.x >= FC_DW_TASKS) conv1_arrive(a, g0);
-      for (int d = blockIdx.x; d < FC_DW_TASKS; d += a.w1.g1) {
+      if (blockIdx.x >= FC_DW_TASKS) conv1_arrive(L, g0);
+      for (int d = blockIdx.x; d < FC_DW_TASKS; d += L.w1.g1) {
         const CTask T = dw_ctask(d);
         PreRegs R;
-        pre_issue(a.fc, T, parity, R, threadIdx.x);
+        pre_issue(L.fc, T, parity, R, threadIdx.x);
         const bool first = d == (int)blockIdx.x;
-        dw_task<false>(a.fc, T, R, step, smem, threadIdx.x, [&]() {
-          if (first) conv1_arrive(a, g0);
+        dw_task<false>(L.fc, T, R, step, smem, threadIdx.x, [&]() {
+          if (first) conv1_arrive(L, g0);
         });
       }
       DMLC_STAMP(DMLC_TK_SGD, 3);
-      conv1_apply(a, blockIdx.x, smem, g0, step, true);
+      conv1_apply(L, blockIdx.x, smem, g0, step, true);
     } else if (a.apply) {
-      conv1_apply(a, blockIdx.x, smem, g0, step);
+      conv1_apply(L, blockIdx.x, smem, g0, step);
     }
-    if (helper) conv2_help(a, blockIdx.x, smem, hg0, step);
+    if (helper) conv2_help(L, blockIdx.x, smem, hg0, step);
     // the next step's raw images over xraw: every conv1 block passed the conv1 barrier after its
     // image loop, so no block of this launch reads xraw any more
-    if (a.apply && a.sgd.mode == 0 && a.sgd.xnext)
-      for (int r = blockIdx.x; r < a.sgd.bidx_n; r += a.w1.g1) copy_next_row(a.sgd, step, r, threadIdx.x);
+    if (a.apply && L.sgd.mode == 0 && L.sgd.xnext)
+      for (int r = blockIdx.x; r < L.sgd.bidx_n; r += L.w1.g1) copy_next_row(L.sgd, step, r, threadIdx.x);
     DMLC_STAMP(DMLC_TK_SGD, 4);
   } else {
     conv2_wgrad_block(a.w2, blockIdx.x - a.w1.g1, a.w1.g1, smem, a.apply != 0);
-    if (a.apply) conv2_apply(a, c4, grp, smem, g0, step);
+    if (a.apply) conv2_apply(late_args(), c4, grp, smem, g0, step);
   }
 }
 static_assert(W1T == W2T, "k_wgrad runs both bodies with one block size");

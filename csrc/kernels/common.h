@@ -34,6 +34,25 @@ DEV f32x4 zero4() { f32x4 z = {0.f, 0.f, 0.f, 0.f}; return z; }
 // threadIdx.x >> 6 uniform, and everything derived from it would otherwise be VALU work
 DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
+// A launch argument read through an opaque pointer into the kernarg segment, made where a kernel's
+// late phase starts.  hipcc loads every field a kernel ever reads in its entry block, and with ~100
+// SGPRs live it serialises them (k_wgrad: ~45 scalar-load round trips, 3.4 us, before the first
+// body instruction); loads through this reference cannot be hoisted above the asm.  The kernarg
+// segment pointer, not &param: taking a by-value parameter's address copies it to scratch.
+// (The opaque value is the 32-bit offset, made uniform again by readfirstlane: an "s"-constrained
+// pointer is an illegal VGPR-to-SGPR copy wherever the compiler's divergence analysis loses it.)
+template <class T> DEV const T& late_kernarg(unsigned off) {
+  typedef __attribute__((address_space(4))) const char* cptr;
+  asm volatile("" : "+v"(off));
+  off = __builtin_amdgcn_readfirstlane(off);
+  return *(const T*)((cptr)__builtin_amdgcn_kernarg_segment_ptr() + off);
+}
+// byte offset of a kernel's second by-value argument (arguments are laid out in order, each at its
+// own alignment)
+template <class A, class B> constexpr unsigned kernarg_second() {
+  return (unsigned)((sizeof(A) + alignof(B) - 1) / alignof(B) * alignof(B));
+}
+
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of row q, columns 4p..4p+3
 // of a 4x16 block of 16-bit elements; lane i of the group receives column i (row q in element q).
 // Two reads (rows kb..kb+3 and kb+4..kb+7) give the 8-element MFMA fragment of one column.
