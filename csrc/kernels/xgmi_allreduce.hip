@@ -218,12 +218,18 @@ __global__ __launch_bounds__(XT) void k_xgmi_allreduce_sgd(XgmiArgs a, DmlcSgdAr
   __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * XT, t0 = (int64_t)blockIdx.x * XT + threadIdx.x;
   xgmi_exchange<W, BF16>(a, s_e, t0, stride);
-  const float lr = lr_of(s, step);
-  for (int64_t i = a.off4 + t0; i < a.off4 + a.n4; i += stride) sgd_apply4(s, i, lr, step);
-  if (s.bidx && t0 < s.bidx_n) s.bidx[t0] = order_row(s.next, step + 1, (int)t0);
-  if (s.xnext)
-    for (int r = blockIdx.x; r < s.bidx_n; r += gridDim.x) copy_next_row(s, step, r, threadIdx.x);
-  if (blockIdx.x == 0 && threadIdx.x < 64) publish_step(s, step, lr, threadIdx.x);
+  // the SGD's arguments through late_kernarg (common.h): not loaded before the exchange starts
+#ifdef DMLC_EAGER_ARGS
+  const DmlcSgdArgs& S = s;
+#else
+  const DmlcSgdArgs& S = late_kernarg<DmlcSgdArgs>(kernarg_second<XgmiArgs, DmlcSgdArgs>());
+#endif
+  const float lr = lr_of(S, step);
+  for (int64_t i = a.off4 + t0; i < a.off4 + a.n4; i += stride) sgd_apply4(S, i, lr, step);
+  if (S.bidx && t0 < S.bidx_n) S.bidx[t0] = order_row(S.next, step + 1, (int)t0);
+  if (S.xnext)
+    for (int r = blockIdx.x; r < S.bidx_n; r += gridDim.x) copy_next_row(S, step, r, threadIdx.x);
+  if (blockIdx.x == 0 && threadIdx.x < 64) publish_step(S, step, lr, threadIdx.x);
   if (threadIdx.x == 0) st_sys(&self->epoch[blockIdx.x], s_e);
 }
 
