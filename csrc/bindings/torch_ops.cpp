@@ -469,12 +469,16 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
   check(loss_part, "loss_part", at::kFloat, {B / 4});
   check(correct_part, "correct_part", at::kInt, {B / 4});
   check(dp2, "dp2", at::kBFloat16, {B, 2304});
-  check_numel(gw1, "gw1", at::kFloat, 2304 * 384);
-  check_numel(gw2, "gw2", at::kFloat, 384 * 192);
-  check_numel(gw3, "gw3", at::kFloat, 192 * 10);
-  check_numel(gb1, "gb1", at::kFloat, 384);
-  check_numel(gb2, "gb2", at::kFloat, 192);
-  check_numel(gb3, "gb3", at::kFloat, 10);
+  // the fc gradients: fp32 views of the flat gradient, or bf16 views (the RCCL bf16 wire, no fused SGD)
+  const bool g16 = gw1.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(!g16 || !fuse_sgd, "fc_chain: bf16 gradient views only without the fused SGD");
+  const auto gt = g16 ? at::kBFloat16 : at::kFloat;
+  check_numel(gw1, "gw1", gt, 2304 * 384);
+  check_numel(gw2, "gw2", gt, 384 * 192);
+  check_numel(gw3, "gw3", gt, 192 * 10);
+  check_numel(gb1, "gb1", gt, 384);
+  check_numel(gb2, "gb2", gt, 192);
+  check_numel(gb3, "gb3", gt, 10);
   check_numel(step, "step", at::kLong, 1);
   check_min(sync, "sync", at::kInt, 212 * 32);   // fc_common.h SY_END
   check_min(err, "err", at::kInt, 1);
@@ -494,8 +498,9 @@ void fc_chain(const Tensor& p2, const Tensor& fc1n, const Tensor& h1part, const 
   a.h1 = h1.data_ptr(); a.h2 = h2.data_ptr(); a.dl = dl.data_ptr(); a.dh1 = dh1.data_ptr(); a.dh2 = dh2.data_ptr();
   a.loss_part = loss_part.data_ptr<float>(); a.correct_part = correct_part.data_ptr<int>();
   a.dp2 = dp2.data_ptr();
-  a.gw1 = gw1.data_ptr<float>(); a.gw2 = gw2.data_ptr<float>(); a.gw3 = gw3.data_ptr<float>();
-  a.gb1 = gb1.data_ptr<float>(); a.gb2 = gb2.data_ptr<float>(); a.gb3 = gb3.data_ptr<float>();
+  a.gw1 = (float*)gw1.data_ptr(); a.gw2 = (float*)gw2.data_ptr(); a.gw3 = (float*)gw3.data_ptr();
+  a.gb1 = (float*)gb1.data_ptr(); a.gb2 = (float*)gb2.data_ptr(); a.gb3 = (float*)gb3.data_ptr();
+  a.grad_bf16 = g16 ? 1 : 0;
   a.fuse_sgd = fuse_sgd ? 1 : 0;
   a.dw_tasks = dw_tasks ? 1 : 0;
   if (fc2n.has_value()) {
@@ -557,7 +562,10 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
   }
   const int64_t end = off[9] + 10;
   check_min(master, "master", at::kFloat, end);
-  check_min(grad, "grad", at::kFloat, end);
+  // the flat gradient: fp32, or bf16 (DmlcSgdArgs::grad16: the RCCL bf16 wire, modes 1 / 2 only)
+  const bool g16 = grad.scalar_type() == at::kBFloat16;
+  check_min(grad, "grad", g16 ? at::kBFloat16 : at::kFloat, end);
+  TORCH_CHECK(!g16 || mode == 1 || mode == 2, "sgd: a bf16 gradient only in modes 1 / 2 (data parallel)");
   const int64_t g1 = part1.size(0), g2 = part2.size(0);
   check(part1, "part1", at::kFloat, {g1, 80, 64});
   check(partb1, "partb1", at::kFloat, {g1, 64});
@@ -583,7 +591,9 @@ static DmlcSgdArgs make_sgd(const Tensor& master, const Tensor& grad, int64_t mo
   dev(stats, "stats");
   TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.dim() == 2 && stats.size(1) == 4, "stats must be [R,4] fp32");
   DmlcSgdArgs a;
-  a.master = master.data_ptr<float>(); a.grad = grad.data_ptr<float>();
+  a.master = master.data_ptr<float>();
+  a.grad = g16 ? nullptr : grad.data_ptr<float>();
+  a.grad16 = g16 ? grad.data_ptr() : nullptr;
   a.mode = (int)mode; a.grad_scale = (float)grad_scale;
   for (int i = 0; i < 10; ++i) a.off[i] = (int)off[i];
   a.part1 = part1.data_ptr<float>(); a.partb1 = partb1.data_ptr<float>(); a.g1 = (int)g1;
@@ -662,6 +672,7 @@ void xgmi_allreduce_sgd(int64_t ctx, int64_t blocks, bool bf16_wire, DMLC_SGD_PA
   TORCH_CHECK(mode == 2 && roles == 0 && finalize && !fc1_fused && !w2f8.has_value() && step_rd.has_value(),
               "xgmi_allreduce_sgd: apply mode (2) over every role, bf16 shadows, the head's step copy");
   DmlcSgdArgs a = make_sgd(DMLC_SGD_ARGS);
+  TORCH_CHECK(!a.grad16, "xgmi_allreduce_sgd: the exchange buffer is fp32");
   c10::DeviceGuard guard(master.device());
   CHECK_HIP(dmlc_xgmi_allreduce_sgd((int)ctx, (int)blocks, bf16_wire ? 1 : 0, &a, stream_of(master)));
 }

@@ -219,6 +219,7 @@ struct DmlcFcArgs {
   const int64_t* step; int64_t* step_copy;             // device step counter; copy for the SGD reader
   unsigned int* sync;                // >= 28 * 32 zeroed uints (counters re-arm themselves)
   unsigned int* err;                 // sticky error word (value 2 = bit 1: a seam wait timed out)
+  int grad_bf16;                     // fuse_sgd 0: gw1..gb3 are bf16 views (DmlcSgdArgs::grad16)
 };
 
 // Fused SGD over the flat fp32 parameter buffer (+ split-K partial reduction, LR schedule from the
@@ -270,6 +271,11 @@ struct DmlcSgdArgs {
   // batch row b at step+1] (3072 B each), so the next forward reads its image without the index
   // hop (DmlcConv1FwdArgs::xraw_in)
   uint8_t* xnext; const uint8_t* xdata;
+  // nullable: the flat gradient in bf16 (data parallel over RCCL with the bf16 wire).  Then modes 1/2
+  // write / read it instead of `grad` (null): the producers round once, the all-reduce runs on it in
+  // place and the SGD reads it -- bitwise the fp32 gradient + cast + all-reduce + cast-back path,
+  // without the two cast launches
+  void* grad16;
 };
 
 // Both weight gradients in one launch (blocks [0,g1): conv1; then 4 * g2 conv2 blocks, one slab per group).

@@ -268,6 +268,24 @@ __global__ __launch_bounds__(256) void k_gemm_grouped(DmlcGemmGroup G) {
 using namespace dmlc;
 
 extern "C" hipError_t dmlc_gemm_grouped(DmlcGemmGroup* G, hipStream_t s) {
+#ifndef DMLC_GEMM_FIFO
+  // Longest blocks first: workgroups are dispatched in blockIdx order, so the problems are laid out
+  // by descending k-steps per block (stable).  In the B > 256 backward the K = batch weight-gradient
+  // tiles (dW1: 216 blocks of 32 k-steps at B = 1024) otherwise start behind the 576 short dp2 tiles
+  // and end the launch alone.  The kernel locates a problem by its block range only.
+  {
+    auto work = [](const DmlcGemmProblem& P) {     // k-steps per block
+      const int ks = (P.K + 31) / 32, sp = P.ksplit > 1 ? P.ksplit : 1;
+      return P.c_mode == 3 ? 0 : (ks + sp - 1) / sp;
+    };
+    for (int i = 1; i < G->nprob; ++i)
+      for (int j = i; j > 0 && work(G->p[j]) > work(G->p[j - 1]); --j) {
+        const DmlcGemmProblem t = G->p[j];
+        G->p[j] = G->p[j - 1];
+        G->p[j - 1] = t;
+      }
+  }
+#endif
   int blocks = 0;
   for (int i = 0; i < G->nprob; ++i) {
     DmlcGemmProblem& P = G->p[i];

@@ -45,8 +45,8 @@ DEV void conv2_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   if (a.mode == 0 || a.mode == 1)
     g = split_sum<C2_SPLIT>(reinterpret_cast<const float*>(a.part2) + e, 1600 * 64, a.g2, lds, threadIdx.x);
   if (threadIdx.x >= T) return;
-  if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[2] + e);
-  if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[2] + e) = g; return; }
+  if (a.mode == 2) g = grad_ld4(a, a.off[2] + e);
+  if (a.mode == 1) { grad_st4(a, a.off[2] + e, g); return; }
   const float4 w = sgd4(a.master + a.off[2] + e, w0, g, lr, a.grad_scale, a.mode != 3);
   const int ci = krow & 63, khw = krow >> 6;
   if (a.w2f8) {                                       // fp8 shadow for the fp8 conv2 forward
@@ -87,8 +87,8 @@ DEV void conv1_rows(const DmlcSgdArgs& a, int blk, float lr, float4* lds) {
   if (a.mode == 0 || a.mode == 1)                     // slab row k'' = kh*16 + kw*3 + ci
     g = split_sum<C1_SPLIT, C1_LOADS>(a.part1 + (size_t)(kh * 16 + kw * 3 + ci) * 64 + co, 80 * 64, a.g1, lds, threadIdx.x);
   if (threadIdx.x >= T) return;
-  if (a.mode == 2) g = *reinterpret_cast<const float4*>(a.grad + a.off[0] + e);
-  if (a.mode == 1) { *reinterpret_cast<float4*>(a.grad + a.off[0] + e) = g; return; }
+  if (a.mode == 2) g = grad_ld4(a, a.off[0] + e);
+  if (a.mode == 1) { grad_st4(a, a.off[0] + e, g); return; }
   conv1_shadow4(a, row, co, sgd4(a.master + a.off[0] + e, w0, g, lr, a.grad_scale, a.mode != 3));
 }
 

@@ -509,7 +509,7 @@ DEV void conv2_reduce(const DmlcWgradArgs& A, int c4, int f_begin, int f_end, fl
     if (sp == 0 && ok) {
       const float4 t = add4(add4(add4(acc, o[0]), o[1]), o[2]);
       if (s.mode == 1) {
-        *reinterpret_cast<float4*>(s.grad + s.off[2] + e) = t;   // reduce only (data parallel)
+        grad_st4(s, s.off[2] + e, t);                          // reduce only (data parallel)
       } else {
         const float4 w = sgd4(s.master + s.off[2] + e, w0, t, lr, s.grad_scale, true);
         conv2_shadow4(s, krow, co, w);
@@ -669,7 +669,7 @@ DEV void conv1_apply(const DmlcWgradArgs& A, int grp, char* smem, unsigned g0, i
       float4 t = lds[ol];
 #pragma unroll
       for (int k = 1; k < C1_SPLIT; ++k) t = add4(t, lds[k * 16 + ol]);
-      if (s.mode == 1) *reinterpret_cast<float4*>(s.grad + s.off[0] + e) = t;   // reduce only
+      if (s.mode == 1) grad_st4(s, s.off[0] + e, t);                           // reduce only
       else conv1_shadow4(s, row, co, sgd4(s.master + s.off[0] + e, w0, t, lr, s.grad_scale, true));
     }
     lds_barrier();

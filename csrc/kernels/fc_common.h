@@ -444,6 +444,8 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
       float v = mb[n0 + tid];
       v -= f * sum;
       mb[n0 + tid] = v;
+    } else if (a.grad_bf16) {
+      ((bf16*)(T.kind == 1 ? uni(a.gb1) : T.kind == 2 ? uni(a.gb2) : uni(a.gb3)))[n0 + tid] = (bf16)sum;
     } else {
       ((float*)(T.kind == 1 ? uni(a.gb1) : T.kind == 2 ? uni(a.gb2) : uni(a.gb3)))[n0 + tid] = sum;
     }
@@ -518,6 +520,17 @@ DEV void dw_task(const DmlcFcArgs& a, const CTask& T, const PreRegs& R, int64_t 
     const int m = m0 + rr, n = n0 + cc;
     if (m >= M || n >= N) continue;
     const float4 v = *reinterpret_cast<const float4*>(ct + rr * CT_LD + cc);
+    if (a.grad_bf16) {                         // the bf16 flat gradient (RCCL bf16 wire)
+      bf16* Cb = (bf16*)(T.kind == 1 ? uni(a.gw1) : T.kind == 2 ? uni(a.gw2) : uni(a.gw3));
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      if (ldc % 4 == 0 && n + 4 <= N) {
+        *reinterpret_cast<bf16x4*>(Cb + (size_t)m * ldc + n) = pack4(v.x, v.y, v.z, v.w);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) if (n + k < N) Cb[(size_t)m * ldc + n + k] = (bf16)vv[k];
+      }
+      continue;
+    }
     float* C = (float*)(T.kind == 1 ? uni(a.gw1) : T.kind == 2 ? uni(a.gw2) : uni(a.gw3));
     if (ldc % 4 == 0 && n + 4 <= N) {
       *reinterpret_cast<float4*>(C + (size_t)m * ldc + n) = v;

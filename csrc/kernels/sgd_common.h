@@ -36,6 +36,22 @@ __host__ __device__ inline int fc1_blocks(const DmlcSgdArgs& a) {
 // fc roles (fc1 bias / weights, fc2 tiles, fc tail) in launch order
 __host__ __device__ inline int fc_role_count(const DmlcSgdArgs& a) { return fc1_blocks(a) + FC2_BLOCKS + FC_TAIL_BLOCKS; }
 
+// The flat gradient, element e: fp32 `grad`, or bf16 `grad16` on the RCCL bf16 wire (api.h).
+DEV float4 grad_ld4(const DmlcSgdArgs& a, size_t e) {
+  if (a.grad16) {
+    const bf16x4 v = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const bf16*>(a.grad16) + e);
+    return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+  }
+  return *reinterpret_cast<const float4*>(a.grad + e);
+}
+DEV void grad_st4(const DmlcSgdArgs& a, size_t e, const float4& g) {
+  if (a.grad16) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(a.grad16) + e) = pack4(g.x, g.y, g.z, g.w);
+  else *reinterpret_cast<float4*>(a.grad + e) = g;
+}
+DEV float grad_ld1(const DmlcSgdArgs& a, size_t e) {
+  return a.grad16 ? (float)reinterpret_cast<const bf16*>(a.grad16)[e] : a.grad[e];
+}
+
 DEV float lr_of(const DmlcSgdArgs& a, int64_t step) {
   return lr_sched(a.lr0, a.decay, a.decay_steps, a.staircase, a.warmup, step);
 }
@@ -125,9 +141,9 @@ DEV void conv_bias(const DmlcSgdArgs& a, int which, float lr, float4* lds, int t
     g = split_sum<16>((which == 0 ? a.partb1 : a.partb2) + c, 64, which == 0 ? a.g1 : a.g2, lds, tid, coh,
                       which == 0 ? a.partb1 : a.partb2);
   if (tid >= 16) return;
-  float* gp = a.grad + a.off[seg] + c;
-  if (a.mode == 1) { *reinterpret_cast<float4*>(gp) = g; return; }
-  if (a.mode == 2) g = *reinterpret_cast<const float4*>(gp);
+  const size_t ge = (size_t)a.off[seg] + c;
+  if (a.mode == 1) { grad_st4(a, ge, g); return; }
+  if (a.mode == 2) g = grad_ld4(a, ge);
   sgd4(a.master + a.off[seg] + c, w0, g, lr, a.grad_scale, a.mode != 3);
 }
 
@@ -145,7 +161,7 @@ DEV void fc1_block(const DmlcSgdArgs& a, int blk, float lr, int64_t step, int ti
     i4[u] = base4 + (blk * FC_F4_PER_THREAD + u) * 256 + tid;
     const int ic = i4[u] < end4 ? i4[u] : base4;             // branch-free loads (clamped)
     w[u] = reinterpret_cast<const float4*>(a.master)[ic];
-    g[u] = reinterpret_cast<const float4*>(a.grad)[ic];
+    g[u] = grad_ld4(a, (size_t)ic * 4);
   }
 #pragma unroll
   for (int u = 0; u < FC_F4_PER_THREAD; ++u) {
@@ -179,7 +195,7 @@ DEV void fc2_block(const DmlcSgdArgs& a, int blk, float lr, bf16* tl /*[FC2_COLS
       const int j4 = u * 256 + tid, kk = j4 / C4, n = n0 + 4 * (j4 - kk * C4);
       const size_t e = (size_t)a.off[6] + (size_t)(k0 + kk) * 192 + n;
       w[u] = *reinterpret_cast<const float4*>(a.master + e);
-      g[u] = *reinterpret_cast<const float4*>(a.grad + e);
+      g[u] = grad_ld4(a, e);
     }
 #pragma unroll
     for (int u = 0; u < F4; ++u) {
@@ -212,7 +228,7 @@ DEV void fc_tail_block(const DmlcSgdArgs& a, int blk, float lr, int tid) {
   const int i = a.off[7] + j;
   float v = a.master[i];
   if (a.mode != 3) {
-    v -= lr * a.grad_scale * a.grad[i];
+    v -= lr * a.grad_scale * grad_ld1(a, i);
     a.master[i] = v;
   }
   if (i >= a.off[8] && i < a.off[8] + 1920) {

@@ -154,7 +154,7 @@ class EagerTrainer:
                 for p in self.model.parameters():
                     p.grad = None
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):           # records only: the model does not advance here
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):   # records only (model unchanged)
                     self._out = self._fwd_bwd_sgd(self._xs, self._ys, self._lr_t)
                 self.graph = g
                 torch.cuda.synchronize(self.device)

@@ -28,7 +28,10 @@ dgrad as its own launch and the SGD as its own launch.
 Data parallel (N > 1): the wgrad launch reduces the conv slabs into the flat gradient instead of
 applying them, then the gradient is exchanged and applied -- serial schedule: one all-reduce of the
 whole flat gradient (xGMI peer-to-peer kernel or RCCL) and one SGD launch; overlap schedule: the fc
-bucket on a comm stream beside the conv backward.
+bucket's all-reduce on a comm stream beside the wgrad launch, the conv bucket after it on the same
+stream, the conv SGD on the main stream and the fc SGD on the comm stream beside the NEXT step's
+forward (_dp_step).  bench.py times both before the timed region and keeps the
+faster (tune_schedule).
 
 Every data-consuming kernel computes its batch rows from the device-resident global_step and the
 generated epoch order (data/order.py: a keyed Feistel permutation per epoch, no index buffer), so
@@ -94,6 +97,8 @@ VARIANT_DEFAULTS = {
     "fwd12_split": True,       # B <= 128: conv1 + conv2 forward in one launch, two workgroups per image;
                                # env DMLC_FWD12_SPLIT=0 off
     "fc_sgd_in_chain": None,   # single GPU, dW tiles in the fc chain: every fc SGD in their epilogues (default B < 256)
+    "grad16": True,            # data parallel, RCCL, bf16 wire, fc chain: the producers write a bf16 flat gradient
+                               # (no cast launches around the all-reduce; bitwise the cast path)
 }
 # int32 words of the SGD arrival ticket (DMLC_TICKET_WORDS in csrc/kernels/api.h)
 TICKET_WORDS = 9 * 32
@@ -295,6 +300,18 @@ class FusedCifarEngine:
         self.pv = p
         gv = {k: self.grad[s.offset:s.offset + s.numel] for k, s in SEG.items()}
         self.gv = gv
+        # data parallel over RCCL with the bf16 wire: the fc chain (its dW tiles), the wgrad launch's
+        # conv-slab reduction / the reduce-only SGD launch write the gradient as bf16 into grad16, the
+        # all-reduce runs on it in place and the apply-only SGD reads it (DmlcSgdArgs::grad16) -- the
+        # fp32 gradient + t.to(bf16) + all-reduce + copy back, bit for bit, minus two cast launches of
+        # 4.27 / 2.1 MB (world-1 A/B: +13.1 us over the single-GPU step with the casts vs +5.7 fp32,
+        # profiles/r6s2_dp1_ab_grad16_bf16.jsonl).  The three-launch fc path writes fp32 only: fc chain
+        # engines (B <= 256, a GPU per rank) only.
+        self.grad16 = None
+        if (self.dp and comm_dtype == "bf16" and self.xgmi is None and self.fc_fused and bool(V["grad16"])):
+            self.grad16 = torch.zeros(self.master.numel(), dtype=torch.bfloat16, device=dev)
+        self.gv_chain = ({k: self.grad16[s.offset:s.offset + s.numel] for k, s in SEG.items()}
+                         if self.grad16 is not None else gv)
 
         # grouped GEMM problem lists (the three-launch fc path)
         self._fc1_fwd = dict(A=[self.p2.view(B, 2304)], B=[self.fc1n], C=[self.h1part], bias=[None],
@@ -539,6 +556,8 @@ class FusedCifarEngine:
         p, gv = self.pv, self.gv
         sched = [self.lr0, self.decay, self.decay_steps, 1.0 if self.staircase else 0.0, self.warmup, 1.0]
         all_sgd = fused_sgd and self.fc_sgd_in_chain
+        if not fused_sgd:
+            gv = self.gv_chain                   # (bf16 views on the RCCL bf16 wire)
         g = p if all_sgd else gv                 # every fc SGD here: the master views, else the gradients
         self.ops.fc_chain(self.p2.view(self.B, 2304), self.fc1n, self.h1part8, p["full_bias_1"], self.fc2t,
                           p["full_bias_2"], self.fc3t, p["full_bias_3"], self.fc3d, self.labels, idx, counter, period,
@@ -583,7 +602,8 @@ class FusedCifarEngine:
 
     def _sgd_args(self, mode: int, scale: float = 1.0, roles: int = 0, finalize: bool = True,
                   fc1_fused: bool = False) -> tuple:
-        return (self.master, self.grad, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.partb2,
+        gflat = self.grad16 if (self.grad16 is not None and mode in (1, 2)) else self.grad
+        return (self.master, gflat, mode, scale, SEG_OFF, self.part1, self.partb1, self.part2, self.partb2,
                 self.w1f, self.w2f, self.w2d, self.fc1n, self.fc2t, self.fc2n, self.fc3t, self.fc3d,
                 self.step_t, self.lr0, self.decay, self.decay_steps, self.staircase, self.ticket,
                 self.loss_part, self.correct_part, self.stats,
@@ -630,7 +650,9 @@ class FusedCifarEngine:
 
     def _allreduce(self, t: torch.Tensor):
         import torch.distributed as dist
-        if self.comm_dtype == "bf16":
+        if t.dtype == torch.bfloat16:            # grad16: already on the wire's dtype
+            dist.all_reduce(t, group=self.pg)
+        elif self.comm_dtype == "bf16":
             tb = t.to(torch.bfloat16)
             dist.all_reduce(tb, group=self.pg)
             t.copy_(tb)
@@ -641,8 +663,17 @@ class FusedCifarEngine:
         off, n = self._buckets[fc]
         if self.xgmi is not None:
             self.xgmi.all_reduce(off, n)
+        elif fc or self.grad16 is not None:
+            self._allreduce(self._wire_grad()[off:off + n])
         else:
-            self._allreduce(self.grad[off:off + n])
+            # the 0.43 MB conv bucket sits on the step's critical path: fp32 on any wire (latency-bound
+            # at this size; the bf16 wire's two cast kernels would cost more than the bytes it saves)
+            import torch.distributed as dist
+            dist.all_reduce(self.grad[off:off + n], group=self.pg)
+
+    def _wire_grad(self) -> torch.Tensor:
+        """The flat gradient the collectives run on (grad16 on the RCCL bf16 wire)."""
+        return self.grad16 if self.grad16 is not None else self.grad
 
     def check_comm(self):
         """Raise if the xGMI all-reduce saw a peer stop participating (sticky device error word) or a
@@ -668,6 +699,12 @@ class FusedCifarEngine:
         self._forward(self.bidx, None, 1, train=True)
         self._fc_backward()
 
+    def _seg_forward(self):
+        self._forward(self.bidx, None, 1, train=True)
+
+    def _seg_fc(self):
+        self._fc_backward()
+
     def _seg_compute_b(self):
         if self.wgrad_reduce:                   # conv slabs reduced inside the wgrad launch
             self._conv_backward(reduce=True)
@@ -675,9 +712,11 @@ class FusedCifarEngine:
         self._seg_compute_b_launch()
 
     def _seg_compute_b_launch(self):
-        """conv backward + the slab reduction as its own SGD launch.  The overlap schedule always uses
-        it: its wgrad launch runs beside comm-stream kernels, so the in-launch sub-grid barriers would
-        not have the co-residency they assume (a wait on another GPU's progress could close a cycle)."""
+        """conv backward + the slab reduction as its own SGD launch (when the in-launch reduction is
+        off: ranks sharing a GPU, DMLC_WGRAD_SGD=0).  The overlap schedule's wgrad launch runs beside
+        the comm stream's fc all-reduce: its sub-grid barriers stay deadlock-free there because the
+        collective never waits on a kernel of this GPU -- a wgrad block that is not yet resident gets
+        its CU once the collective finishes -- and every wait is bounded (error word, never a hang)."""
         self._conv_backward()
         self._sgd(mode=1 if self.dp else 0)
 
@@ -702,7 +741,7 @@ class FusedCifarEngine:
         g = self._compute_gradients(idx)
         if check:
             self.check_barriers()
-        return g
+        return g if self.grad16 is None else self.grad16.float()   # (grad16: a converted copy)
 
     def _compute_gradients(self, idx: Optional[torch.Tensor] = None):
         if idx is None:
@@ -729,6 +768,7 @@ class FusedCifarEngine:
         interrupted capture): the next step starts clean instead of failing the pairing checks."""
         self._fc_src = None
         self._dgrad_done = False
+        self._pending_comm = None          # callers synchronise the device first (capture())
         if self.fwd12_split and not torch.cuda.is_current_stream_capturing():
             self.c12_flags.zero_()         # stream-ordered: no half-finished hand-off carries over
 
@@ -738,6 +778,8 @@ class FusedCifarEngine:
         except BaseException:
             self._reset_step_state()
             raise
+        if not torch.cuda.is_current_stream_capturing():
+            self._join_comm()             # an eager step ends joined (captures join at the chain's end)
 
     def _eager_step_body(self):
         if not self.dp:
@@ -756,7 +798,8 @@ class FusedCifarEngine:
         if self.dp_schedule == "serial":
             self._serial_dp_step([self._seg_compute_ab, self._seg_apply])
             return
-        self._dp_step([self._seg_compute_a, self._seg_compute_b_launch, self._seg_apply_fc, self._seg_apply_conv])
+        self._dp_step([self._seg_forward, self._seg_fc, self._seg_compute_b, self._seg_apply_fc,
+                       self._seg_apply_conv])
 
     def _seg_compute_ab(self):
         self._seg_compute_a()
@@ -774,30 +817,51 @@ class FusedCifarEngine:
         if self.xgmi is not None:
             self.xgmi.all_reduce(0, n)
         else:
-            self._allreduce(self.grad[:n])
+            self._allreduce(self._wire_grad()[:n])
         seg[1]()
 
     def _dp_step(self, seg):
-        """Data-parallel step around two all-reduce buckets:
-            main: A = fwd + head + fc backward | B = conv backward + conv-grad reduction
-            comm:        wait A -> all-reduce fc grads -> apply fc  | wait B -> all-reduce conv grads -> apply conv
-        The fc bucket (90 % of the bytes) and the fc SGD overlap the conv backward."""
+        """Data-parallel step around two all-reduce buckets, two streams:
+            main: fwd | [join s-1] fc chain | wgrad (+ conv slab reduction) |        [wait] conv SGD (+ finalize)
+            comm:                  [wait] all-reduce fc | [wait] all-reduce conv -> fc SGD
+        Both collectives go through ONE stream in one order (one communicator, the same issue order on
+        every rank).  The fc bucket (90 % of the bytes) crosses the links while the wgrad launch runs;
+        only the 0.43 MB conv bucket and the conv SGD stay on the step's critical path.  The fc SGD
+        (fc weights + shadows) is NOT joined at the end of the step: the next step's forward does not
+        read an fc parameter, so the join sits before the next fc chain (the fc SGD runs beside the
+        next conv12 forward) -- :meth:`_join_comm` closes a sequence (end of a captured chain, an eager
+        step, before a graph replay).
+        seg: [forward, fc chain, conv backward, fc apply, conv apply] (eager launchers or, with eager
+        collectives, replays of the segment graphs)."""
         main = torch.cuda.current_stream(self.device)
         seg[0]()
-        ev = torch.cuda.Event()
-        ev.record(main)
-        self.comm_stream.wait_event(ev)
+        self._join_comm()                       # step s-1's fc SGD wrote the shadows the chain reads
+        seg[1]()
+        ev_fc = torch.cuda.Event()
+        ev_fc.record(main)
+        self.comm_stream.wait_event(ev_fc)
         with torch.cuda.stream(self.comm_stream):
             self._allreduce_bucket(fc=True)
-            seg[2]()
-        seg[1]()
-        ev2 = torch.cuda.Event()
-        ev2.record(main)
-        self.comm_stream.wait_event(ev2)
+        seg[2]()
+        ev_wg = torch.cuda.Event()
+        ev_wg.record(main)
+        self.comm_stream.wait_event(ev_wg)
+        ev_conv, ev_done = torch.cuda.Event(), torch.cuda.Event()
         with torch.cuda.stream(self.comm_stream):
             self._allreduce_bucket(fc=False)
+            ev_conv.record(self.comm_stream)
             seg[3]()
-        main.wait_stream(self.comm_stream)
+            ev_done.record(self.comm_stream)
+        main.wait_event(ev_conv)
+        seg[4]()
+        self._pending_comm = ev_done
+
+    def _join_comm(self):
+        """The current stream waits for the last step's comm-stream work (the fc SGD)."""
+        ev = getattr(self, "_pending_comm", None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            self._pending_comm = None
 
     # --- graph capture --------------------------------------------------------------------------
     @property
@@ -818,11 +882,11 @@ class FusedCifarEngine:
         self.graphs, self.chains = [], {}
         pool = torch.cuda.graph_pool_handle()
         if self.single_graph:
-            segs = [self._eager_step]
+            segs = [lambda: self._steps_joined(1)]
         elif self.dp_schedule == "serial":
             segs = [self._seg_compute_ab, self._seg_apply]
         else:
-            segs = [self._seg_compute_a, self._seg_compute_b_launch, self._seg_apply_fc, self._seg_apply_conv]
+            segs = [self._seg_forward, self._seg_fc, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv]
         self._captured_schedule = self.dp_schedule
         # a capture records launches without running them: the step counter and weights are
         # identical before and after
@@ -831,7 +895,7 @@ class FusedCifarEngine:
         if self.single_graph:
             k = 2
             while k <= int(steps_per_graph):
-                self.chains[k] = self._capture_one(lambda k=k: [self._eager_step() for _ in range(k)], pool)
+                self.chains[k] = self._capture_one(lambda k=k: self._steps_joined(k), pool)
                 k *= 2
         self.chains[1] = self.graphs[0] if self.single_graph else None
         self._pool = pool
@@ -843,16 +907,26 @@ class FusedCifarEngine:
         k = int(k)
         if not self.single_graph or not self.graphs or k < 2 or self.chains.get(k) is not None:
             return False
-        self.chains[k] = self._capture_one(lambda: [self._eager_step() for _ in range(k)], self._pool)
+        self.chains[k] = self._capture_one(lambda: self._steps_joined(k), self._pool)
         torch.cuda.synchronize(self.device)
         return True
+
+    def _steps_joined(self, k: int):
+        """``k`` steps, then the comm stream joined (a captured graph must end on its origin stream;
+        inside it, step s's fc SGD overlaps step s+1's forward)."""
+        for _ in range(k):
+            self._eager_step()
+        self._join_comm()
 
     def _capture_one(self, fn, pool):
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, pool=pool, stream=s):
+            # thread_local: the capture forbids unsafe calls on THIS thread only -- the process group's
+            # watchdog thread polls the events of earlier (eager) collectives, and under the default
+            # global mode one such poll invalidates the capture (seen on a 1-rank nccl group)
+            with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
                 fn()
         torch.cuda.current_stream(self.device).wait_stream(s)
         return g
@@ -872,6 +946,7 @@ class FusedCifarEngine:
             for _ in range(n):
                 self.step()
             return
+        self._join_comm()
         for k in sorted(chains, reverse=True):
             while n >= k:
                 chains[k].replay()
@@ -883,11 +958,13 @@ class FusedCifarEngine:
         if not self.graphs:
             self._eager_step()
         elif len(self.graphs) == 1:
+            self._join_comm()
             self.graphs[0].replay()
         elif self._captured_schedule == "serial":
             self._serial_dp_step([g.replay for g in self.graphs])
         else:
             self._dp_step([g.replay for g in self.graphs])
+            self._join_comm()
         self.host_step += 1
 
     def tune_schedule(self, iters: int = 30, steps_per_graph: int = 8, rounds: int = 2, log=None) -> str:

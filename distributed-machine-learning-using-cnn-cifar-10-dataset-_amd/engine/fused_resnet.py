@@ -407,7 +407,10 @@ class FusedResNetEngine:
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            with torch.cuda.graph(g, pool=pool, stream=s):
+            # thread_local: the capture forbids unsafe calls on THIS thread only -- the process group's
+            # watchdog thread polls the events of earlier (eager) collectives, and under the default
+            # global mode one such poll invalidates the capture (seen on a 1-rank nccl group)
+            with torch.cuda.graph(g, pool=pool, stream=s, capture_error_mode="thread_local"):
                 fn()
         torch.cuda.current_stream(self.device).wait_stream(s)
         return g

@@ -46,12 +46,14 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedu
     dist.destroy_process_group()
 
 
-def _dp_reference(world, B, steps, batches, comm_dtype, allreduce, fc_fused=False):
+def _dp_reference(world, B, steps, batches, comm_dtype, allreduce, fc_fused=False, wire_from=0):
     """Replays the data-parallel run on ONE world-1 engine: at every step each rank's gradient on its
     own batch from the shared weights (the DP kernels compute exactly it / world: the loss scale
     1/(B*world) is a power-of-two multiple of 1/B here, which commutes with every rounding), summed in
     rank order like the xGMI kernel (bf16 wire: bf16 inputs, fp32 sum, bf16 result), then the SAME
-    apply-only SGD kernel.  Returns (initial, final) flat parameters."""
+    apply-only SGD kernel.  ``wire_from``: the bf16 wire carries the flat gradient from this offset on
+    (RCCL overlap schedule: the fc bucket only -- its conv bucket crosses as fp32).  Returns
+    (initial, final) flat parameters."""
     from dmlc.engine.fused import FusedCifarEngine
     x, y = _data()
     # the fc kernels the ranks ran (ranks sharing one GPU run the three-launch fc path, not the
@@ -60,7 +62,12 @@ def _dp_reference(world, B, steps, batches, comm_dtype, allreduce, fc_fused=Fals
                            variant={"fc_fused": bool(fc_fused)})
     assert ref.fc_fused == fc_fused
     init = ref.flat_params().clone()
-    bf = (lambda t: t.to(torch.bfloat16).float()) if comm_dtype == "bf16" else (lambda t: t)
+    def bf(t):
+        if comm_dtype != "bf16":
+            return t
+        t = t.clone()
+        t[wire_from:] = t[wire_from:].to(torch.bfloat16).float()
+        return t
     for s in range(steps):
         tot = None
         for r in range(world):
@@ -96,7 +103,11 @@ def test_dp_matches_mean_of_rank_gradients(tmp_path, world, graph, comm_dtype, a
     assert all(r["step"] == steps for r in rs)
     for r in rs[1:]:
         assert torch.equal(rs[0]["flat"], r["flat"])      # replicas identical
-    init, want = _dp_reference(world, B, steps, [r["batches"] for r in rs], comm_dtype, allreduce, rs[0]["fc_fused"])
+    # the RCCL overlap schedule sends its conv bucket as fp32 on any wire (fused.py _allreduce_bucket)
+    from dmlc.models import cifar_cnn as M
+    wire_from = M.FC_BUCKET_OFFSET if (allreduce == "rccl" and schedule == "overlap") else 0
+    init, want = _dp_reference(world, B, steps, [r["batches"] for r in rs], comm_dtype, allreduce, rs[0]["fc_fused"],
+                               wire_from=wire_from)
     d_dp, d_ref = rs[0]["flat"] - init, want - init
     rel = float((d_dp - d_ref).norm() / d_ref.norm())
     tol = 1e-2 if (comm_dtype == "bf16" and allreduce == "rccl") else 1e-5
@@ -105,7 +116,7 @@ def test_dp_matches_mean_of_rank_gradients(tmp_path, world, graph, comm_dtype, a
         assert torch.equal(rs[0]["flat"], want)           # same sums, same order, same kernels
 
 
-def _rank_node(rank, world, port, out, B, steps, lockfile):
+def _rank_node(rank, world, port, out, B, steps, lockfile, schedule="serial", comm_dtype="fp32"):
     """One rank of a node rehearsal: the engine is told it has a GPU of its own (LOCAL_WORLD_SIZE=1),
     so it takes the paths an 8-GPU node runs -- the persistent fc chain with the conv2 dgrad, the
     wgrad launch reducing the conv slabs into the flat gradient, the split forward at B <= 128 --
@@ -122,10 +133,10 @@ def _rank_node(rank, world, port, out, B, steps, lockfile):
                             timeout=datetime.timedelta(seconds=60))
     x, y = _data()
     eng = FusedCifarEngine(B, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
-                           relu_logits=False, comm_dtype="fp32", allreduce="rccl", dp_schedule="serial",
+                           relu_logits=False, comm_dtype=comm_dtype, allreduce="rccl", dp_schedule=schedule,
                            staircase=False)
     flags = {"fc_fused": eng.fc_fused, "fc_dgrad": eng.fc_dgrad, "wgrad_reduce": eng.wgrad_reduce,
-             "fwd12_split": eng.fwd12_split}
+             "fwd12_split": eng.fwd12_split, "grad16": eng.grad16 is not None}
     n = eng.master.numel()
 
     def gpu(fn):
@@ -137,11 +148,19 @@ def _rank_node(rank, world, port, out, B, steps, lockfile):
             finally:
                 fcntl.flock(f, fcntl.LOCK_UN)
 
-    for _ in range(steps):                     # _serial_dp_step, with the GPU turns made explicit
-        gpu(eng._seg_compute_ab)
-        eng.check_barriers()
-        eng._allreduce(eng.grad[:n])
-        gpu(eng._seg_apply)
+    for _ in range(steps):
+        if schedule == "serial":               # _serial_dp_step, with the GPU turns made explicit
+            gpu(eng._seg_compute_ab)
+            eng.check_barriers()
+            eng._allreduce(eng._wire_grad()[:n])
+            gpu(eng._seg_apply)
+        else:                                  # _dp_step: fc bucket after the chain, conv bucket after wgrad
+            gpu(lambda: (eng._seg_forward(), eng._seg_fc()))
+            eng._allreduce_bucket(fc=True)
+            gpu(eng._seg_compute_b)
+            eng.check_barriers()
+            eng._allreduce_bucket(fc=False)
+            gpu(lambda: (eng._seg_apply_fc(), eng._seg_apply_conv()))
         eng.host_step += 1
     torch.save({"flat": eng.flat_params(), "step": eng.global_step(), "flags": flags,
                 "batches": [eng.batch_indices(s) for s in range(steps)]}, os.path.join(out, f"r{rank}.pt"))
@@ -149,28 +168,36 @@ def _rank_node(rank, world, port, out, B, steps, lockfile):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,B", [(2, 32), (2, 160), (4, 64)])
-def test_dp_node_kernels_match_mean_of_rank_gradients(tmp_path, world, B):
+@pytest.mark.parametrize("world,B,schedule,comm_dtype", [(2, 32, "serial", "fp32"), (2, 160, "serial", "fp32"),
+                                                         (4, 64, "serial", "fp32"), (2, 256, "overlap", "fp32"),
+                                                         (4, 64, "overlap", "fp32"), (2, 256, "serial", "bf16"),
+                                                         (2, 64, "overlap", "bf16")])
+def test_dp_node_kernels_match_mean_of_rank_gradients(tmp_path, world, B, schedule, comm_dtype):
     """The data-parallel step with the kernels a node with one GPU per rank runs (fc chain + dgrad,
     reduce-mode wgrad with 1/(B*W) loss scale, split forward) -- which ranks sharing one GPU cannot
     run concurrently -- rehearsed with the ranks taking turns on the card, 6 steps, against the exact
-    replay of the DP semantics on one engine with the same kernels (_dp_reference, fc chain on)."""
+    replay of the DP semantics on one engine with the same kernels (_dp_reference, fc chain on).
+    Both step schedules: serial (one all-reduce, one SGD launch) and overlap (fc bucket after the
+    chain, conv bucket after the wgrad launch, fc / conv SGD launches)."""
     import torch.multiprocessing as mp
     from dmlc.cli import free_port
     steps = 6
-    mp.spawn(_rank_node, args=(world, free_port(), str(tmp_path), B, steps, str(tmp_path / "gpu.lock")),
-             nprocs=world, join=True)
+    mp.spawn(_rank_node, args=(world, free_port(), str(tmp_path), B, steps, str(tmp_path / "gpu.lock"), schedule,
+                               comm_dtype), nprocs=world, join=True)
     rs = [torch.load(tmp_path / f"r{k}.pt", weights_only=True) for k in range(world)]
     f = rs[0]["flags"]
     assert f["fc_fused"] and f["fc_dgrad"] and f["wgrad_reduce"], f
     assert f["fwd12_split"] == (B <= 128), f
+    assert f["grad16"] == (comm_dtype == "bf16"), f      # the bf16 wire: producers write bf16 (grad16)
     assert all(r["step"] == steps for r in rs)
     for r in rs[1:]:
         assert torch.equal(rs[0]["flat"], r["flat"])      # replicas identical
-    init, want = _dp_reference(world, B, steps, [r["batches"] for r in rs], "fp32", "rccl", fc_fused=True)
+    init, want = _dp_reference(world, B, steps, [r["batches"] for r in rs], comm_dtype, "rccl", fc_fused=True)
     d_dp, d_ref = rs[0]["flat"] - init, want - init
     rel = float((d_dp - d_ref).norm() / d_ref.norm())
-    assert rel <= 1e-5, rel
+    # bf16: gloo sums the two bf16 gradients in its own order / precision (the reference: fp32 sum of
+    # the bf16 inputs, rounded once) -- the tolerance of the other gloo bf16 cases
+    assert rel <= (1e-5 if comm_dtype == "fp32" else 1e-2), rel
 
 
 def test_dp_reference_union_batch_consistency():
@@ -373,3 +400,52 @@ def test_xgmi_sgd_epilogue_is_bit_identical(B, comm_dtype):
     if comm_dtype == "fp32":
         assert torch.equal(fused.master, single.master)
         assert torch.equal(fused.fc1n_current(), single.fc1n_current())
+
+
+def _grad16_rank(rank, world, port, out, steps, B):
+    sys.path.insert(0, REPO)
+    import datetime
+    import torch.distributed as dist
+    import dmlc  # noqa: F401
+    from dmlc.engine.fused import FusedCifarEngine
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60), device_id=torch.device("cuda", 0))
+    x, y = _data()
+    res = {}
+    for sched in ("serial", "overlap"):
+        for g16 in (True, False):
+            eng = FusedCifarEngine(B, x, y, device="cuda:0", seed=5, lr=1e-4, relu_logits=False, dp_force=True,
+                                   dp_schedule=sched, allreduce="rccl", comm_dtype="bf16", variant={"grad16": g16})
+            assert (eng.grad16 is not None) == g16, (sched, g16)
+            eng.step()
+            eng.capture(steps_per_graph=4)
+            eng.run(steps - 1)
+            torch.cuda.synchronize()
+            res[(sched, g16)] = {"flat": eng.flat_params(), "step": eng.global_step(),
+                                 "fc1n": eng.fc1n_current().cpu(), "w2f": eng.w2f.cpu()}
+    torch.save({f"{k[0]}-{int(k[1])}": v for k, v in res.items()}, os.path.join(out, "g16.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("B", [256, 64])
+def test_rccl_bf16_wire_grad16_equals_cast_path(tmp_path, B):
+    """Round 6: on the RCCL bf16 wire the fc chain, the wgrad launch's slab reduction and the
+    reduce-only SGD write the flat gradient as bf16 (grad16) and the apply-only SGD reads it -- no
+    cast launches around the all-reduce.  On a 1-rank nccl group (captured RCCL, chained graphs) it
+    must equal the fp32 gradient + t.to(bf16) + all-reduce + copy-back path bit for bit (the same
+    single rounding of every gradient element), and the overlap schedule the serial one."""
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    steps = 9
+    mp.spawn(_grad16_rank, args=(1, free_port(), str(tmp_path), steps, B), nprocs=1, join=True)
+    r = torch.load(tmp_path / "g16.pt", weights_only=True)
+    a, b = r["serial-1"], r["serial-0"]
+    assert a["step"] == b["step"] == r["overlap-1"]["step"] == steps
+    assert torch.isfinite(a["flat"]).all()
+    for k in ("flat", "fc1n", "w2f"):
+        assert torch.equal(a[k], b[k]), k
+        # the overlap schedule's conv bucket crosses as bf16 too when grad16 holds it (without grad16
+        # it goes fp32, fused.py _allreduce_bucket): the same weights as the serial step
+        assert torch.equal(r["overlap-1"][k], a[k]), k
