@@ -712,11 +712,13 @@ class FusedCifarEngine:
         self._seg_compute_b_launch()
 
     def _seg_compute_b_launch(self):
-        """conv backward + the slab reduction as its own SGD launch (when the in-launch reduction is
-        off: ranks sharing a GPU, DMLC_WGRAD_SGD=0).  The overlap schedule's wgrad launch runs beside
-        the comm stream's fc all-reduce: its sub-grid barriers stay deadlock-free there because the
-        collective never waits on a kernel of this GPU -- a wgrad block that is not yet resident gets
-        its CU once the collective finishes -- and every wait is bounded (error word, never a hang)."""
+        """conv backward + the slab reduction as its own SGD launch.  The overlap schedule always uses
+        it: its wgrad launch runs beside the comm stream's collective, and sub-grid barriers there
+        could close a cycle across GPUs -- a collective partly resident on each of two GPUs, each
+        GPU's missing collective blocks waiting for CUs held by wgrad blocks that spin for their own
+        missing blocks, which wait for the CUs of the resident collective blocks, which wait on the
+        other GPU.  The bounded spin would turn that into a timeout (a wrong step), so no in-launch
+        barrier ever runs beside a collective."""
         self._conv_backward()
         self._sgd(mode=1 if self.dp else 0)
 
@@ -798,7 +800,7 @@ class FusedCifarEngine:
         if self.dp_schedule == "serial":
             self._serial_dp_step([self._seg_compute_ab, self._seg_apply])
             return
-        self._dp_step([self._seg_forward, self._seg_fc, self._seg_compute_b, self._seg_apply_fc,
+        self._dp_step([self._seg_forward, self._seg_fc, self._seg_compute_b_launch, self._seg_apply_fc,
                        self._seg_apply_conv])
 
     def _seg_compute_ab(self):
@@ -822,7 +824,7 @@ class FusedCifarEngine:
 
     def _dp_step(self, seg):
         """Data-parallel step around two all-reduce buckets, two streams:
-            main: fwd | [join s-1] fc chain | wgrad (+ conv slab reduction) |        [wait] conv SGD (+ finalize)
+            main: fwd | [join s-1] fc chain | wgrad, slab-reduction launch |     [wait] conv SGD (+ finalize)
             comm:                  [wait] all-reduce fc | [wait] all-reduce conv -> fc SGD
         Both collectives go through ONE stream in one order (one communicator, the same issue order on
         every rank).  The fc bucket (90 % of the bytes) crosses the links while the wgrad launch runs;
@@ -886,7 +888,8 @@ class FusedCifarEngine:
         elif self.dp_schedule == "serial":
             segs = [self._seg_compute_ab, self._seg_apply]
         else:
-            segs = [self._seg_forward, self._seg_fc, self._seg_compute_b, self._seg_apply_fc, self._seg_apply_conv]
+            segs = [self._seg_forward, self._seg_fc, self._seg_compute_b_launch, self._seg_apply_fc,
+                    self._seg_apply_conv]
         self._captured_schedule = self.dp_schedule
         # a capture records launches without running them: the step counter and weights are
         # identical before and after
@@ -995,10 +998,22 @@ class FusedCifarEngine:
             torch.cuda.synchronize(self.device)
             t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=bdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
+            # a persistent launch's bounded wait timed out on some rank: that schedule is out (the
+            # sticky word is cleared for the run that follows; every rank sees the same MAX)
+            e = torch.tensor([int(self.wbar[10 * 32].item()) if self.barriers_in_use else 0],
+                             dtype=torch.float64, device=bdev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.pg)
+            if float(e.item()) != 0.0:
+                if log:
+                    log(f"dp schedule {sched}: a persistent launch's wait timed out -- not eligible")
+                self.wbar[10 * 32].zero_()
+                times[sched].append(math.inf)
+                continue
             times[sched].append(float(t.item()) / iters)
         best_t = {k: min(v) for k, v in times.items()}
         best = min(best_t, key=best_t.get)
-        self.comm_info.update(schedule=best, schedule_us={k: round(v * 1e6, 1) for k, v in best_t.items()})
+        self.comm_info.update(schedule=best, schedule_us={k: round(v * 1e6, 1) for k, v in best_t.items()
+                                                          if v != math.inf})
         if log:
             log(f"dp schedule: {best} ({self.comm_info['schedule_us']})")
         if best != self.dp_schedule:

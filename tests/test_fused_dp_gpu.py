@@ -157,8 +157,7 @@ def _rank_node(rank, world, port, out, B, steps, lockfile, schedule="serial", co
         else:                                  # _dp_step: fc bucket after the chain, conv bucket after wgrad
             gpu(lambda: (eng._seg_forward(), eng._seg_fc()))
             eng._allreduce_bucket(fc=True)
-            gpu(eng._seg_compute_b)
-            eng.check_barriers()
+            gpu(eng._seg_compute_b_launch)
             eng._allreduce_bucket(fc=False)
             gpu(lambda: (eng._seg_apply_fc(), eng._seg_apply_conv()))
         eng.host_step += 1
