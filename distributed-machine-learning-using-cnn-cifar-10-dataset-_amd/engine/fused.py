@@ -1003,6 +1003,8 @@ class FusedCifarEngine:
             e = torch.tensor([int(self.wbar[10 * 32].item()) if self.barriers_in_use else 0],
                              dtype=torch.float64, device=bdev)
             dist.all_reduce(e, op=dist.ReduceOp.MAX, group=self.pg)
+            if self.xgmi is not None:
+                self.xgmi.check()      # a timed-out exchange leaves no consistent epoch to resume from
             if float(e.item()) != 0.0:
                 if log:
                     log(f"dp schedule {sched}: a persistent launch's wait timed out -- not eligible")
