@@ -20,7 +20,7 @@ def _data():
     return x, y
 
 
-def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedule="overlap"):
+def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedule="overlap", variant=None):
     sys.path.insert(0, REPO)
     import torch.distributed as dist
     import dmlc  # noqa: F401
@@ -31,8 +31,10 @@ def _rank(rank, world, port, out, B, steps, graph, comm_dtype, allreduce, schedu
     x, y = _data()
     eng = FusedCifarEngine(B, x, y, device="cuda:0", world_size=world, rank=rank, seed=5, lr=1e-4,
                            relu_logits=False, comm_dtype=comm_dtype, allreduce=allreduce,
-                           dp_schedule=schedule, staircase=False)
+                           dp_schedule=schedule, staircase=False, variant=variant)
     assert eng.comm_info["allreduce"] == ("xgmi" if allreduce == "xgmi" else "rccl"), eng.comm_info
+    if variant and variant.get("comm_sgd"):
+        assert eng.comm_sgd
     if allreduce == "xgmi":
         assert eng.comm_info["wire"] == comm_dtype, eng.comm_info      # bf16 no longer forces RCCL
     eng.step()
@@ -114,6 +116,30 @@ def test_dp_matches_mean_of_rank_gradients(tmp_path, world, graph, comm_dtype, a
     assert rel <= tol, rel
     if allreduce == "xgmi" and world == 2:
         assert torch.equal(rs[0]["flat"], want)           # same sums, same order, same kernels
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("comm_dtype", ["fp32", "bf16"])
+def test_xgmi_sgd_epilogue_w2_equals_exchange_plus_sgd_launch(tmp_path, comm_dtype):
+    """the exchange kernel with the SGD in its epilogue (variant comm_sgd) at W = 2 -- the
+    per-peer barriers of its workgroups, the SGD reading the peer-pushed sums after the exchange --
+    against the exchange + SGD launch, bit for bit (the ranks share the test box's GPU; the exchange
+    kernel's workgroups are split between them)."""
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    B, steps = 32, 8
+    res = {}
+    for v in (True, False):
+        d = tmp_path / f"v{int(v)}"
+        d.mkdir()
+        mp.spawn(_rank, args=(2, free_port(), str(d), B, steps, True, comm_dtype, "xgmi", "serial",
+                              {"comm_sgd": v}), nprocs=2, join=True)
+        res[v] = [torch.load(d / f"r{k}.pt", weights_only=True) for k in range(2)]
+    for v in res:
+        assert res[v][0]["step"] == res[v][1]["step"] == steps
+        assert torch.equal(res[v][0]["flat"], res[v][1]["flat"])
+    assert torch.isfinite(res[True][0]["flat"]).all()
+    assert torch.equal(res[True][0]["flat"], res[False][0]["flat"])
 
 
 def _rank_node(rank, world, port, out, B, steps, lockfile, schedule="serial", comm_dtype="fp32"):
