@@ -436,7 +436,8 @@ class FusedCifarEngine:
         self._captured_schedule = None
         if self.dp:
             self.comm_info.update(schedule=dp_schedule, backend=self._backend(),
-                                  captured_comm=bool(self.capture_comm or self.xgmi is not None))
+                                  captured_comm=bool(self.capture_comm or self.xgmi is not None),
+                                  grad_dtype="bf16" if self.grad16 is not None else "fp32")
         self.host_step = 0
         self._sync_bidx()
         self.refresh_shadows()
