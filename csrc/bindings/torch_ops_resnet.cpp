@@ -29,14 +29,10 @@ Geom geom(int64_t cin, int64_t cout, int64_t hin, int64_t stride) {
   TORCH_CHECK(false, "rn: unsupported conv geometry cin=", cin, " cout=", cout, " hin=", hin, " stride=", stride);
 }
 
-// per-layer statistics accumulators: fp64 [NSLOT][2][64] (sum, sum of squares / R1, R2)
-void check_stat(const Tensor& t, const char* n) { check_numel(t, n, at::kDouble, DMLC_RN_NSLOT * 128); }
-// deterministic-mode side buffer of one statistic: [B][128] fp32 partials + the group tickets
-float* det_ptr(const c10::optional<Tensor>& det, int64_t B) {
-  if (!det.has_value()) return nullptr;
-  check_numel(*det, "det", at::kFloat, B * 128 + DMLC_RN_DET_TICKETS);
-  return det->data_ptr<float>();
-}
+// per-layer statistics accumulators: fixed-point int64 [NSLOT][256] (integer parts of sum / sum of
+// squares or R1 / R2 at [0, 128), their 48-bit fractions at [128, 256); resnet.hip fx_add)
+void check_stat(const Tensor& t, const char* n) { check_numel(t, n, at::kLong, DMLC_RN_NSLOT * 256); }
+#define STAT_PTR(t) reinterpret_cast<long long*>((t).data_ptr<int64_t>())
 
 // nvalid: the first nvalid images are real, the rest batch padding (0: all B); every BatchNorm mean is
 // over the real images only
@@ -51,7 +47,7 @@ void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::o
             int64_t cx, const c10::optional<Tensor>& z_prev, const c10::optional<Tensor>& stat_prev,
             const c10::optional<Tensor>& gamma_prev, const c10::optional<Tensor>& beta_prev,
             const c10::optional<Tensor>& sc_src, int64_t sc_mode, const c10::optional<Tensor>& a_out, const Tensor& w,
-            const Tensor& z, const Tensor& stat, const c10::optional<Tensor>& stat_det, int64_t nvalid) {
+            const Tensor& z, const Tensor& stat, int64_t nvalid) {
   const Geom g = geom(cin, cout, hin, stride);
   const int64_t B = z.size(0), nv = valid_count(nvalid, B);
   check(w, "w", at::kBFloat16, {g.cout, g.kp()});
@@ -82,13 +78,12 @@ void rn_fwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10::o
       TORCH_CHECK(sc_src.has_value(), "sc_mode 2 needs sc_src");
       check(*sc_src, "sc_src", at::kBFloat16, {B, 2 * hin, 2 * hin, cin / 2});
     }
-    a.z_prev = z_prev->data_ptr(); a.stat_prev = stat_prev->data_ptr<double>();
+    a.z_prev = z_prev->data_ptr(); a.stat_prev = STAT_PTR(*stat_prev);
     a.gamma_prev = gamma_prev->data_ptr<float>(); a.beta_prev = beta_prev->data_ptr<float>();
     a.sc_src = sc_mode ? sc_src->data_ptr() : nullptr; a.sc_mode = (int)sc_mode;
     a.a_out = a_out->data_ptr(); a.inv_n_prev = 1.f / (float)(nv * hin * hin);
   }
-  a.w = w.data_ptr(); a.z = z.data_ptr(); a.stat = stat.data_ptr<double>();
-  a.stat_det = det_ptr(stat_det, B);
+  a.w = w.data_ptr(); a.z = z.data_ptr(); a.stat = STAT_PTR(stat);
   c10::DeviceGuard guard(z.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_fwd(&gc, &a, stream_of(z)));
@@ -98,7 +93,7 @@ DmlcRnDgradArgs dgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
                            const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd,
                            const Tensor& a_prev, const Tensor& z_prev, const Tensor& stat_prev,
                            const c10::optional<Tensor>& gy_sc, int64_t sc_mode, const Tensor& gy_prev,
-                           const Tensor& red_prev, const c10::optional<Tensor>& red_det, int64_t nvalid) {
+                           const Tensor& red_prev, int64_t nvalid) {
   TORCH_CHECK(cin >= 16, "rn_dgrad: the stem has no input gradient");
   const int64_t B = gy.size(0), ho = g.hout(), nv = valid_count(nvalid, B);
   check(gy, "gy", at::kBFloat16, {B, ho, ho, cout});
@@ -118,25 +113,24 @@ DmlcRnDgradArgs dgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
     check(*gy_sc, "gy_sc", at::kBFloat16, {B, hin / 2, hin / 2, 2 * cin});
   }
   DmlcRnDgradArgs a{};
-  a.gy = gy.data_ptr(); a.z = z.data_ptr(); a.stat = stat.data_ptr<double>(); a.red = red.data_ptr<double>();
+  a.gy = gy.data_ptr(); a.z = z.data_ptr(); a.stat = STAT_PTR(stat); a.red = STAT_PTR(red);
   a.gamma = gamma.data_ptr<float>(); a.inv_n = 1.f / (float)(nv * ho * ho);
   a.wd = wd.data_ptr();
-  a.a_prev = a_prev.data_ptr(); a.z_prev = z_prev.data_ptr(); a.stat_prev = stat_prev.data_ptr<double>();
+  a.a_prev = a_prev.data_ptr(); a.z_prev = z_prev.data_ptr(); a.stat_prev = STAT_PTR(stat_prev);
   a.inv_n_prev = 1.f / (float)(nv * hin * hin);
   a.nvalid = (int)nv;
   a.gy_sc = sc_mode ? gy_sc->data_ptr() : nullptr; a.sc_mode = (int)sc_mode;
-  a.gy_prev = gy_prev.data_ptr(); a.red_prev = red_prev.data_ptr<double>(); a.B = (int)B;
-  a.red_det = det_ptr(red_det, B);
+  a.gy_prev = gy_prev.data_ptr(); a.red_prev = STAT_PTR(red_prev); a.B = (int)B;
   return a;
 }
 
 void rn_dgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
               const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
               const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
-              const Tensor& gy_prev, const Tensor& red_prev, const c10::optional<Tensor>& red_det, int64_t nvalid) {
+              const Tensor& gy_prev, const Tensor& red_prev, int64_t nvalid) {
   const Geom g = geom(cin, cout, hin, stride);
   const DmlcRnDgradArgs a = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
-                                       gy_sc, sc_mode, gy_prev, red_prev, red_det, nvalid);
+                                       gy_sc, sc_mode, gy_prev, red_prev, nvalid);
   c10::DeviceGuard guard(gy.device());
   const DmlcRnLayerGeom gc = g.c();
   CHECK_HIP(dmlc_rn_dgrad(&gc, &a, stream_of(gy)));
@@ -167,7 +161,7 @@ DmlcRnWgradArgs wgrad_args(const Geom& g, int64_t cin, int64_t cout, int64_t hin
     check(*x, "x", at::kBFloat16, {B, hin, hin, cin});
     a.x = x->data_ptr();
   }
-  a.gy = gy.data_ptr(); a.z = z.data_ptr(); a.stat = stat.data_ptr<double>(); a.red = red.data_ptr<double>();
+  a.gy = gy.data_ptr(); a.z = z.data_ptr(); a.stat = STAT_PTR(stat); a.red = STAT_PTR(red);
   a.gamma = gamma.data_ptr<float>(); a.inv_n = 1.f / (float)(nv * ho * ho);
   a.part = part.data_ptr<float>(); a.G = (int)G; a.B = (int)B; a.nvalid = (int)nv;
   return a;
@@ -189,11 +183,11 @@ void rn_wgrad(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const c10:
 void rn_bwd(int64_t cin, int64_t cout, int64_t hin, int64_t stride, const Tensor& gy, const Tensor& z,
             const Tensor& stat, const Tensor& red, const Tensor& gamma, const Tensor& wd, const Tensor& a_prev,
             const Tensor& z_prev, const Tensor& stat_prev, const c10::optional<Tensor>& gy_sc, int64_t sc_mode,
-            const Tensor& gy_prev, const Tensor& red_prev, const Tensor& part, const c10::optional<Tensor>& red_det,
-            int64_t nvalid, bool per_image) {
+            const Tensor& gy_prev, const Tensor& red_prev, const Tensor& part, int64_t nvalid,
+            bool per_image) {
   const Geom g = geom(cin, cout, hin, stride);
   const DmlcRnDgradArgs d = dgrad_args(g, cin, cout, hin, gy, z, stat, red, gamma, wd, a_prev, z_prev, stat_prev,
-                                       gy_sc, sc_mode, gy_prev, red_prev, red_det, nvalid);
+                                       gy_sc, sc_mode, gy_prev, red_prev, nvalid);
   const DmlcRnWgradArgs w = wgrad_args(g, cin, cout, hin, c10::nullopt, c10::nullopt, c10::nullopt, 1, 0, 0, a_prev, gy,
                                        z, stat, red, gamma, part, nvalid);
   TORCH_CHECK(!per_image || (((cin == 16 && hin == 32) || (cin == 32 && hin == 16)) && cout == cin && stride == 1 &&
@@ -209,7 +203,7 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
              const Tensor& fcw, const Tensor& fcb, const Tensor& labels, const Tensor& idx,
              const c10::optional<Tensor>& counter, int64_t period, double inv_batch, const Tensor& gy,
              const Tensor& red, const Tensor& fc_part, const Tensor& loss_img, const Tensor& correct_img,
-             const c10::optional<Tensor>& logits, const c10::optional<Tensor>& red_det, int64_t nvalid,
+             const c10::optional<Tensor>& logits, int64_t nvalid,
              const c10::optional<Tensor>& step, const c10::optional<Tensor>& step_copy) {
   const int64_t B = z.size(0), nv = valid_count(nvalid, B);
   check(z, "z", at::kBFloat16, {B, 8, 8, 64});
@@ -226,14 +220,13 @@ void rn_head(const Tensor& z, const Tensor& stat, const Tensor& gamma, const Ten
   check_numel(loss_img, "loss_img", at::kFloat, B);
   check_numel(correct_img, "correct_img", at::kInt, B);
   DmlcRnHeadArgs a{};
-  a.z = z.data_ptr(); a.stat = stat.data_ptr<double>(); a.gamma = gamma.data_ptr<float>();
+  a.z = z.data_ptr(); a.stat = STAT_PTR(stat); a.gamma = gamma.data_ptr<float>();
   a.beta = beta.data_ptr<float>(); a.inv_n = 1.f / (float)(nv * 64);
   a.sc = sc.data_ptr(); a.fcw = fcw.data_ptr<float>(); a.fcb = fcb.data_ptr<float>();
   a.labels = labels.data_ptr<int>(); a.src = index_src(idx, counter, period, B);
   check_order_fits(a.src, labels.size(0));
   a.inv_batch = (float)inv_batch;
-  a.gy = gy.data_ptr(); a.red = red.data_ptr<double>(); a.fc_part = fc_part.data_ptr<float>();
-  a.red_det = det_ptr(red_det, B);
+  a.gy = gy.data_ptr(); a.red = STAT_PTR(red); a.fc_part = fc_part.data_ptr<float>();
   a.loss_img = loss_img.data_ptr<float>(); a.correct_img = correct_img.data_ptr<int>();
   a.logits_out = nullptr;
   if (logits.has_value()) {
@@ -277,8 +270,8 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
   dev(master, "master"); dev(state, "state");
   TORCH_CHECK(master.scalar_type() == at::kFloat && state.scalar_type() == at::kFloat, "master/state must be fp32");
   const int64_t np = master.numel(), ns = state.numel();
-  check(stat, "stat", at::kDouble, {L, DMLC_RN_NSLOT, 128});
-  check(red, "red", at::kDouble, {L, DMLC_RN_NSLOT, 128});
+  check(stat, "stat", at::kLong, {L, DMLC_RN_NSLOT, 256});
+  check(red, "red", at::kLong, {L, DMLC_RN_NSLOT, 256});
   check(fc_part, "fc_part", at::kFloat, {B, 656});
   check_numel(correct_img, "correct_img", at::kInt, B);
   check_numel(loss_img, "loss_img", at::kFloat, B);
@@ -317,7 +310,7 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
     }
     a.inv_n[l] = 1.f / (float)(nv * g.hout() * g.hout());
   }
-  a.stat = stat.data_ptr<double>(); a.red = red.data_ptr<double>();
+  a.stat = STAT_PTR(stat); a.red = STAT_PTR(red);
   a.state = state.data_ptr<float>(); a.bn_momentum = (float)bn_momentum;
   a.fcw_off = (int)fcw_off; a.fcb_off = (int)fcb_off; a.fc_part = fc_part.data_ptr<float>(); a.B = (int)B;
   a.mode = (int)mode;
@@ -344,22 +337,22 @@ void rn_sgd(const Tensor& master, const c10::optional<Tensor>& grad, double grad
 TORCH_LIBRARY_FRAGMENT(dmlc, m) {
   m.def("rn_fwd(int cin, int cout, int hin, int stride, Tensor? data, Tensor? idx, Tensor? counter, int period, "
         "int cy, int cx, Tensor? z_prev, Tensor? stat_prev, Tensor? gamma_prev, Tensor? beta_prev, Tensor? sc_src, "
-        "int sc_mode, Tensor(a!)? a_out, Tensor w, Tensor(b!) z, Tensor(c!) stat, Tensor(d!)? stat_det=None, "
+        "int sc_mode, Tensor(a!)? a_out, Tensor w, Tensor(b!) z, Tensor(c!) stat, "
         "int nvalid=0) -> ()");
   m.def("rn_dgrad(int cin, int cout, int hin, int stride, Tensor gy, Tensor z, Tensor stat, Tensor red, "
         "Tensor gamma, Tensor wd, Tensor a_prev, Tensor z_prev, Tensor stat_prev, Tensor? gy_sc, int sc_mode, "
-        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!)? red_det=None, int nvalid=0) -> ()");
+        "Tensor(a!) gy_prev, Tensor(b!) red_prev, int nvalid=0) -> ()");
   m.def("rn_wgrad(int cin, int cout, int hin, int stride, Tensor? data, Tensor? idx, Tensor? counter, int period, "
         "int cy, int cx, Tensor? x, Tensor gy, Tensor z, Tensor stat, Tensor red, Tensor gamma, "
         "Tensor(a!) part, int nvalid=0) -> ()");
   m.def("rn_bwd(int cin, int cout, int hin, int stride, Tensor gy, Tensor z, Tensor stat, Tensor red, "
         "Tensor gamma, Tensor wd, Tensor a_prev, Tensor z_prev, Tensor stat_prev, Tensor? gy_sc, int sc_mode, "
-        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part, Tensor(d!)? red_det=None, int nvalid=0, "
+        "Tensor(a!) gy_prev, Tensor(b!) red_prev, Tensor(c!) part, int nvalid=0, "
         "bool per_image=False) -> ()");
   m.def("rn_head(Tensor z, Tensor stat, Tensor gamma, Tensor beta, Tensor sc, Tensor fcw, Tensor fcb, "
         "Tensor labels, Tensor idx, Tensor? counter, int period, float inv_batch, Tensor(a!) gy, Tensor(b!) red, "
         "Tensor(c!) fc_part, Tensor(d!) loss_img, Tensor(e!) correct_img, Tensor(f!)? logits, "
-        "Tensor(g!)? red_det=None, int nvalid=0, Tensor? step=None, Tensor(h!)? step_copy=None) -> ()");
+        "int nvalid=0, Tensor? step=None, Tensor(h!)? step_copy=None) -> ()");
   m.def("rn_sgd(Tensor(a!) master, Tensor(b!)? grad, float grad_scale, Tensor(c!) state, int[] conv_off, "
         "int[] gamma_off, int[] beta_off, int[] mm_off, int[] mv_off, int fcw_off, int fcb_off, Tensor[] part, "
         "Tensor(d!)[] wf, Tensor(e!)[] wd, Tensor stat, Tensor red, Tensor fc_part, Tensor loss_img, "

@@ -1,10 +1,9 @@
 // Host-side launch API of the fused ResNet-20 kernels (csrc/kernels/resnet.hip).
 //
-// Conventions: activations NHWC bf16; per-layer BatchNorm statistics live in NSLOT fp64 slots per
-// layer (slot = producing block & 7).  Deterministic mode (`det` side buffer set): every producing
-// block stores its fp32 partials, and the last block of each slot's group (per-group ticket) sums the
-// group's partials in block order into the slot -- bitwise reproducible, no zeroing.  Otherwise: fp64
-// atomicAdd into the slot (zeroed once per step).  Conv weights have two bf16 shadows:
+// Conventions: activations NHWC bf16; per-layer BatchNorm statistics live in NSLOT fixed-point slots
+// per layer (slot = producing block & 7; int64 [NSLOT][hi 128 | lo 128], integer part + 48-bit
+// fraction added with 64-bit integer atomics -- order independent, so bitwise reproducible; zeroed
+// once per step by the engine).  Conv weights have two bf16 shadows:
 //   fwd   w [COUT][KP]  k  = tap*CINP + ci        (tap = kh*3 + kw, CINP = max(CIN, 8), KP = 9*CINP -> x32)
 //   dgrad wd [CIN][KPD] k' = tap'*COUT + co       (tap' = 8 - tap: rotated 180 degrees, KPD = 9*COUT -> x32)
 // Layer l computes z_l = conv_l(x_l) with x_l = a_{l-1}, a = relu(bn(z) [+ shortcut]).
@@ -25,7 +24,7 @@ struct DmlcRnFwdArgs {
   // input of this conv: the dataset (stem) or the BN-apply of the previous layer
   const uint8_t* data; DmlcIndexSrc src; int cy, cx;      // stem only
   const void* z_prev;        // bf16 [B][Hin][Hin][CIN]  pre-BN output of layer l-1
-  const double* stat_prev;   // [NSLOT][2][64] sum z, sum z^2 of layer l-1
+  const long long* stat_prev;   // [NSLOT][256] fixed-point sum z, sum z^2 of layer l-1
   const float* gamma_prev; const float* beta_prev;
   const void* sc_src;        // nullable: block input feeding the residual of layer l-1 (bf16)
   int sc_mode;               // 0 none, 1 identity [B][Hin][Hin][CIN], 2 subsample+zero-pad [B][2Hin][2Hin][CIN/2]
@@ -33,23 +32,21 @@ struct DmlcRnFwdArgs {
   float inv_n_prev;          // 1 / (B * Hin * Hin)
   const void* w;             // bf16 [COUT][KP]
   void* z;                   // bf16 [B][Hout][Hout][COUT]
-  double* stat;              // [NSLOT][2][64] accumulators of layer l
-  float* stat_det;           // nullable: deterministic side buffer [B][128] fp32 partials + 8x32 tickets
+  long long* stat;           // [NSLOT][256] fixed-point accumulators of layer l
   int B;
   int nvalid;                // images b >= nvalid are batch padding: no contribution to the statistics
 };
 
 struct DmlcRnDgradArgs {
   // BN backward of layer l (prologue): g_z = gamma*rstd*(g_y - R1/N - xhat*R2/N)
-  const void* gy; const void* z; const double* stat; const double* red; const float* gamma; float inv_n;
+  const void* gy; const void* z; const long long* stat; const long long* red; const float* gamma; float inv_n;
   const void* wd;            // bf16 [CIN][KPD]
   // epilogue: g_a_{l-1} (+ shortcut) -> g_y_{l-1} = g_a * (a_{l-1} > 0), reductions of layer l-1
-  const void* a_prev; const void* z_prev; const double* stat_prev; float inv_n_prev;
+  const void* a_prev; const void* z_prev; const long long* stat_prev; float inv_n_prev;
   const void* gy_sc;         // nullable: g_y of the block's second conv (shortcut gradient)
   int sc_mode;               // 1 identity, 2 subsample (gy_sc is [B][Hin/2][Hin/2][2*CIN])
   void* gy_prev;             // bf16 [B][Hin][Hin][CIN]
-  double* red_prev;          // [NSLOT][2][64]
-  float* red_det;            // nullable: deterministic side buffer of red_prev (see stat_det)
+  long long* red_prev;       // [NSLOT][256]
   int B;
   int nvalid;                // padding images (b >= nvalid) get g_z = 0 (their g_y is 0 already)
 };
@@ -57,20 +54,19 @@ struct DmlcRnDgradArgs {
 struct DmlcRnWgradArgs {
   const uint8_t* data; DmlcIndexSrc src; int cy, cx;      // stem input
   const void* x;             // bf16 a_{l-1} [B][Hin][Hin][CIN] (l >= 1)
-  const void* gy; const void* z; const double* stat; const double* red; const float* gamma; float inv_n;
+  const void* gy; const void* z; const long long* stat; const long long* red; const float* gamma; float inv_n;
   float* part;               // [G][KP][COUT] fp32 split-K slabs
   int G, B;
   int nvalid;                // padding images contribute nothing (g_z = 0)
 };
 
 struct DmlcRnHeadArgs {
-  const void* z; const double* stat; const float* gamma; const float* beta; float inv_n;   // layer 18
+  const void* z; const long long* stat; const float* gamma; const float* beta; float inv_n;   // layer 18
   const void* sc;            // identity shortcut (block input) bf16 [B][8][8][64]
   const float* fcw; const float* fcb;   // fp32 master views [64][10], [10]
   const int* labels; DmlcIndexSrc src; float inv_batch;
   void* gy;                  // bf16 [B][8][8][64] g_y_18
-  double* red;               // [NSLOT][2][64] reductions of layer 18
-  float* red_det;            // nullable: deterministic side buffer of red
+  long long* red;            // [NSLOT][256] reductions of layer 18
   float* fc_part;            // [B][656] per-image dW_fc (640) + db_fc (10) + pad
   float* loss_img; int* correct_img;    // [B]
   float* logits_out;         // nullable [B][10]
@@ -80,8 +76,7 @@ struct DmlcRnHeadArgs {
 };
 
 #define DMLC_RN_LAYERS 19
-#define DMLC_RN_NSLOT 8      // fp64 statistics accumulators per layer: [NSLOT][2][64] (slot = block & 7)
-#define DMLC_RN_DET_TICKETS (8 * 32)   // uints after the [nblk][128] partials of a det side buffer
+#define DMLC_RN_NSLOT 8      // fixed-point statistics slots per layer: [NSLOT][256] int64 (slot = block & 7)
 struct DmlcRnSgdArgs {
   float* master; int nparams;
   float* grad; float grad_scale;   // DP: modes 1 (write) / 2 (read, scaled)
@@ -90,7 +85,7 @@ struct DmlcRnSgdArgs {
   int cin[DMLC_RN_LAYERS], cout[DMLC_RN_LAYERS];
   const float* part[DMLC_RN_LAYERS]; int G[DMLC_RN_LAYERS];
   void* wf[DMLC_RN_LAYERS]; void* wd[DMLC_RN_LAYERS];
-  const double* stat; const double* red;   // [19][NSLOT][2][64] each
+  const long long* stat; const long long* red;   // [19][NSLOT][256] each
   float* state; int mm_off[DMLC_RN_LAYERS], mv_off[DMLC_RN_LAYERS];   // BN moving statistics
   float bn_momentum; float inv_n[DMLC_RN_LAYERS];
   int fcw_off, fcb_off; const float* fc_part; int B;

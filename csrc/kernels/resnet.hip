@@ -12,9 +12,13 @@
 //     the backward); the backward mirrors it: each dgrad's epilogue produces g_y of the layer below
 //     plus its two BN reductions (sum g_y, sum g_y*xhat), and the consumer rebuilds
 //     g_z = gamma*rstd*(g_y - R1/N - xhat*R2/N) in its prologue;
-//   * the fp64 accumulators are spread over NSLOT copies (slot = blockIdx & 7, i.e. one per XCD under
-//     round-robin dispatch) so 256 blocks do not serialise on 64 addresses; consumers fold the slots
-//     once per block (64 threads) into LDS coefficient tables;
+//   * the statistics are exact fixed-point sums: every block splits each fp32 channel partial into an
+//     integer part and a 48-bit fraction and adds both with 64-bit integer atomics into one of NSLOT
+//     copies (slot = blockIdx & 7, i.e. one per XCD under round-robin dispatch) so 256 blocks do not
+//     serialise on 64 addresses; integer addition is associative, so the totals -- and everything
+//     downstream -- are bitwise reproducible (graph replay == eager launches) at the cost of fp64
+//     atomics (r6: the ticketed per-slot-group flush this replaces cost 54 us per step); consumers fold
+//     the slots once per block (64 threads) into LDS coefficient tables;
 //   * stride-2 dgrad is a stride-1 correlation over a zero-inserted LDS image (pad 2/0);
 //   * weight gradients: split-K over image groups x m-chunks, several images staged per barrier, both
 //     operands read with ds_read_b64_tr_b16 from NHWC LDS images (per-lane row addresses absorb stride
@@ -46,28 +50,70 @@ DEV void st_rn8(void* base, uint32_t off, const bf16x4& v) {
 DEV void st_rn16(void* base, uint32_t off, const uint4& v) { st_out16(base, off, v); }
 DEV void st_rn8(void* base, uint32_t off, const bf16x4& v) { st_out8(base, off, __builtin_bit_cast(uint2, v)); }
 #endif
-constexpr int NSLOT = DMLC_RN_NSLOT;          // fp64 statistics copies per layer: [NSLOT][2][64]
+constexpr int NSLOT = DMLC_RN_NSLOT;          // statistics copies per layer: [NSLOT][hi 128 | lo 128] int64
 constexpr double BN_EPS = 1e-3;
-
-#ifdef RN_EXP_NOATOM   // experiment: drop the BN-statistics atomics (timing only; numerics are wrong)
-#define RN_ATOMIC_ADD(p, v) ((void)(p), (void)(v))
-#else
-#define RN_ATOMIC_ADD(p, v) atomicAdd(p, v)
-#endif
 
 __host__ __device__ constexpr int round32(int x) { return (x + 31) / 32 * 32; }
 
-// channel c of a slotted accumulator: (sum, sum of squares) or (R1, R2)
-DEV void slot_sums(const double* st, int c, double& s1, double& s2) {
-  double a[NSLOT], b[NSLOT];
-#pragma unroll
-  for (int k = 0; k < NSLOT; ++k) { a[k] = st[k * 128 + c]; b[k] = st[k * 128 + 64 + c]; }
-  s1 = 0.0; s2 = 0.0;
-#pragma unroll
-  for (int k = 0; k < NSLOT; ++k) { s1 += a[k]; s2 += b[k]; }
+// Fixed-point BN statistics.  A slot holds, per statistic e (0..63 sum / R1, 64..127 sum of squares /
+// R2), an int64 integer part at [e] and a uint64 fraction in units of 2^-48 at [128 + e].  One add
+// splits x = floor(x) + f exactly (|x| < 2^50, so x - floor(x) and f * 2^48 are exact in fp64) and
+// rounds f * 2^48 to an integer (error <= 2^-49 per add, far below the fp32 partial's own rounding).
+// A non-finite or absurd partial adds the poison 2^56 to the integer part; legitimate slot totals stay
+// below 2^55 in magnitude (<= 32 adds of < 2^50 each at B = 256), so the decoder turns any slot at or
+// beyond 2^55 into NaN -- a diverged step still shows up as NaN downstream.
+constexpr double FX_ONE = 281474976710656.0;             // 2^48
+constexpr double FX_LIM = 1125899906842624.0;            // 2^50
+constexpr long long FX_POISON = 1LL << 56;
+constexpr long long FX_BAD = 1LL << 55;
+
+DEV void fx_add(long long* slot, int e, float v) {
+  const double x = (double)v;
+  long long hi;
+  unsigned long long lo;
+  if (__builtin_fabs(x) < FX_LIM) {
+    const double f = __builtin_floor(x);
+    hi = (long long)f;
+    lo = (unsigned long long)__builtin_rint((x - f) * FX_ONE);   // in [0, 2^48]
+  } else {
+    hi = FX_POISON;
+    lo = 0;
+  }
+  atomicAdd(reinterpret_cast<unsigned long long*>(slot + e), (unsigned long long)hi);
+  atomicAdd(reinterpret_cast<unsigned long long*>(slot + 128 + e), lo);
 }
 
-DEV void bn_mean_rstd(const double* stat, int c, float inv_n, float& mean, float& rstd) {
+// total of statistic e over the NSLOT copies of one layer's slotted accumulator (all loads first)
+DEV double fx_total(const long long* st, int e) {
+  long long h[NSLOT];
+  unsigned long long l[NSLOT];
+#pragma unroll
+  for (int k = 0; k < NSLOT; ++k) {
+    h[k] = st[k * 256 + e];
+    l[k] = (unsigned long long)st[k * 256 + 128 + e];
+  }
+  long long hs = 0;
+  unsigned long long ls = 0;
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < NSLOT; ++k) {
+    hs += h[k];
+    ls += l[k];
+    bad |= h[k] >= FX_BAD || h[k] <= -FX_BAD;
+  }
+  return bad ? __builtin_nan("") : (double)hs + (double)ls * (1.0 / FX_ONE);
+}
+
+// channel c of a slotted accumulator: (sum, sum of squares) or (R1, R2)
+DEV void slot_sums(const long long* st, int c, double& s1, double& s2) {
+  s1 = fx_total(st, c);
+  s2 = fx_total(st, 64 + c);
+}
+
+// (no FMA contraction in the coefficient math: the backend's -ffp-contract=fast choices depend on
+// the surrounding kernel, and every kernel that rebuilds these coefficients must get the same bits)
+DEV void bn_mean_rstd(const long long* stat, int c, float inv_n, float& mean, float& rstd) {
+#pragma clang fp contract(off)
   double s1, s2;
   slot_sums(stat, c, s1, s2);
   const double m = s1 * (double)inv_n;
@@ -78,8 +124,9 @@ DEV void bn_mean_rstd(const double* stat, int c, float inv_n, float& mean, float
 }
 
 // BN backward: g_z = A*g_y + Bc*z + Cc  with  A = gamma*rstd, Bc = -gamma*rstd^2*R2/N, Cc = -A*R1/N - Bc*mean
-DEV void bnb_coeffs(const double* stat, const double* red, const float* gamma, int c, float inv_n, float& A,
+DEV void bnb_coeffs(const long long* stat, const long long* red, const float* gamma, int c, float inv_n, float& A,
                     float& Bc, float& Cc) {
+#pragma clang fp contract(off)
   float mean, rstd;
   bn_mean_rstd(stat, c, inv_n, mean, rstd);
   double r1, r2;
@@ -100,86 +147,11 @@ DEV uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint2, v).x;
 }
 
-// Deterministic slot flush: this block's 2 x C fp32 channel partials go to its row of the side buffer
-// `det` ([nblk][128] fp32, then DMLC_RN_DET_TICKETS uints) with device-coherent (sc1) stores; once
-// they are acknowledged the block takes a ticket of its group (blocks b with b & 7 == slot), and the
-// group's last arriver sums the group's rows in block order (fp64) into the slot with a plain store
-// -- the consumers run in later launches.  No fp64 atomics: the sums are bitwise reproducible (graph
-// replay == eager launches).  t1/t2 valid in threads tid < C; every thread of the block must call.
-template <int C>
-DEV void det_flush(float t1, float t2, double* dst, float* det, int nblk, int tid) {
-  __shared__ int flag[1];
-  const int b = blockIdx.x, slot = b & (NSLOT - 1);
-  if (tid < C) {
-    __hip_atomic_store(det + (size_t)b * 128 + tid, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(det + (size_t)b * 128 + 64 + tid, t2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0): this thread's partial stores acknowledged
-  __syncthreads();
-  if (tid == 0) {
-    unsigned* tk = reinterpret_cast<unsigned*>(det + (size_t)nblk * 128) + slot * 32;
-    const unsigned gsize = (unsigned)((nblk - slot + NSLOT - 1) / NSLOT);
-    const bool last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
-    if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
-    flag[0] = last ? 1 : 0;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  // the group's rows: T = 256 / (2C) threads per statistic (8 / 4 / 2 for 16 / 32 / 64 channels),
-  // thread h of a statistic sums rows h, h+T, ... in order, 8 loads in flight; the T partials are
-  // combined in fixed order through LDS.  At B = 256 (32 rows per group) that is ONE memory round
-  // trip for the 16- and 32-channel layers (two threads per statistic took two).
-  constexpr int NSTAT = 2 * C, T = 256 / NSTAT;
-  static_assert(256 % NSTAT == 0 && RT == 256, "det_flush: statistics must tile the 256 threads");
-  __shared__ double partT[256];
-  const int st = tid / T, h = tid - st * T;
-  const int e = st < C ? st : 64 + (st - C);          // row position of the statistic
-  const int rows = (nblk - slot + NSLOT - 1) / NSLOT;
-  // device-coherent (sc1) loads issued as one asm block (the compiler puts a vmcnt(0) behind every
-  // atomic load), rows past the group clamped to row 0 of the slot and weighted 0
-  double s = 0.0;
-  if (tid < 256) {
-    for (int r0 = h; r0 < rows; r0 += 8 * T) {
-      const float* p[8];
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = r0 + T * u < rows ? r0 + T * u : 0;
-        p[u] = det + (size_t)(slot + NSLOT * r) * 128 + e;
-      }
-      asm volatile(
-          "global_load_dword %0, %8, off sc1\n\t"
-          "global_load_dword %1, %9, off sc1\n\t"
-          "global_load_dword %2, %10, off sc1\n\t"
-          "global_load_dword %3, %11, off sc1\n\t"
-          "global_load_dword %4, %12, off sc1\n\t"
-          "global_load_dword %5, %13, off sc1\n\t"
-          "global_load_dword %6, %14, off sc1\n\t"
-          "global_load_dword %7, %15, off sc1\n\t"
-          "s_waitcnt vmcnt(0)"
-          : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
-          : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
-          : "memory");
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += r0 + T * u < rows ? (double)v[u] : 0.0;
-    }
-    partT[tid] = s;
-  }
-  __syncthreads();
-  if (tid < NSTAT) {
-    double acc = 0.0;
-#pragma unroll
-    for (int k = 0; k < T; ++k) acc += partT[tid * T + k];
-    dst[slot * 128 + (tid < C ? tid : 64 + tid - C)] = acc;
-  }
-}
-
-// block-level channel reduction of per-lane partials (lanes with equal li share a channel group) and
-// either the deterministic slot flush (det != null) or one fp64 atomic per channel into this block's
-// slot
+// block-level channel reduction of per-lane partials (lanes with equal li share a channel group), then
+// one fixed-point add per statistic into this block's slot
 template <int CT, int C>
-DEV void reduce_flush(float (&s1)[4], float (&s2)[4], float* red, double* dst, int w, int g, int li, int tid,
-                      float* det = nullptr, int nblk = 0) {
+DEV void reduce_flush(float (&s1)[4], float (&s2)[4], float* red, long long* dst, int w, int g, int li,
+                      int tid) {
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -199,14 +171,10 @@ DEV void reduce_flush(float (&s1)[4], float (&s2)[4], float* red, double* dst, i
     for (int ww = 0; ww < 4; ++ww)
       if (ww % CT == tid / 16) { t1 += red[(ww * 2) * 64 + tid]; t2 += red[(ww * 2 + 1) * 64 + tid]; }
   }
-  if (det) {
-    det_flush<C>(t1, t2, dst, det, nblk, tid);
-    return;
-  }
   if (tid < C) {
-    double* d = dst + (blockIdx.x & (NSLOT - 1)) * 128;
-    RN_ATOMIC_ADD(d + tid, (double)t1);
-    RN_ATOMIC_ADD(d + 64 + tid, (double)t2);
+    long long* d = dst + (blockIdx.x & (NSLOT - 1)) * 256;
+    fx_add(d, tid, t1);
+    fx_add(d, 64 + tid, t2);
   }
 }
 
@@ -364,7 +332,7 @@ __global__ __launch_bounds__(RT) void k_rn_fwd(DmlcRnFwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) { s1[r] = 0.f; s2[r] = 0.f; }
   }
-  reduce_flush<F::CT, COUT>(s1, s2, red, a.stat, w, g, li, tid, a.stat_det, a.B);
+  reduce_flush<F::CT, COUT>(s1, s2, red, a.stat, w, g, li, tid);
   if (TS) DMLC_STAMP(0, 5);                       // 5: statistics flushed (end)
 }
 
@@ -538,7 +506,7 @@ DEV void rn_dgrad_body(const DmlcRnDgradArgs& a) {   // workgroup blockIdx.x = i
     }
   }
   if (TS) DMLC_STAMP(1, 3);                       // 3: g_y stored, partial sums ready
-  reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid, a.red_det, a.B);
+  reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid);
   if (TS) DMLC_STAMP(1, 4);                       // 4: reductions flushed (end)
 }
 
@@ -948,7 +916,7 @@ __global__ __launch_bounds__(RT, 2) void k_rn_bwd_img(DmlcRnDgradArgs a, DmlcRnW
       for (int j = 0; j < EC; ++j) cur[j] = nxt[j];
     }
   }
-  reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid, a.red_det, a.B);
+  reduce_flush<D::CT, CIN>(s1, s2, red, a.red_prev, w, g, li, tid);
 
   // ---- weight gradient of this image: C[k = (tap, ci)][co] = sum_px X[px + tap][ci] g_z[px][co] ----
   // m-tile m: k = 16m .. 16m+15 = tap (16m) / CIN, channels (16m) % CIN .. +15 (taps past 8: K padding)
@@ -1121,14 +1089,10 @@ __global__ __launch_bounds__(RT) void k_rn_head(DmlcRnHeadArgs a) {
   __syncthreads();
   const float t1 = tid < 64 ? redl[0][0][tid] + redl[0][1][tid] + redl[0][2][tid] + redl[0][3][tid] : 0.f;
   const float t2 = tid < 64 ? redl[1][0][tid] + redl[1][1][tid] + redl[1][2][tid] + redl[1][3][tid] : 0.f;
-  if (a.red_det) {
-    det_flush<64>(t1, t2, a.red, a.red_det, a.B, tid);
-    return;
-  }
   if (tid < 64) {
-    double* d = a.red + (b & (NSLOT - 1)) * 128;
-    RN_ATOMIC_ADD(d + tid, (double)t1);
-    RN_ATOMIC_ADD(d + 64 + tid, (double)t2);
+    long long* d = a.red + (b & (NSLOT - 1)) * 256;
+    fx_add(d, tid, t1);
+    fx_add(d, 64 + tid, t2);
   }
 }
 
@@ -1237,14 +1201,11 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
     const bool act = c < a.cout[L];
     const int cc = act ? c : 0;
     const size_t og = (size_t)a.gamma_off[L] + cc, ob = (size_t)a.beta_off[L] + cc;
-    const double* rp = a.red + (size_t)L * NSLOT * 128;
-    const double* sp = a.stat + (size_t)L * NSLOT * 128;
-    double ra[NSLOT], rb[NSLOT], sa[NSLOT], sb[NSLOT];
-#pragma unroll
-    for (int k = 0; k < NSLOT; ++k) {
-      ra[k] = rp[k * 128 + cc]; rb[k] = rp[k * 128 + 64 + cc];
-      sa[k] = sp[k * 128 + cc]; sb[k] = sp[k * 128 + 64 + cc];
-    }
+    const long long* rp = a.red + (size_t)L * NSLOT * 256;
+    const long long* sp = a.stat + (size_t)L * NSLOT * 256;
+    // (fx_total issues its 16 loads before any arithmetic; the four totals are independent)
+    const double r1 = fx_total(rp, cc), r2 = fx_total(rp, 64 + cc);
+    const double s1 = fx_total(sp, cc), s2 = fx_total(sp, 64 + cc);
     float* mm = a.state + a.mm_off[L] + cc;
     float* mv = a.state + a.mv_off[L] + cc;
     // (a.grad exists only in the data-parallel modes 1/2; the running statistics are only updated
@@ -1256,9 +1217,6 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
     if (L == 0 && apply)
       for (int q = tid; q < a.B; q += RT) { lsv += a.loss_img[q]; csv += (float)a.correct_img[q]; }
     if (act) {
-      double r1 = 0.0, r2 = 0.0, s1 = 0.0, s2 = 0.0;    // same fixed slot order as slot_sums
-#pragma unroll
-      for (int k = 0; k < NSLOT; ++k) { r1 += ra[k]; r2 += rb[k]; s1 += sa[k]; s2 += sb[k]; }
       if (mode == 1) {
         a.grad[og] = (float)r2;
         a.grad[ob] = (float)r1;

@@ -72,6 +72,25 @@ def _kpd(cout):
     return (9 * cout + 31) // 32 * 32
 
 
+FX_ONE = float(2 ** 48)   # fraction unit of the fixed-point BN statistics (resnet.hip fx_add)
+
+
+def fx_encode(x: torch.Tensor):
+    """Host mirror of resnet.hip fx_add for finite |x| < 2^50: (integer part, 48-bit fraction)."""
+    x = x.double()
+    f = torch.floor(x)
+    return f.long(), torch.round((x - f) * FX_ONE).long()
+
+
+def fx_decode(slots: torch.Tensor) -> torch.Tensor:
+    """Totals of fixed-point statistic slots [..., NSLOT, 256] int64 -> fp64 [..., 128] (resnet.hip
+    fx_total; a slot at or beyond the poison bound 2^55 decodes to NaN)."""
+    hi, lo = slots[..., :128], slots[..., 128:]
+    bad = (hi.abs() >= 2 ** 55).any(-2)
+    tot = hi.sum(-2).double() + lo.sum(-2).double() / FX_ONE
+    return torch.where(bad, torch.full_like(tot, float("nan")), tot)
+
+
 def _block_sc_mode(b_layer: int) -> int:
     """Shortcut mode of the block whose second conv is ``b_layer`` (1 identity, 2 subsample+pad)."""
     a_layer = b_layer - 1
@@ -89,7 +108,7 @@ class FusedResNetEngine:
                  rank: int = 0, process_group=None, seed: int = 0, groups: Optional[List[int]] = None,
                  stats_len: int = 4096, comm_dtype: str = "fp32", wgrad_branch: Optional[bool] = None,
                  allreduce: str = "auto", capture_comm: Optional[bool] = None, dp_force: bool = False,
-                 deterministic: Optional[bool] = None, warmup_steps: int = 0,
+                 warmup_steps: int = 0,
                  merged_bwd: Optional[bool] = None, bwd_img_level: int = 1, sgd_split: bool = False):
         ops = _ops()
         self.ops = ops
@@ -162,18 +181,12 @@ class FusedResNetEngine:
         self.z = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout, LAYERS)]
         self.gy = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout, LAYERS)]
         self.a = [z(B, ho, ho, co) for ho, (_, _, co, _, _) in zip(hout[:-1], LAYERS[:-1])]   # a_0 .. a_17
-        # [stat | red] fp64 sums, NSLOT copies per layer (see csrc/kernels/resnet.hip)
-        self.acc = torch.zeros(2, NL, NSLOT, 128, dtype=torch.float64, device=dev)
+        # [stat | red] BatchNorm sums, NSLOT fixed-point copies per layer (resnet.hip fx_add): per statistic
+        # an int64 integer part [0, 128) and a 48-bit fraction [128, 256), added with 64-bit integer
+        # atomics -- order independent, so every step is bitwise reproducible (graph replay == eager);
+        # zeroed at the start of each forward
+        self.acc = torch.zeros(2, NL, NSLOT, 256, dtype=torch.int64, device=dev)
         self.stat, self.red = self.acc[0], self.acc[1]
-        # deterministic BN statistics (default): per-block fp32 partials + per-slot group tickets, the
-        # group's last block sums its partials in block order into the slot (resnet.hip det_flush) --
-        # bitwise reproducible, no per-step zeroing; deterministic=False: fp64 atomics
-        self.deterministic = True if deterministic is None else bool(deterministic)
-        self.det = (torch.zeros(2, NL, B * 128 + 8 * 32, dtype=torch.float32, device=dev)
-                    if self.deterministic else None)
-        det = (lambda k, l: self.det[k][l]) if self.deterministic else (lambda k, l: None)
-        self._det_stat = [det(0, l) for l in range(NL)]
-        self._det_red = [det(1, l) for l in range(NL)]
         # per-image backward (k_rn_bwd_img, merged backward only): bwd_img_level 0 off, 1 the 16->16
         # layers (their wgrad keeps one slab per image anyway), 2 also the 32->32 stride-1 layers (one
         # slab per image instead of B/2 groups: more slab bytes for the SGD, fewer re-reads)
@@ -246,18 +259,22 @@ class FusedResNetEngine:
         """This rank's rows of ``epoch`` (int32 [period * B]), the order the kernels generate."""
         return self.order.epoch_shard(epoch).to(torch.int32)
 
+    def bn_sums(self) -> torch.Tensor:
+        """Decoded BatchNorm sums of the last step, fp64 [2, NL, 128]: [0] sum z / sum z^2, [1] R1 / R2
+        (channels at [0, cout) and [64, 64 + cout))."""
+        return fx_decode(self.acc)
+
     def batch_indices(self, step: int) -> torch.Tensor:
         return self.order.batch(step).to(torch.int32)
 
     # --- kernels ------------------------------------------------------------------------------
     def _forward(self, idx, counter, period, logits_out=None):
         o = self.ops
-        if not self.deterministic:
-            self.acc.zero_()
+        self.acc.zero_()
         for l, (_, ci, co, h, s) in enumerate(LAYERS):
             if l == 0:
                 o.rn_fwd(ci, co, h, s, self.data, idx, counter, period, 0, 0, None, None, None, None, None, 0, None,
-                         self.wf[0], self.z[0], self.stat[0], self._det_stat[0], self.Bv)
+                         self.wf[0], self.z[0], self.stat[0], self.Bv)
                 continue
             p = l - 1
             sc_mode, sc_src = 0, None
@@ -265,10 +282,10 @@ class FusedResNetEngine:
                 sc_mode = _block_sc_mode(p)
                 sc_src = self.a[p - 2]
             o.rn_fwd(ci, co, h, s, None, None, None, 1, 0, 0, self.z[p], self.stat[p], self.gamma[p], self.beta[p],
-                     sc_src, sc_mode, self.a[p], self.wf[l], self.z[l], self.stat[l], self._det_stat[l], self.Bv)
+                     sc_src, sc_mode, self.a[p], self.wf[l], self.z[l], self.stat[l], self.Bv)
         o.rn_head(self.z[18], self.stat[18], self.gamma[18], self.beta[18], self.a[16], self.fcw, self.fcb,
                   self.labels, idx, counter, period, 1.0 / (self.Bv * self.world_size), self.gy[18], self.red[18],
-                  self.fc_part, self.loss_img, self.correct_img, logits_out, self._det_red[18], self.Bv,
+                  self.fc_part, self.loss_img, self.correct_img, logits_out, self.Bv,
                   self.step_t, self.step_sgd)
 
     def _per_image(self, l) -> bool:
@@ -303,7 +320,7 @@ class FusedResNetEngine:
                     gy_sc = self.gy[l + 1]
                 o.rn_bwd(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
                          self.a[l - 1], self.z[l - 1], self.stat[l - 1], gy_sc, sc_mode, self.gy[l - 1],
-                         self.red[l - 1], self.part[l], self._det_red[l - 1], self.Bv, self._per_image(l))
+                         self.red[l - 1], self.part[l], self.Bv, self._per_image(l))
                 if self.sgd_split and l in self._sgd_points:
                     # layers >= l: slabs complete, weights no longer read this step
                     self.side_stream.wait_stream(main)
@@ -329,7 +346,7 @@ class FusedResNetEngine:
                 gy_sc = self.gy[l + 1]
             o.rn_dgrad(ci, co, h, s, self.gy[l], self.z[l], self.stat[l], self.red[l], self.gamma[l], self.wd[l],
                        self.a[p], self.z[p], self.stat[p], gy_sc, sc_mode, self.gy[p], self.red[p],
-                       self._det_red[p], self.Bv)
+                       self.Bv)
         if side is not main:
             main.wait_stream(side)
 

@@ -151,13 +151,12 @@ def test_sgd_step_and_bn_running_stats():
 
 @pytest.mark.parametrize("B", [32, 256])
 def test_graph_replay_matches_eager_launches_bitwise(B):
-    """Deterministic BN statistics (per-slot group sums in block order, no fp64 atomics): chained graph
+    """Deterministic BN statistics (fixed-point slots added with integer atomics): chained graph
     replays == eager launches bit for bit -- weights, BN moving statistics and published losses --
     across 10 steps (SURVEY.md §5.2 determinism goal)."""
     data, labels = _data(8 * B, seed=7)
     e1 = FusedResNetEngine(B, data, labels, seed=6, lr=0.02)
     e2 = FusedResNetEngine(B, data, labels, seed=6, lr=0.02)
-    assert e1.deterministic and e2.deterministic
     e2.capture()
     for _ in range(10):
         e1.step()
@@ -169,19 +168,24 @@ def test_graph_replay_matches_eager_launches_bitwise(B):
     assert [e1.read_stats(k) for k in range(1, 11)] == [e2.read_stats(k) for k in range(1, 11)]
 
 
-def test_deterministic_stats_match_atomic_stats():
-    """The deterministic slot sums equal the fp64-atomic ones up to fp64 summation order."""
+def test_fixed_point_bn_sums_match_activations():
+    """The fixed-point slot totals (integer atomics, resnet.hip fx_add) equal an fp64 sum of the stored
+    pre-BN activations per channel, up to their bf16 rounding."""
     B = 64
     data, labels = _data(4 * B, seed=9)
-    det = FusedResNetEngine(B, data, labels, seed=8, deterministic=True)
-    ato = FusedResNetEngine(B, data, labels, seed=8, deterministic=False)
-    gd = det.compute_gradients().cpu().clone()
-    ga = ato.compute_gradients().cpu().clone()
+    eng = FusedResNetEngine(B, data, labels, seed=8)
+    eng.compute_gradients()
     torch.cuda.synchronize()
-    s_det = det.acc.sum(2)
-    s_ato = ato.acc.sum(2)
-    assert torch.allclose(s_det, s_ato, rtol=1e-9, atol=1e-12), float((s_det - s_ato).abs().max())
-    assert _rel(gd, ga) < 1e-4
+    sums = eng.bn_sums().cpu()
+    assert torch.isfinite(sums).all()
+    for l in (0, 7, 18):
+        z = eng.z[l].double().cpu()
+        co = z.shape[-1]
+        s1, s2 = z.sum((0, 1, 2)), (z * z).sum((0, 1, 2))
+        assert _rel(sums[0, l, :co], s1) < 2e-2, l
+        assert _rel(sums[0, l, 64:64 + co], s2) < 2e-2, l
+        if co < 64:
+            assert float(sums[0, l, co:64].abs().max()) == 0.0
 
 
 def test_short_training_reduces_loss():

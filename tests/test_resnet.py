@@ -125,3 +125,33 @@ def test_fused_resnet_layer_table_matches_model():
         for _, ci, co, _, _ in FR.LAYERS:
             g = FR.FusedResNetEngine._pick_groups(B, ci, co)
             assert 1 <= g <= B and g & (g - 1) == 0
+
+
+def test_fixed_point_bn_slots_are_order_independent():
+    """The fused engine's BatchNorm sums are fixed-point (resnet.hip fx_add / fx_total): integer part +
+    48-bit fraction per fp32 partial.  Any add order gives the same bits, the total matches an fp64 sum,
+    and a poisoned slot (non-finite partial) decodes to NaN.  Host mirror of the encoding."""
+    from dmlc.engine import fused_resnet as FR
+    g = torch.Generator().manual_seed(0)
+    parts = (torch.randn(256, 128, generator=g) * torch.logspace(-6, 4, 128)).float()   # one row per block
+    hi, lo = FR.fx_encode(parts)
+    assert int(lo.min()) >= 0 and int(lo.max()) <= 2 ** 48
+
+    def accumulate(order):
+        slots = torch.zeros(FR.NSLOT, 256, dtype=torch.int64)
+        for b in order.tolist():
+            slots[b % FR.NSLOT, :128] += hi[b]
+            slots[b % FR.NSLOT, 128:] += lo[b]
+        return slots
+
+    s1 = accumulate(torch.arange(256))
+    s2 = accumulate(torch.randperm(256, generator=g))
+    assert torch.equal(s1, s2)
+    tot = FR.fx_decode(s1)
+    ref = parts.double().sum(0)
+    # each add rounds its fraction to 2^-48 (error <= 2^-49): an absolute bound, far below the fp32
+    # partials' own relative rounding (2^-24)
+    assert bool(((tot - ref).abs() <= 256 * 2.0 ** -49 + 1e-13 * ref.abs()).all())
+    s1[3, 5] += 1 << 56                                      # a non-finite partial's poison
+    t = FR.fx_decode(s1)
+    assert torch.isnan(t[5]) and torch.isfinite(t[:5]).all()
