@@ -149,10 +149,15 @@ def select(numel: int, rank: int, world: int, device: torch.device, buckets: Lis
         if log:
             log(f"xgmi all-reduce unavailable ({info['xgmi_unavailable']}); using RCCL")
         return None, info
-    ok = 1.0 if ar.self_test() else 0.0
+    # (a first cross-GPU run is where a mapping problem would show: a raising self-test counts as a
+    # failed one, so every rank still agrees on RCCL instead of one rank leaving the collective)
+    try:
+        ok, why = (1.0 if ar.self_test() else 0.0), "self-test mismatch"
+    except Exception as e:                       # noqa: BLE001
+        ok, why = 0.0, f"self-test raised {type(e).__name__}: {e}"
     if _reduce(ok, dist.ReduceOp.MIN, bdev, group) < 1.0:
         ar.close()
-        info["xgmi_unavailable"] = "self-test mismatch"
+        info["xgmi_unavailable"] = why
         if log:
             log("xgmi all-reduce self-test failed; using RCCL")
         return None, info

@@ -61,6 +61,35 @@ def test_xgmi_selection_is_rccl_without_gpu():
     assert ar is None and info["allreduce"] == "rccl"
 
 
+def test_xgmi_selection_falls_back_when_self_test_raises(monkeypatch):
+    """A self-test that raises (a first cross-GPU mapping problem) selects RCCL on every rank instead
+    of leaving the collective (gloo world 1 stands in for the group; the IPC context is a stub)."""
+    import torch.distributed as dist
+    from dmlc.cli import free_port
+    from dmlc.parallel import xgmi
+
+    class Stub:
+        closed = False
+
+        def __init__(self, *a, **k):
+            pass
+
+        def self_test(self):
+            raise RuntimeError("hipErrorIllegalAddress")
+
+        def close(self):
+            Stub.closed = True
+
+    monkeypatch.setattr(xgmi, "XgmiAllReduce", Stub)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
+    try:
+        ar, info = xgmi.select(1024, 0, 2, torch.device("cuda", 0), [(0, 1024)])
+    finally:
+        dist.destroy_process_group()
+    assert ar is None and info["allreduce"] == "rccl" and Stub.closed
+    assert "self-test raised RuntimeError" in info["xgmi_unavailable"]
+
+
 def test_role_mapping():
     base = dict(ps_hosts="localhost:2222", worker_hosts="localhost:2223,localhost:2224,otherhost:2225")
     r = cli.resolve_role(TrainConfig(job_name="worker", task_index=1, **base), env={})
