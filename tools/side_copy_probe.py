@@ -18,6 +18,12 @@ where an fc-bucket exchange would run.  Variants:
   d2h         device -> pinned host (the SDMA engines: the CU-free path a graph's peer copies take);
               PCIe-bound, so its size is --d2h-mb (default 0.25 MB ~ 5 us of PCIe) -- it measures the
               interference of an SDMA stream with the step, not the link
+  kern        the same bytes moved by a PyTorch elementwise kernel (dst = src * 1, hundreds of
+              workgroups on the CUs) -- a kernel node instead of a memcpy node
+  xgmi8       the xGMI exchange kernel (xgmi_allreduce.hip) on a one-rank context over the bucket,
+              8 workgroups (one release/acquire pair each): the <= 8-workgroup P2P kernel of the
+              round-5 review, its fixed cost beside the wgrad launch
+  xgmi        the same with the launcher's default workgroup count
 Prints one JSON line per measurement and a summary with the per-step delta against ``none``."""
 import argparse
 import ctypes
@@ -59,8 +65,20 @@ class SideCopyEngine(FusedCifarEngine):
         elif mode == "d2h":
             rc = hip().hipHostMalloc(ctypes.byref(self.host), self.nbytes, 0)
             assert rc == 0, rc
+        elif mode == "kern":
+            self.dst = torch.empty_like(self.src)
+        elif mode.startswith("xgmi"):
+            from dmlc.parallel.xgmi import XgmiAllReduce
+            self.xg = XgmiAllReduce(n4, 0, 1)
+            self.xg.buf.normal_()
 
     def _copy(self):
+        if self.mode == "kern":
+            torch.mul(self.src, 1.0, out=self.dst)
+            return
+        if self.mode.startswith("xgmi"):
+            self.xg.all_reduce(0, self.xg.numel, blocks=8 if self.mode == "xgmi8" else 0)
+            return
         s = ctypes.c_void_p(self.side.cuda_stream)
         if self.mode == "d2d":
             rc = hip().hipMemcpyAsync(ctypes.c_void_p(self.dst.data_ptr()), ctypes.c_void_p(self.src.data_ptr()),
@@ -80,14 +98,19 @@ class SideCopyEngine(FusedCifarEngine):
         ev = torch.cuda.Event()
         ev.record(main)
         self.side.wait_event(ev)
-        if self.mode in ("d2d", "d2h"):
-            self._copy()
+        if self.mode != "fork":
+            with torch.cuda.stream(self.side):
+                self._copy()
         done = torch.cuda.Event()
         done.record(self.side)
         self._conv_backward(apply=True)
         self._pending_comm = done
 
     def close(self):
+        if getattr(self, "xg", None) is not None:
+            self.xg.check()
+            self.xg.close()
+            self.xg = None
         if self.host.value:
             hip().hipHostFree(self.host)
             self.host = ctypes.c_void_p()
@@ -100,7 +123,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--mb", type=float, default=3.84)
     ap.add_argument("--d2h-mb", type=float, default=0.25)
-    ap.add_argument("--variants", default="none,fork,d2d,d2h")
+    ap.add_argument("--variants", default="none,fork,d2d,d2h,kern,xgmi8,xgmi")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     g = torch.Generator().manual_seed(0)
@@ -124,7 +147,7 @@ def main():
             eng.check_barriers()
             assert torch.isfinite(eng.master).all()
             best[name] = min(best.get(name, 1e30), us)
-            print(json.dumps({"variant": name, "round": r, "bytes": nb if name in ("d2d", "d2h") else 0,
+            print(json.dumps({"variant": name, "round": r, "bytes": nb if name != "none" and name != "fork" else 0,
                               "us_per_step": round(us, 2)}), flush=True)
             eng.close()
             del eng
