@@ -1134,6 +1134,8 @@ __global__ __launch_bounds__(RT) void k_rn_sgd(DmlcRnSgdArgs a) {
   const bool reduce = mode <= 1, apply = mode == 0 || mode == 2;
   const int blk = blockIdx.x, tid = threadIdx.x;
   constexpr int NL = DMLC_RN_LAYERS;
+  // (the BN blocks dispatched first instead of last measured no better: 612.0-612.9 vs 608.4-611.3
+  // us/step, profiles/r6s3_rn_sgd_bn_first_ab.txt -- they are not the launch's tail)
   // block role: every range start compared at once (21 independent kernarg loads, one latency; the
   // search loop paid one dependent scalar load per range -- ~20 in a row for the BN blocks)
   int l = 0;
