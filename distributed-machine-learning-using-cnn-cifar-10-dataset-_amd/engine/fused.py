@@ -56,6 +56,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import config as C
+from ..parallel.dist import quiesce_for_capture
 from ..data.order import OrderSpec
 from ..models import cifar_cnn as M
 from ..ops import _ext
@@ -192,7 +193,8 @@ class FusedCifarEngine:
             pattern = ([(0, self.master.numel())] if dp_schedule == "serial"
                        else [self._buckets[True], self._buckets[False]])
             self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev, pattern,
-                                                 mode=allreduce, group=process_group, wire=comm_dtype)
+                                                 mode=allreduce, group=process_group, wire=comm_dtype,
+                                                 captured=self.capture_comm)
         elif dp_force and world_size == 1 and allreduce == "xgmi" and dev.type == "cuda":
             # a one-rank xGMI context (no peers): the DP step's exchange kernel on a single GPU
             from ..parallel import xgmi as X
@@ -880,7 +882,7 @@ class FusedCifarEngine:
         steps need no host work, across epoch boundaries too).  :meth:`run` replays any step count
         as a sum of chains -- no single-step tails, no host gap between the chained steps.
         RCCL without ``capture_comm``: compute graphs around eager collectives (no chains)."""
-        torch.cuda.synchronize(self.device)
+        quiesce_for_capture(self.device, self.pg if self.dp else None)
         self._reset_step_state()
         self.graphs, self.chains = [], {}
         pool = torch.cuda.graph_pool_handle()
@@ -911,6 +913,7 @@ class FusedCifarEngine:
         k = int(k)
         if not self.single_graph or not self.graphs or k < 2 or self.chains.get(k) is not None:
             return False
+        quiesce_for_capture(self.device, self.pg if self.dp else None)
         self.chains[k] = self._capture_one(lambda: self._steps_joined(k), self._pool)
         torch.cuda.synchronize(self.device)
         return True

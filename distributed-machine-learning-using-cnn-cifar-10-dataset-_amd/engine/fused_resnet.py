@@ -27,6 +27,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import config as C
+from ..parallel.dist import quiesce_for_capture
 from ..data.order import OrderSpec
 from ..models import resnet as R
 from ..ops import _ext
@@ -154,7 +155,7 @@ class FusedResNetEngine:
             from ..parallel import xgmi as X
             self.xgmi, self.comm_info = X.select(self.master.numel(), rank, world_size, dev,
                                                  [(0, self.master.numel())], mode=allreduce, group=process_group,
-                                                 wire=comm_dtype)
+                                                 wire=comm_dtype, captured=self.capture_comm)
         if self.xgmi is not None:
             self.grad = self.xgmi.buf[:self.master.numel()]
             self.grad.zero_()
@@ -436,7 +437,7 @@ class FusedResNetEngine:
         """The whole step as one graph (N=1, xGMI, or RCCL with ``capture_comm``) plus chains of
         2, 4, ... ``steps_per_graph`` steps for :meth:`run`; RCCL without ``capture_comm``: compute
         and apply graphs around an eager all-reduce."""
-        torch.cuda.synchronize(self.device)
+        quiesce_for_capture(self.device, self.pg if self.dp else None)
         self.graphs, self.chains = [], {}
         pool = torch.cuda.graph_pool_handle()
         segs = [self._eager_step] if self.single_graph else [self._seg_compute, self._seg_apply]

@@ -171,3 +171,21 @@ def shutdown(info: DistInfo):
     if info.initialized and dist.is_initialized():
         dist.destroy_process_group()
         info.initialized = False
+
+
+# ProcessGroupNCCL's watchdog thread wakes every ~100 ms and queries the end event of every eager
+# collective it still tracks.  Those events live on the group's internal stream, which a captured
+# collective joins into the capture; a query landing while a HIP graph capture is open fails with
+# hipErrorCapturedEvent and terminates the watchdog -- and the process (seen once on a 1-rank nccl
+# group: tests/test_fused_dp_gpu.py, rccl bf16-wire test).  Completed work leaves the list on the
+# watchdog's next pass, so a capture that follows eager collectives first lets it drain.
+WATCHDOG_DRAIN_S = 0.35
+
+
+def quiesce_for_capture(device, group=None) -> None:
+    """Call before a graph capture that may follow eager RCCL collectives (a no-op sleep-free
+    synchronise on any other backend / without a process group)."""
+    if device is not None and torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+    if dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl":
+        time.sleep(WATCHDOG_DRAIN_S)

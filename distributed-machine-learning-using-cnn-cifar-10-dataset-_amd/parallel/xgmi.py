@@ -113,6 +113,26 @@ def _reduce(v: float, op, device, group=None) -> float:
     return float(t.item())
 
 
+def _capture(fn, device, group=None) -> Optional["torch.cuda.CUDAGraph"]:
+    """``fn``'s launches as a HIP graph, or None if the capture fails (nothing runs while capturing).
+    thread_local: the process group's watchdog thread may poll events meanwhile (engine/fused.py)."""
+    try:
+        from .dist import quiesce_for_capture
+        quiesce_for_capture(device, group)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                fn()
+        torch.cuda.current_stream(device).wait_stream(s)
+        torch.cuda.synchronize(device)
+        return g
+    except Exception:                            # noqa: BLE001 -- eager timing instead
+        torch.cuda.synchronize(device)
+        return None
+
+
 def _time(fn, iters: int, device) -> float:
     for _ in range(3):
         fn()
@@ -125,12 +145,14 @@ def _time(fn, iters: int, device) -> float:
 
 
 def select(numel: int, rank: int, world: int, device: torch.device, buckets: List[Tuple[int, int]],
-           mode: str = "auto", group=None, log=None, wire: str = "fp32") -> Tuple[Optional[XgmiAllReduce], Dict]:
+           mode: str = "auto", group=None, log=None, wire: str = "fp32",
+           captured: bool = False) -> Tuple[Optional[XgmiAllReduce], Dict]:
     """Collective choice of the gradient all-reduce.  Returns (XgmiAllReduce | None, info).
 
     mode "rccl": never xGMI.  "xgmi": xGMI unless it cannot work (then RCCL).  "auto": like "xgmi",
     and over RCCL additionally only if measured faster than RCCL on ``buckets`` ((offset, numel)),
-    RCCL moving the same wire dtype."""
+    RCCL moving the same wire dtype.  ``captured``: the step graph will hold the collective, so both
+    are timed as graph replays (eagerly if either capture fails on any rank)."""
     info: Dict = {"allreduce": "rccl"}
     if mode == "rccl" or world == 1 or device.type != "cuda":
         return None, info
@@ -172,11 +194,24 @@ def select(numel: int, rank: int, world: int, device: torch.device, buckets: Lis
             for off, n in buckets:
                 dist.all_reduce(scratch[off:off + n], group=group)
 
-        tx = _reduce(_time(run_x, 20, device), dist.ReduceOp.MAX, bdev, group)
-        tr = _reduce(_time(run_r, 20, device), dist.ReduceOp.MAX, bdev, group)
+        # captured (the step graph holds the collective): time both as graph replays -- a collective
+        # that brings cross-queue dependencies into a graph pays them there and not eagerly (one graph
+        # branch node costs ~20 us per step here, profiles/r6s3_side_copy_probe.jsonl).  Capturing runs
+        # no collective, so every rank first agrees that both captures worked, else all time eagerly.
+        gx = gr = None
+        if captured:
+            gx, gr = _capture(run_x, device, group), _capture(run_r, device, group)
+        both = _reduce(1.0 if gx is not None and gr is not None else 0.0, dist.ReduceOp.MIN, bdev, group) >= 1.0
+        if both:
+            fx, fr = gx.replay, gr.replay
+        else:
+            fx, fr = run_x, run_r
+        tx = _reduce(_time(fx, 20, device), dist.ReduceOp.MAX, bdev, group)
+        tr = _reduce(_time(fr, 20, device), dist.ReduceOp.MAX, bdev, group)
+        del gx, gr
         ar.buf.zero_()
         torch.cuda.synchronize(device)
-        info.update(xgmi_us=round(tx * 1e6, 1), rccl_us=round(tr * 1e6, 1))
+        info.update(xgmi_us=round(tx * 1e6, 1), rccl_us=round(tr * 1e6, 1), timed="graph" if both else "eager")
         if not tx < tr:
             ar.close()
             return None, info

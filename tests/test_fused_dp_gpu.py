@@ -3,6 +3,7 @@ vs a single-process fused run on the union batch.  Two ranks share the one GPU o
 talk over gloo (which all-reduces GPU tensors through the host); on an 8-GPU node the same code
 path runs over RCCL.  allreduce="xgmi" runs the IPC peer-to-peer all-reduce kernel instead
 (parallel/xgmi.py; the two ranks map each other's gradient buffer on the shared GPU).  SURVEY.md §2.D / §4 'Distributed'."""
+import json
 import os
 import sys
 
@@ -474,3 +475,44 @@ def test_rccl_bf16_wire_grad16_equals_cast_path(tmp_path, B):
         # the overlap schedule's conv bucket crosses as bf16 too when grad16 holds it (without grad16
         # it goes fp32, fused.py _allreduce_bucket): the same weights as the serial step
         assert torch.equal(r["overlap-1"][k], a[k]), k
+
+
+def _select_rank(rank, world, port, out):
+    sys.path.insert(0, REPO)
+    import datetime
+    import torch.distributed as dist
+    import dmlc  # noqa: F401
+    from dmlc.parallel import xgmi as X
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60), device_id=torch.device("cuda", 0))
+    real = X.XgmiAllReduce
+    # select() at world 2 over a 1-rank nccl group, the IPC context built at world 1 (one GPU): the
+    # captured-timing path (both collectives captured, agreed, replayed) runs for real
+    X.XgmiAllReduce = lambda numel, r, w, group=None, wire="fp32": real(numel, 0, 1, None, wire=wire)
+    res = {}
+    for captured in (True, False):
+        ar, info = X.select(1 << 20, 0, 2, torch.device("cuda", 0), [(0, 1 << 20)], mode="auto",
+                            wire="bf16", captured=captured)
+        res[str(captured)] = dict(info)
+        if ar is not None:
+            ar.close()
+    torch.save(res, os.path.join(out, "select.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_select_times_captured_collectives_as_graph_replays(tmp_path):
+    """The xGMI-vs-RCCL choice of a job whose step graph holds the collective times both as graph
+    replays (a collective that adds cross-queue dependencies pays them only when captured), and
+    falls back to eager timing otherwise; both choices report their timings."""
+    import torch.multiprocessing as mp
+    from dmlc.cli import free_port
+    mp.spawn(_select_rank, args=(1, free_port(), str(tmp_path)), nprocs=1, join=True)
+    res = torch.load(tmp_path / "select.pt", weights_only=True)
+    print(json.dumps(res))
+    assert res["True"]["timed"] == "graph", res
+    assert res["False"]["timed"] == "eager", res
+    for info in res.values():
+        assert info["xgmi_us"] > 0 and info["rccl_us"] > 0, info
+        assert info["allreduce"] in ("xgmi", "rccl") and "xgmi_unavailable" not in info, info
