@@ -36,6 +36,11 @@ constexpr int RT = 256;
 // streaming (nt) stores for the activations / gradients / slabs the next launches read (common.h:
 // fewer dirty L2 lines to write back at every one of the ~58 kernel boundaries): 0.695 -> 0.682 ms
 constexpr bool kNtRn = kNtDefault;
+#ifdef DMLC_RN_SLAB_PLAIN   // A/B build, slabs stored plain: 640.4-641.5 vs 611.7-611.9 us (r6s3_rn_slab_plain_ab.txt)
+constexpr bool kNtSlab = false;
+#else
+constexpr bool kNtSlab = kNtRn;
+#endif
 // activation stores (z, a, g_y -> the next launch): write-through (common.h st_out16 / st_out8) unless
 // -DDMLC_RN_NT (the r3 streaming form); the fp32 slabs stay streaming (their 4-B write-through
 // stores are one fabric write each: 375 vs 401 k images/s, r5 same-box A/B)
@@ -704,7 +709,7 @@ DEV void rn_wgrad_body(const DmlcRnWgradArgs& a, const int grp, const int mc) {
 #pragma unroll
       for (int n = 0; n < NT; ++n)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) st_maybe_nt<kNtRn>(out + (16 * m + 4 * g + i) * COUT + 16 * n + li, acc[j][n][i]);
+        for (int i = 0; i < 4; ++i) st_maybe_nt<kNtSlab>(out + (16 * m + 4 * g + i) * COUT + 16 * n + li, acc[j][n][i]);
     }
   }
   if (TS) DMLC_STAMP(2, 3);                       // 3: slab written (end)
@@ -973,7 +978,7 @@ __global__ __launch_bounds__(RT, 2) void k_rn_bwd_img(DmlcRnDgradArgs a, DmlcRnW
 #pragma unroll
       for (int n = 0; n < I::NT; ++n)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) st_maybe_nt<kNtRn>(out + (16 * m + 4 * g + i) * COUT + 16 * n + li, wacc[j][n][i]);
+        for (int i = 0; i < 4; ++i) st_maybe_nt<kNtSlab>(out + (16 * m + 4 * g + i) * COUT + 16 * n + li, wacc[j][n][i]);
     }
   }
 }
